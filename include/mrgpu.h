@@ -1,0 +1,157 @@
+/*
+ * mrgpu.h -- C ABI of libmrgpu.so, the MI355X (gfx950) engine for the Freebirdgo/MapReduce_Rust
+ * worker data path: map -> SipHash partition -> (shuffle) -> sort -> group/reduce -> mr-{r}.txt.
+ *
+ * Plain pointers and sizes only.  Every call returns MRG_OK (0) or a negative MRG_E* code and never
+ * aborts across the ABI; mrg_last_error() gives a thread-local message for the last failure.
+ * Device pointers ("d_") are HIP device allocations on the context's device; host pointers ("h_").
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference repo root):
+ *   mrg_map        call_map_func(Box::new(wc::map), &contents)      src/mr/worker.rs:16-18, 147-150
+ *                  + cal_hash_for_key / index = h % reduce_n        src/mr/worker.rs:111-115, 129
+ *                  + write_key_value_to_file (partitioned output)   src/mr/worker.rs:117-140
+ *                  wc::map                                          src/app/wc.rs:6-13
+ *   mrg_reduce     read_file_to_mem_reduce + sort + group loop      src/mr/worker.rs:79-109, 157-193
+ *                  call_reduce_func(Box::new(wc::reduce), ...)      src/mr/worker.rs:20-25, 174-178
+ *                  wc::reduce                                       src/app/wc.rs:15-17
+ *   mrg_run_job    the whole mrcoordinator + N x mrworker run       src/bin/mrworker.rs:43-149,
+ *                  (static plan instead of coordinator.rs:137-215 task assignment)
+ *   mrg_job_*      the same path with device-resident input, split at the shuffle so that a
+ *                  multi-GPU host can exchange partitions between GPUs (RCCL all-to-all).
+ */
+#ifndef MRGPU_H
+#define MRGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define MRG_OK 0
+#define MRG_EINVAL (-1)   /* bad argument / state (reference: assert! failures, worker.rs:130,143-160) */
+#define MRG_EUTF8 (-2)    /* input is not UTF-8 (reference: read_to_string().unwrap() panics, worker.rs:75) */
+#define MRG_EHIP (-3)     /* HIP runtime error */
+#define MRG_ENOMEM (-4)   /* device or host allocation failed */
+#define MRG_EIO (-5)      /* file open/read/write failed (reference: unwrap/`?` on fs ops, worker.rs:73,122,168) */
+
+/* ---- apps (the reference selects wc at compile time, worker.rs:5,148,175) ---- */
+#define MRG_APP_WC 0       /* src/app/wc.rs */
+#define MRG_APP_INDEXER 1  /* build-defined (no indexer in the reference): word -> "n doc1,doc2,..." */
+
+/* ---- flags ---- */
+#define MRG_FLAG_NO_COMPAT_DROP_LAST 0x1u  /* default (flag clear): reproduce worker.rs:169-184, which never
+                                              writes the last group of a partition.  Set: write it. */
+/* bits 8..15: truncate every internal (non-partition) hash to this many bits; 0 = full 64 bits.
+   A test knob that forces hash collisions so the full-string tie-break paths are exercised. */
+#define MRG_FLAG_DEBUG_HASH_BITS(n) (((uint32_t)(n) & 0xFFu) << 8)
+
+/* Exchange record (mrg_job_export / mrg_job_import / mrg_parts): 40 bytes, little-endian.
+ *   u64 k0, k1   first 16 key bytes, big-endian packed, zero padded (keys never contain NUL)
+ *   u64 count    occurrences (wc) / 1 (indexer)
+ *   u32 doc      global document id (indexer), 0xFFFFFFFF for wc
+ *   u32 len      key length in bytes
+ *   u64 heap     byte offset of the full key in the heap buffer if len > 16, else ~0
+ * The heap holds the bytes of keys longer than 16 bytes. */
+#define MRG_XREC_BYTES 40
+
+typedef struct mrg_ctx mrg_ctx;
+typedef struct mrg_parts mrg_parts;
+
+typedef struct {
+    uint64_t input_bytes;      /* bytes mapped */
+    uint64_t tokens;           /* tokens produced by the tokenizer */
+    uint64_t long_tokens;      /* tokens longer than 16 bytes (slow path) */
+    uint64_t map_records;      /* records leaving the map kernel (LDS-combine misses + flush) */
+    uint64_t distinct_keys;    /* keys after aggregation (wc: words; indexer: (word, doc) pairs) */
+    uint64_t output_bytes;     /* bytes of all mr-{r}.txt */
+    double ms_map;             /* map kernel (tokenize + LDS combine), last call, HIP events */
+    double ms_aggregate;       /* global aggregation + partition hash */
+    double ms_sort;            /* radix sort */
+    double ms_format;          /* output formatting */
+    uint32_t map_launches;     /* map kernel launches in the last mrg_job_map */
+    uint32_t reserved;
+} mrg_stats;
+
+const char *mrg_last_error(void);
+const char *mrg_version(void);
+
+/* One context per thread and device.  Owns a HIP stream (or uses one set by mrg_set_stream) and all
+ * device workspaces, which grow on demand and are reused across jobs. */
+int mrg_open(int device, mrg_ctx **out);
+int mrg_close(mrg_ctx *ctx);
+/* Run every kernel of this context on `hip_stream` (a hipStream_t; NULL = the context's own). */
+int mrg_set_stream(mrg_ctx *ctx, void *hip_stream);
+int mrg_get_stats(mrg_ctx *ctx, mrg_stats *out);
+/* Per-stage HIP-event timing (mrg_stats.ms_*); off by default (it adds events to the stream). */
+int mrg_set_timing(mrg_ctx *ctx, int enable);
+
+/* ---- device-resident job (bench, multi-GPU) ---- */
+
+/* Start a job.  n_reduce = nReduce (worker.rs:129).  Clears previous job state. */
+int mrg_job_begin(mrg_ctx *ctx, int app, uint32_t n_reduce, uint32_t flags);
+/* Document names, indexed by global document id (indexer output; ignored by wc).  Every rank of a
+ * multi-GPU job passes the full table.  Names must not contain ' ', ',' or '\n'. */
+int mrg_job_set_doc_names(mrg_ctx *ctx, const char *const *names, uint32_t n_names);
+/* Input: documents laid out back to back in ONE device buffer d_bytes (16-byte aligned);
+ * document i is d_bytes[h_doc_off[i] .. h_doc_off[i+1]) with global id h_doc_ids[i] (NULL: i).
+ * The buffer is borrowed until the next mrg_job_begin. */
+int mrg_job_set_input(mrg_ctx *ctx, const uint8_t *d_bytes, const uint64_t *h_doc_off, uint32_t n_docs,
+                      const uint32_t *h_doc_ids);
+/* Map: tokenize (wc.rs:6-13) + combine + SipHash partition (worker.rs:111-115).  Validates UTF-8. */
+int mrg_job_map(mrg_ctx *ctx);
+/* Shuffle boundary.  Owner of partition r is r % n_owners.  Sizes first (host arrays of n_owners),
+ * then pack into caller device buffers ordered by owner (records, then heap bytes). */
+int mrg_job_export_sizes(mrg_ctx *ctx, uint32_t n_owners, uint64_t *h_rec_counts, uint64_t *h_heap_bytes);
+int mrg_job_export(mrg_ctx *ctx, void *d_rec, void *d_heap);
+/* Replace the job's keys by the aggregation of received exchange records: the concatenation of
+ * n_segs senders' exports, sender i contributing h_seg_recs[i] records and h_seg_heap[i] heap bytes
+ * (record heap offsets are relative to their sender's heap segment).  n_segs = 0: one segment. */
+int mrg_job_import(mrg_ctx *ctx, const void *d_rec, uint64_t n_rec, const void *d_heap, uint64_t heap_bytes,
+                   const uint64_t *h_seg_recs, const uint64_t *h_seg_heap, uint32_t n_segs);
+/* Reduce: sort (byte order, worker.rs:162-164), group, reduce, format every owned partition.
+ * *h_out_bytes = total bytes of the mr-{r}.txt contents (concatenated in r order). */
+int mrg_job_reduce(mrg_ctx *ctx, uint64_t *h_out_bytes);
+/* Device pointer to the output and the byte offset of each partition (h_part_off[n_reduce + 1]). */
+int mrg_job_output(mrg_ctx *ctx, const uint8_t **d_out, uint64_t *h_part_off);
+/* Copy the output to host memory (h_dst of at least *h_out_bytes). */
+int mrg_job_copy_output(mrg_ctx *ctx, uint8_t *h_dst, uint64_t cap);
+
+/* ---- plugin-surface equivalents, host buffers (one map task / one reduce task) ---- */
+
+/* One map task over one input file's bytes: wc.rs:6-13 + worker.rs:117-140, combined per
+ * partition.  doc = the document name (indexer value); doc_id its global id. */
+int mrg_map(mrg_ctx *ctx, int app, const uint8_t *h_bytes, size_t n, const char *doc, uint32_t doc_id,
+            uint32_t n_reduce, uint32_t flags, mrg_parts **out);
+/* Records of partition r of a map output (exchange-record format above). */
+int mrg_parts_get(const mrg_parts *parts, uint32_t r, const uint8_t **h_rec, uint64_t *n_rec,
+                  const uint8_t **h_heap, uint64_t *heap_bytes);
+void mrg_parts_free(mrg_parts *parts);
+/* One reduce task: partition r of k map outputs -> exact bytes of mr-{r}.txt (worker.rs:157-193).
+ * For the indexer, doc_names[id] names global document id (n_docs entries). */
+int mrg_reduce(mrg_ctx *ctx, int app, uint32_t r, const mrg_parts *const *in, size_t k, uint32_t n_reduce,
+               uint32_t flags, const char *const *doc_names, uint32_t n_docs, uint8_t **h_out, size_t *h_out_len);
+
+/* The whole job on one GPU: files are read, mapped, reduced; out_dir/mr-{r}.txt written.
+ * Indexer document names are the file paths as given (the reference opens "data/gut-{m}.txt"). */
+int mrg_run_job(const char *const *files, size_t n_files, uint32_t n_reduce, int app, const char *out_dir,
+                uint32_t flags, int device);
+
+/* Free host memory returned by the library (mrg_reduce output). */
+void mrg_free(void *p);
+
+/* ---- synthetic inputs for the benchmark (not on the data path) ---- */
+
+/* Zipf(s) text over a vocabulary of `vocab` distinct lowercase words (BASELINE config C3/C4),
+ * written to d_dst[0 .. n_bytes).  Deterministic in (seed, file_index); see DESIGN.md. */
+int mrg_gen_zipf(mrg_ctx *ctx, uint8_t *d_dst, uint64_t n_bytes, uint64_t seed, uint64_t file_index,
+                 uint32_t vocab, double s);
+/* Near-unique 12-character keys (BASELINE config C5): token i of file f, 1% repeats. */
+int mrg_gen_unique(mrg_ctx *ctx, uint8_t *d_dst, uint64_t n_bytes, uint64_t seed, uint64_t file_index);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MRGPU_H */

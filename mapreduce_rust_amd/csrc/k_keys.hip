@@ -1,0 +1,283 @@
+// k_keys.hip -- global aggregation of map records, long-key tie-break grouping, partitioning and
+// the shuffle pack (gfx950).
+//
+// Global table: the reduce side's "group equal keys" (src/mr/worker.rs:165-184) done by hashing
+// instead of sorting every record: records from all map workgroups are summed per exact key in an
+// HBM open-addressing table with the same monotone claim protocol as the LDS table (k_map.hip):
+// device-scope 64-bit CAS per key word, so the table is exact without locks.  Every distinct key
+// then gets its partition SipHash-1-3(key ++ 0xFF) % nReduce (worker.rs:111-115, 129) -- once per
+// key, not per token.
+#include "mrg_device.h"
+#include "mrg_internal.h"
+
+namespace {
+
+inline dim3 grid_for(uint64_t n, int b = 256) { return dim3((unsigned)((n + b - 1) / b)); }
+
+__global__ void k_table_clear(TableArgs T, bool idx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= T.cap) return;
+    T.tk0[i] = MRG_EMPTY_K0;
+    T.tk1[i] = MRG_EMPTY_K1;
+    T.tcnt[i] = 0;
+    if (idx) T.tdoc[i] = MRG_EMPTY_DOC;
+}
+
+__device__ __forceinline__ void table_add(const TableArgs &T, uint64_t a, uint64_t b, uint32_t d, uint64_t c,
+                                          bool idx) {
+    uint64_t h = mrg_key_mix(a, b, d);
+    if (T.hash_bits) h &= (1ull << T.hash_bits) - 1u;
+    uint64_t slot = (h ^ (h >> 31)) & (T.cap - 1);
+    for (uint64_t probe = 0; probe < T.cap; ++probe) {
+        const unsigned long long x =
+            atomicCAS((unsigned long long *)&T.tk0[slot], MRG_EMPTY_K0, (unsigned long long)a);
+        if (x == MRG_EMPTY_K0 || x == a) {
+            const unsigned long long y =
+                atomicCAS((unsigned long long *)&T.tk1[slot], MRG_EMPTY_K1, (unsigned long long)b);
+            if (y == MRG_EMPTY_K1 || y == b) {
+                bool ok = true;
+                if (idx) {
+                    const unsigned int z = atomicCAS(&T.tdoc[slot], MRG_EMPTY_DOC, d);
+                    ok = (z == MRG_EMPTY_DOC || z == d);
+                }
+                if (ok) {
+                    atomicAdd((unsigned long long *)&T.tcnt[slot], (unsigned long long)c);
+                    return;
+                }
+            }
+        }
+        slot = (slot + 1u) & (T.cap - 1);
+    }
+}
+
+__global__ void k_table_insert(TableArgs T, const uint64_t *k0, const uint64_t *k1, const uint32_t *cnt,
+                               const uint32_t *doc, uint64_t n, bool idx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    table_add(T, k0[i], k1[i], idx ? doc[i] : MRG_EMPTY_DOC, cnt[i], idx);
+}
+
+__global__ void k_table_insert_x(TableArgs T, const XRec *x, uint64_t n, bool idx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const XRec r = x[i];
+    if (r.len > 16u) return;  // long keys take the fingerprint-sort path
+    table_add(T, r.k0, r.k1, idx ? r.doc : MRG_EMPTY_DOC, r.cnt, idx);
+}
+
+__global__ void k_table_compact(TableArgs T, bool idx, KeySet out, unsigned long long *counter) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool full = i < T.cap && T.tk0[i] != MRG_EMPTY_K0;
+    const uint64_t j = mrg_wave_append(counter, full);
+    if (!full) return;
+    const uint64_t a = T.tk0[i], b = T.tk1[i];
+    out.k0[j] = a;
+    out.k1[j] = b;
+    out.cnt[j] = T.tcnt[i];
+    out.doc[j] = idx ? T.tdoc[i] : MRG_EMPTY_DOC;
+    out.len[j] = mrg_short_len(a, b);
+    out.hoff[j] = MRG_NO_HEAP;
+}
+
+// worker.rs:129  index = (DefaultHasher(key) % reduce_n as u64) as i32
+__global__ void k_partition(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t n_reduce) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t L = ks.len[i];
+    const uint64_t h = L <= 16u ? mrg_siphash_short(ks.k0[i], ks.k1[i], L) : mrg_siphash_bytes(heap + ks.hoff[i], L);
+    ks.part[i] = (uint32_t)(h % (uint64_t)n_reduce);
+}
+
+// Long keys after the fingerprint sort: element i (sorted order) belongs to the run of equal
+// fingerprints; within the run its representative is the FIRST element with equal full key bytes
+// (and doc): the collision-safe tie-break, equal fingerprints never merge different strings.
+__global__ void k_long_group(const uint64_t *fp, const uint32_t *idx, const uint32_t *doc, const uint8_t *heap,
+                             const uint64_t *hoff, const uint32_t *flen, uint64_t n, uint32_t *rep) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t me = idx[i];
+    const uint64_t f = fp[i];
+    uint64_t g = 0, hi = i;  // first index of the run of fingerprint f
+    while (g < hi) {
+        const uint64_t mid = (g + hi) >> 1;
+        if (fp[mid] < f) g = mid + 1; else hi = mid;
+    }
+    uint32_t r = me;
+    const uint8_t *mk = heap + hoff[me];
+    const uint32_t ml = flen[me];
+    for (uint64_t j = g; j < i; ++j) {
+        const uint32_t o = idx[j];
+        if (flen[o] != ml || (doc && doc[o] != doc[me])) continue;
+        const uint8_t *ok = heap + hoff[o];
+        bool eq = true;
+        for (uint32_t b = 0; b < ml && eq; ++b) eq = mk[b] == ok[b];
+        if (eq) { r = o; break; }
+    }
+    rep[me] = r;
+}
+
+__global__ void k_long_count(const uint32_t *rep, const uint64_t *cnt_in, uint64_t n, unsigned long long *acc) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    atomicAdd(&acc[rep[i]], (unsigned long long)(cnt_in ? cnt_in[i] : 1u));
+}
+
+__global__ void k_long_emit(const uint32_t *rep, const uint64_t *k0, const uint64_t *k1, const uint32_t *flen,
+                            const uint64_t *hoff, const uint32_t *doc, uint64_t n, const unsigned long long *acc,
+                            KeySet out, unsigned long long *counter, bool idx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool mine = i < n && rep[i] == (uint32_t)i;
+    const uint64_t j = mrg_wave_append(counter, mine);
+    if (!mine) return;
+    out.k0[j] = k0[i];
+    out.k1[j] = k1[i];
+    out.cnt[j] = acc[i];
+    out.doc[j] = idx ? doc[i] : MRG_EMPTY_DOC;
+    out.len[j] = flen[i];
+    out.hoff[j] = hoff[i];
+}
+
+// received exchange records with long keys -> long items over the received heap
+__global__ void k_x_split_long(const XRec *x, uint64_t n, const uint64_t *seg_rec_end, const uint64_t *seg_heap_base,
+                               uint32_t n_segs, LongItems li, unsigned long long *counter) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool lng = i < n && x[i].len > 16u;
+    const uint64_t j = mrg_wave_append(counter, lng);
+    if (!lng) return;
+    uint32_t sgi = 0;  // segment (sender) of record i
+    while (sgi + 1 < n_segs && i >= seg_rec_end[sgi]) ++sgi;
+    const XRec r = x[i];
+    li.start[j] = seg_heap_base[sgi] + r.heap;
+    li.rawlen[j] = r.len;
+    li.doc[j] = r.doc;
+    li.cnt[j] = r.cnt;
+}
+
+__global__ void k_export_count(KeySet ks, uint64_t n, uint32_t n_owners, unsigned long long *rec_cnt,
+                               unsigned long long *heap_cnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t o = ks.part[i] % n_owners;
+    atomicAdd(&rec_cnt[o], 1ull);
+    if (ks.len[i] > 16u) atomicAdd(&heap_cnt[o], (unsigned long long)ks.len[i]);
+}
+
+__global__ void k_export_pack(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t n_owners, const uint64_t *rec_base,
+                              const uint64_t *heap_base, unsigned long long *rec_cur, unsigned long long *heap_cur,
+                              XRec *out, uint8_t *out_heap) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t o = ks.part[i] % n_owners;
+    const uint64_t slot = rec_base[o] + atomicAdd(&rec_cur[o], 1ull);
+    XRec r;
+    r.k0 = ks.k0[i];
+    r.k1 = ks.k1[i];
+    r.cnt = ks.cnt[i];
+    r.doc = ks.doc[i];
+    r.len = ks.len[i];
+    r.heap = MRG_NO_HEAP;
+    if (r.len > 16u) {
+        const uint64_t h = atomicAdd(&heap_cur[o], (unsigned long long)r.len);  // relative to owner segment
+        const uint8_t *src = heap + ks.hoff[i];
+        uint8_t *dst = out_heap + heap_base[o] + h;
+        for (uint32_t b = 0; b < r.len; ++b) dst[b] = src[b];
+        r.heap = h;
+    }
+    out[slot] = r;
+}
+
+__global__ void k_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, SortRec *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SortRec r;
+    r.k0 = ks.k0[i];
+    r.k1 = ks.k1[i];
+    r.part = ks.part[i];
+    r.doc = doc_rank ? doc_rank[ks.doc[i]] : 0u;
+    r.idx = (uint32_t)i;
+    r.pad = 0;
+    out[i] = r;
+}
+
+template <class T>
+__global__ void k_fill(T *p, T v, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+__global__ void k_iota(uint32_t *p, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = (uint32_t)i;
+}
+
+}  // namespace
+
+void mrg_launch_table_clear(const TableArgs &t, bool indexer, hipStream_t s) {
+    hipLaunchKernelGGL(k_table_clear, grid_for(t.cap), dim3(256), 0, s, t, indexer);
+}
+void mrg_launch_table_insert(const TableArgs &t, const uint64_t *k0, const uint64_t *k1, const uint32_t *cnt32,
+                             const uint32_t *doc, uint64_t n, bool indexer, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_table_insert, grid_for(n), dim3(256), 0, s, t, k0, k1, cnt32, doc, n, indexer);
+}
+void mrg_launch_table_insert_x(const TableArgs &t, const XRec *x, uint64_t n, bool indexer, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_table_insert_x, grid_for(n), dim3(256), 0, s, t, x, n, indexer);
+}
+void mrg_launch_table_compact(const TableArgs &t, bool indexer, KeySet out, unsigned long long *counter,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(k_table_compact, grid_for(t.cap), dim3(256), 0, s, t, indexer, out, counter);
+}
+void mrg_launch_partition(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t n_reduce, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_partition, grid_for(n), dim3(256), 0, s, ks, heap, n, n_reduce);
+}
+void mrg_launch_long_group(const uint64_t *fp_sorted, const uint32_t *idx_sorted, const uint32_t *doc,
+                           const uint8_t *heap, const uint64_t *hoff, const uint32_t *flen, uint64_t n,
+                           uint32_t *rep, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_long_group, grid_for(n), dim3(256), 0, s, fp_sorted, idx_sorted, doc, heap, hoff, flen, n,
+                       rep);
+}
+void mrg_launch_long_emit(const uint32_t *rep, const uint64_t *cnt_in, const uint64_t *k0, const uint64_t *k1,
+                          const uint32_t *flen, const uint64_t *hoff, const uint32_t *doc, uint64_t n,
+                          unsigned long long *acc, KeySet out, unsigned long long *counter, bool indexer,
+                          hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_long_count, grid_for(n), dim3(256), 0, s, rep, cnt_in, n, acc);
+    hipLaunchKernelGGL(k_long_emit, grid_for(n), dim3(256), 0, s, rep, k0, k1, flen, hoff, doc, n,
+                       (const unsigned long long *)acc, out, counter, indexer);
+}
+void mrg_launch_x_split_long(const XRec *x, uint64_t n, const uint64_t *seg_rec_end, const uint64_t *seg_heap_base,
+                             uint32_t n_segs, LongItems li, unsigned long long *counter, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_x_split_long, grid_for(n), dim3(256), 0, s, x, n, seg_rec_end, seg_heap_base, n_segs, li,
+                       counter);
+}
+void mrg_launch_export_count(KeySet ks, uint64_t n, uint32_t n_owners, unsigned long long *rec_cnt,
+                             unsigned long long *heap_cnt, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_export_count, grid_for(n), dim3(256), 0, s, ks, n, n_owners, rec_cnt, heap_cnt);
+}
+void mrg_launch_export_pack(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t n_owners,
+                            const uint64_t *rec_base, const uint64_t *heap_base, unsigned long long *rec_cur,
+                            unsigned long long *heap_cur, XRec *out, uint8_t *out_heap, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_export_pack, grid_for(n), dim3(256), 0, s, ks, heap, n, n_owners, rec_base, heap_base,
+                       rec_cur, heap_cur, out, out_heap);
+}
+void mrg_launch_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, void *recs, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_make_sortrec, grid_for(n), dim3(256), 0, s, ks, n, doc_rank, (SortRec *)recs);
+}
+void mrg_launch_fill_u32(uint32_t *p, uint32_t v, uint64_t n, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_fill<uint32_t>, grid_for(n), dim3(256), 0, s, p, v, n);
+}
+void mrg_launch_fill_u64(uint64_t *p, uint64_t v, uint64_t n, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_fill<uint64_t>, grid_for(n), dim3(256), 0, s, p, v, n);
+}
+void mrg_launch_iota_u32(uint32_t *p, uint64_t n, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_iota, grid_for(n), dim3(256), 0, s, p, n);
+}

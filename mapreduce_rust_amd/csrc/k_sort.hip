@@ -1,0 +1,279 @@
+// k_sort.hip -- device-wide exclusive scan and stable LSD radix sort (8-bit digits) for gfx950.
+//
+// Replaces the reduce-side key_value_contents.sort_by(|a, b| a.key.cmp(&b.key)) (src/mr/worker.rs:
+// 162-164) for the DISTINCT keys of the owned partitions, and sorts long-key fingerprints for the
+// collision-safe grouping.  One upfront kernel builds the digit histograms of every pass; passes
+// whose digit is constant are skipped (e.g. key bytes beyond the longest key, nReduce <= 256).
+// Per pass: per-tile histogram -> scan -> stable scatter, the local rank computed by a wave64
+// 8-ballot match (peers with the same digit) plus per-wave digit counters in LDS.
+#include "mrg_device.h"
+#include "mrg_internal.h"
+
+namespace {
+
+constexpr int BS = 256;                 // threads per block
+constexpr int IPT = 8;                  // items per thread
+constexpr int TILE = BS * IPT;          // 2048 items per tile
+
+// ------------------------------------------------------------------ block scan helpers
+template <class T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+    const int lane = __lane_id();
+    for (int o = 1; o < 64; o <<= 1) {
+        const T u = __shfl_up(v, o);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
+
+// exclusive scan across the block of one value per thread; returns exclusive prefix, *total = sum
+template <class T>
+__device__ __forceinline__ T block_excl_scan(T v, T *s_wave, T *total) {
+    const int lane = __lane_id(), w = threadIdx.x >> 6;
+    const T inc = wave_incl_scan(v);
+    if (lane == 63) s_wave[w] = inc;
+    __syncthreads();
+    T base = 0, tot = 0;
+    for (int i = 0; i < BS / 64; ++i) {
+        const T x = s_wave[i];
+        if (i < w) base += x;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + inc - v;
+}
+
+template <class T>
+__global__ void k_scan_tile_sums(const T *in, uint64_t n, T *sums) {
+    __shared__ T s_wave[BS / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * TILE + (uint64_t)threadIdx.x * IPT;
+    T v = 0;
+    for (int k = 0; k < IPT; ++k)
+        if (base + k < n) v += in[base + k];
+    T tot;
+    block_excl_scan(v, s_wave, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// exclusive scan of each tile, plus tile prefix (from `prefix`, may be null)
+template <class T>
+__global__ void k_scan_tiles(const T *in, T *out, uint64_t n, const T *prefix) {
+    __shared__ T s_wave[BS / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * TILE + (uint64_t)threadIdx.x * IPT;
+    T x[IPT];
+    T v = 0;
+    for (int k = 0; k < IPT; ++k) {
+        x[k] = base + k < n ? in[base + k] : (T)0;
+        v += x[k];
+    }
+    T tot;
+    T run = block_excl_scan(v, s_wave, &tot);
+    if (prefix) run += prefix[blockIdx.x];
+    for (int k = 0; k < IPT; ++k) {
+        if (base + k < n) out[base + k] = run;
+        run += x[k];
+    }
+}
+
+template <class T>
+void scan_rec(const T *in, T *out, uint64_t n, T *tmp, hipStream_t s) {
+    if (!n) return;
+    const uint64_t nt = (n + TILE - 1) / TILE;
+    if (nt == 1) {
+        hipLaunchKernelGGL(k_scan_tiles<T>, dim3(1), dim3(BS), 0, s, in, out, n, (const T *)nullptr);
+        return;
+    }
+    T *sums = tmp;
+    T *rest = tmp + nt;
+    hipLaunchKernelGGL(k_scan_tile_sums<T>, dim3((unsigned)nt), dim3(BS), 0, s, in, n, sums);
+    scan_rec<T>(sums, sums, nt, rest, s);
+    hipLaunchKernelGGL(k_scan_tiles<T>, dim3((unsigned)nt), dim3(BS), 0, s, in, out, n, (const T *)sums);
+}
+
+uint64_t scan_tmp(uint64_t n) {
+    uint64_t t = 0;
+    while (n > TILE) {
+        n = (n + TILE - 1) / TILE;
+        t += n;
+    }
+    return t + 16;
+}
+
+// ------------------------------------------------------------------ radix sort
+struct RecTraits {  // SortRec, key = (part, k0, k1, doc); pass q counts bytes from the LSB end
+    using R = SortRec;
+    static constexpr int NPASS = 24;
+    __device__ static __forceinline__ uint32_t digit(const R &r, int q) {
+        if (q < 4) return (r.doc >> (8 * q)) & 0xFFu;
+        if (q < 12) return (uint32_t)(r.k1 >> (8 * (q - 4))) & 0xFFu;
+        if (q < 20) return (uint32_t)(r.k0 >> (8 * (q - 12))) & 0xFFu;
+        return (r.part >> (8 * (q - 20))) & 0xFFu;
+    }
+};
+struct KV64 {
+    uint64_t key;
+    uint32_t val, pad;
+};
+struct KVTraits {
+    using R = KV64;
+    static constexpr int NPASS = 8;
+    __device__ static __forceinline__ uint32_t digit(const R &r, int q) { return (uint32_t)(r.key >> (8 * q)) & 0xFFu; }
+};
+
+// all-pass histograms in one read: hist[q * 256 + d]
+template <class TR>
+__global__ void k_all_hist(const typename TR::R *in, uint64_t n, unsigned long long *hist) {
+    __shared__ unsigned int s_h[TR::NPASS * 256];
+    for (int i = threadIdx.x; i < TR::NPASS * 256; i += BS) s_h[i] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BS) {
+        const typename TR::R r = in[i];
+        for (int q = 0; q < TR::NPASS; ++q) atomicAdd(&s_h[q * 256 + TR::digit(r, q)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < TR::NPASS * 256; i += BS)
+        if (s_h[i]) atomicAdd(&hist[i], (unsigned long long)s_h[i]);
+}
+
+// per-tile digit counts, digit-major: cnt[d * ntiles + tile]
+template <class TR>
+__global__ void k_tile_hist(const typename TR::R *in, uint64_t n, int q, uint32_t *cnt, uint32_t ntiles) {
+    __shared__ unsigned int s_h[256];
+    s_h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    for (int k = 0; k < IPT; ++k) {
+        const uint64_t i = base + (uint64_t)k * BS + threadIdx.x;
+        if (i < n) atomicAdd(&s_h[TR::digit(in[i], q)], 1u);
+    }
+    __syncthreads();
+    cnt[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = s_h[threadIdx.x];
+}
+
+// stable scatter: item order inside a tile is (round k, thread t) = base + k*BS + t, exactly the
+// order the ranks are assigned in
+template <class TR>
+__global__ void k_scatter(const typename TR::R *in, typename TR::R *out, uint64_t n, int q, const uint32_t *off,
+                          uint32_t ntiles) {
+    __shared__ uint32_t s_base[256];
+    __shared__ uint32_t s_run[256];
+    __shared__ uint32_t s_wc[BS / 64][256];
+    const int t = threadIdx.x, w = t >> 6;
+    s_base[t] = off[(uint64_t)t * ntiles + blockIdx.x];
+    s_run[t] = 0;
+    for (int i = 0; i < BS / 64; ++i) s_wc[i][t] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    const uint64_t lt = mrg_lanemask_lt();
+    for (int k = 0; k < IPT; ++k) {
+        const uint64_t i = base + (uint64_t)k * BS + t;
+        const bool valid = i < n;
+        typename TR::R r;
+        uint32_t d = 0;
+        if (valid) {
+            r = in[i];
+            d = TR::digit(r, q);
+        }
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < 8; ++b) {
+            const uint64_t m = __ballot(valid && ((d >> b) & 1u));
+            peers &= ((d >> b) & 1u) ? m : ~m;
+        }
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        if (valid && rank == 0) s_wc[w][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = s_base[d] + s_run[d] + rank;
+            for (int i2 = 0; i2 < w; ++i2) pos += s_wc[i2][d];
+            out[pos] = r;
+        }
+        __syncthreads();
+        {
+            uint32_t add = 0;
+            for (int i2 = 0; i2 < BS / 64; ++i2) {
+                add += s_wc[i2][t];
+                s_wc[i2][t] = 0;
+            }
+            s_run[t] += add;
+        }
+        __syncthreads();
+    }
+}
+
+template <class TR>
+typename TR::R *radix_sort_t(typename TR::R *a, typename TR::R *b, uint64_t n, const bool *want, void *tmp,
+                             hipStream_t s, int *passes_run) {
+    if (passes_run) *passes_run = 0;
+    if (n <= 1) return a;
+    const uint32_t ntiles = (uint32_t)((n + TILE - 1) / TILE);
+    unsigned long long *hist = (unsigned long long *)tmp;
+    uint32_t *cnt = (uint32_t *)(hist + TR::NPASS * 256);
+    uint32_t *scantmp = cnt + (uint64_t)256 * ntiles;
+    hipMemsetAsync(hist, 0, sizeof(unsigned long long) * TR::NPASS * 256, s);
+    const unsigned g = (unsigned)std::min<uint64_t>((n + BS - 1) / BS, 1024);
+    hipLaunchKernelGGL(k_all_hist<TR>, dim3(g), dim3(BS), 0, s, a, n, hist);
+    unsigned long long h[TR::NPASS * 256];
+    hipMemcpyAsync(h, hist, sizeof h, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    for (int q = 0; q < TR::NPASS; ++q) {
+        if (!want[q]) continue;
+        bool trivial = false;
+        for (int d = 0; d < 256; ++d)
+            if (h[q * 256 + d] == n) { trivial = true; break; }
+        if (trivial) continue;
+        hipLaunchKernelGGL(k_tile_hist<TR>, dim3(ntiles), dim3(BS), 0, s, a, n, q, cnt, ntiles);
+        scan_rec<uint32_t>(cnt, cnt, (uint64_t)256 * ntiles, scantmp, s);
+        hipLaunchKernelGGL(k_scatter<TR>, dim3(ntiles), dim3(BS), 0, s, a, b, n, q, cnt, ntiles);
+        std::swap(a, b);
+        if (passes_run) ++*passes_run;
+    }
+    return a;
+}
+
+__global__ void k_pack_kv(const uint64_t *k, const uint32_t *v, uint64_t n, KV64 *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = KV64{k[i], v[i], 0};
+}
+__global__ void k_unpack_kv(const KV64 *in, uint64_t n, uint64_t *k, uint32_t *v) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { k[i] = in[i].key; v[i] = in[i].val; }
+}
+
+}  // namespace
+
+uint64_t mrg_scan_tmp_elems(uint64_t n) { return scan_tmp(n); }
+
+void mrg_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t s) {
+    scan_rec<uint64_t>(in, out, n, tmp, s);
+}
+
+uint64_t mrg_sort_tmp_bytes(uint64_t n) {
+    const uint64_t ntiles = (n + TILE - 1) / TILE;
+    return sizeof(unsigned long long) * 24 * 256 + sizeof(uint32_t) * (256 * ntiles + scan_tmp(256 * ntiles)) + 256;
+}
+
+SortRec *mrg_radix_sort(SortRec *recs, SortRec *alt, uint64_t n, const SortPlan &plan, void *tmp, hipStream_t s,
+                        int *passes_run) {
+    bool want[24];
+    for (int q = 0; q < 24; ++q) {
+        if (q < 4) want[q] = plan.use_doc && (uint32_t)q < plan.doc_bytes;
+        else if (q < 12) want[q] = plan.use_k1;
+        else if (q < 20) want[q] = plan.use_k0;
+        else want[q] = plan.use_part && (uint32_t)(q - 20) < plan.part_bytes;
+    }
+    return radix_sort_t<RecTraits>(recs, alt, n, want, tmp, s, passes_run);
+}
+
+// (key, val) pairs sorted by key, stable, in place; kv_tmp holds two KV64 staging arrays (4n u64).
+void mrg_radix_sort_u64(uint64_t *keys, uint32_t *vals, uint64_t *kv_tmp, uint64_t n, void *tmp, hipStream_t s) {
+    if (n <= 1) return;
+    KV64 *a = (KV64 *)kv_tmp;
+    KV64 *b = a + n;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(k_pack_kv, dim3(g), dim3(256), 0, s, keys, vals, n, a);
+    bool want[8];
+    for (int q = 0; q < 8; ++q) want[q] = true;
+    KV64 *r = radix_sort_t<KVTraits>(a, b, n, want, tmp, s, nullptr);
+    hipLaunchKernelGGL(k_unpack_kv, dim3(g), dim3(256), 0, s, r, n, keys, vals);
+}

@@ -1,0 +1,151 @@
+// mrg_internal.h -- host-side declarations shared by the kernel files and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#define MRG_MAP_WG 256          // threads per map workgroup (4 waves)
+#define MRG_MAP_SEG 16          // input bytes per lane per tile
+#define MRG_MAP_TILE (MRG_MAP_WG * MRG_MAP_SEG)  // 4 KiB tile per workgroup iteration
+#define MRG_MAP_HALO 256        // bytes after the tile staged in LDS (tokens crossing the tile end)
+#define MRG_MAP_BEHIND 16       // bytes before the tile staged in LDS (previous codepoint)
+
+// counters[] slots written by the kernels
+enum { CNT_REC = 0, CNT_LONG = 1, CNT_TOKENS = 2, CNT_ERRPOS = 3, CNT_KEYS = 4, CNT_N = 8 };
+
+// Stream-ordered caching allocator interface (all work of a context runs on one stream, so a
+// buffer released after its last enqueued use can be handed out again immediately).
+struct DevPool {
+    virtual void *get(size_t bytes) = 0;
+    virtual void put(void *p) = 0;
+    virtual ~DevPool() {}
+};
+
+struct MapArgs {
+    const uint8_t *in;
+    const uint64_t *doc_off;     // [n_docs + 1] byte offsets into `in`
+    const uint64_t *chunk_base;  // [n_docs + 1] first tile index of each document
+    const uint32_t *doc_id;      // [n_docs] global document id
+    uint32_t n_docs;
+    uint64_t n_chunks;
+    // short-key records (LDS-combine misses and the final LDS flush)
+    uint64_t *rk0, *rk1;
+    uint32_t *rcnt, *rdoc;
+    uint64_t rcap;
+    // long-key token records (> 16 key bytes)
+    uint64_t *lstart;
+    uint32_t *llen, *ldoc;
+    uint64_t lcap;
+    unsigned long long *counters;
+    uint32_t hash_bits;          // 0 = full; else truncate internal hashes (collision test knob)
+};
+
+// A set of keys with counts (SoA).  len > 16 keys have their bytes at heap[hoff .. hoff+len).
+struct KeySet {
+    uint64_t *k0, *k1, *cnt, *hoff;
+    uint32_t *doc, *len, *part;
+};
+
+struct TableArgs {
+    uint64_t *tk0, *tk1, *tcnt;
+    uint32_t *tdoc;
+    uint64_t cap;                // power of two
+    uint32_t hash_bits;
+};
+
+// Exchange record, MRG_XREC_BYTES = 40 (include/mrgpu.h)
+struct XRec {
+    uint64_t k0, k1, cnt;
+    uint32_t doc, len;
+    uint64_t heap;
+};
+static_assert(sizeof(XRec) == 40, "XRec layout");
+
+// Long items: keys > 16 bytes, as raw byte ranges of `base` (input text or a received heap).
+struct LongItems {
+    const uint8_t *base;
+    uint64_t *start;
+    uint32_t *rawlen, *doc;
+    uint64_t *cnt;               // null: 1 each
+    uint64_t n;
+};
+
+// ---- k_map.hip
+void mrg_launch_map(const MapArgs &a, int app, int grid, int lds_cap, hipStream_t s);
+int mrg_map_max_grid(int app, int lds_cap, int device);
+void mrg_launch_long_prep(const uint8_t *base, const uint64_t *start, const uint32_t *rawlen, uint64_t n,
+                          uint64_t *k0, uint64_t *k1, uint32_t *flen, uint64_t *flen64, uint64_t *fp,
+                          uint32_t hash_bits, hipStream_t s);
+void mrg_launch_long_gather(const uint8_t *base, const uint64_t *start, const uint32_t *rawlen, uint64_t n,
+                            const uint64_t *dst_off, uint8_t *heap, hipStream_t s);
+
+// ---- k_keys.hip
+void mrg_launch_table_clear(const TableArgs &t, bool indexer, hipStream_t s);
+void mrg_launch_table_insert(const TableArgs &t, const uint64_t *k0, const uint64_t *k1, const uint32_t *cnt32,
+                             const uint32_t *doc, uint64_t n, bool indexer, hipStream_t s);
+void mrg_launch_table_insert_x(const TableArgs &t, const XRec *x, uint64_t n, bool indexer, hipStream_t s);
+void mrg_launch_table_compact(const TableArgs &t, bool indexer, KeySet out, unsigned long long *counter,
+                              hipStream_t s);
+void mrg_launch_partition(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t n_reduce, hipStream_t s);
+void mrg_launch_long_group(const uint64_t *fp_sorted, const uint32_t *idx_sorted, const uint32_t *doc,
+                           const uint8_t *heap, const uint64_t *hoff, const uint32_t *flen, uint64_t n,
+                           uint32_t *rep, hipStream_t s);
+void mrg_launch_long_emit(const uint32_t *rep, const uint64_t *cnt_in, const uint64_t *k0, const uint64_t *k1,
+                          const uint32_t *flen, const uint64_t *hoff, const uint32_t *doc, uint64_t n,
+                          unsigned long long *acc, KeySet out, unsigned long long *counter, bool indexer,
+                          hipStream_t s);
+void mrg_launch_x_split_long(const XRec *x, uint64_t n, const uint64_t *seg_rec_end, const uint64_t *seg_heap_base,
+                             uint32_t n_segs, LongItems li, unsigned long long *counter, hipStream_t s);
+void mrg_launch_export_count(KeySet ks, uint64_t n, uint32_t n_owners, unsigned long long *rec_cnt,
+                             unsigned long long *heap_cnt, hipStream_t s);
+void mrg_launch_export_pack(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t n_owners,
+                            const uint64_t *rec_base, const uint64_t *heap_base, unsigned long long *rec_cur,
+                            unsigned long long *heap_cur, XRec *out, uint8_t *out_heap, hipStream_t s);
+void mrg_launch_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, void *recs, hipStream_t s);
+void mrg_launch_fill_u32(uint32_t *p, uint32_t v, uint64_t n, hipStream_t s);
+void mrg_launch_fill_u64(uint64_t *p, uint64_t v, uint64_t n, hipStream_t s);
+void mrg_launch_iota_u32(uint32_t *p, uint64_t n, hipStream_t s);
+
+// ---- k_sort.hip
+uint64_t mrg_scan_tmp_elems(uint64_t n);
+// exclusive scan of u64 values (in == out allowed); tmp holds mrg_scan_tmp_elems(n) u64
+void mrg_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t s);
+struct SortRec {  // 32 bytes
+    uint64_t k0, k1;
+    uint32_t part, doc;
+    uint32_t idx, pad;
+};
+struct SortPlan {
+    bool use_doc, use_k1, use_k0, use_part;
+    uint32_t part_bytes;   // bytes of `part` that can be non-zero
+    uint32_t doc_bytes;
+};
+uint64_t mrg_sort_tmp_bytes(uint64_t n);
+// Stable sort by (part, k0, k1, doc) ascending.  Returns the buffer (recs or alt) with the result.
+SortRec *mrg_radix_sort(SortRec *recs, SortRec *alt, uint64_t n, const SortPlan &plan, void *tmp, hipStream_t s,
+                        int *passes_run);
+// Stable sort of (u64 key, u32 val) pairs by key, in place in (keys, vals); kv_tmp holds 4n u64.
+void mrg_radix_sort_u64(uint64_t *keys, uint32_t *vals, uint64_t *kv_tmp, uint64_t n, void *tmp, hipStream_t s);
+
+// ---- k_format.hip
+struct FormatArgs {
+    const SortRec *recs;        // sorted by (part, key prefix, doc rank)
+    uint64_t n;
+    KeySet ks;
+    const uint8_t *heap;
+    uint32_t n_reduce;
+    int drop_last;
+    int indexer;
+    int any_long;
+    const uint8_t *names;       // indexer: doc names concatenated in rank order
+    const uint64_t *name_off;   // [n_docs + 1], by rank
+};
+// Writes every mr-{r}.txt (concatenated in r order) into *out_buf (grown from the pool) and the
+// partition byte offsets to part_off_host[0..n_reduce].  Returns the total byte count.
+uint64_t mrg_format(const FormatArgs &f, DevPool &pool, uint8_t **out_buf, uint64_t *out_cap,
+                    uint64_t *part_off_host, hipStream_t s);
+
+// ---- k_gen.hip
+int mrg_gen_zipf_impl(uint8_t *dst, uint64_t n, uint64_t seed, uint64_t file_index, uint32_t vocab, double s,
+                      hipStream_t st);
+int mrg_gen_unique_impl(uint8_t *dst, uint64_t n, uint64_t seed, uint64_t file_index, hipStream_t st);

@@ -1,0 +1,893 @@
+// mrgpu.cpp -- C ABI (include/mrgpu.h) and host orchestration of libmrgpu.so.
+//
+// Pipeline of one job, all on one HIP stream of the context:
+//   map     k_map (tokenize + LDS combine)                         wc.rs:6-13, worker.rs:117-131
+//   agg     HBM table insert/compact + long-key fingerprint sort   worker.rs:165-184 (grouping)
+//           + SipHash-1-3 % R per distinct key                     worker.rs:111-115, 129
+//   [shuffle: export by owner = r % G, exchange by the caller (RCCL all-to-all), import]
+//   reduce  radix sort by (r, key bytes[, doc]) + format lines     worker.rs:162-184, wc.rs:15-17
+// Errors never cross the ABI as exceptions or aborts: every entry point returns a status code.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "mrg_internal.h"
+#include "mrgpu.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+struct MrgError {
+    int code;
+    std::string msg;
+};
+
+[[noreturn]] void raise(int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    throw MrgError{code, buf};
+}
+
+#define HIPCHK(x)                                                                      \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) raise(MRG_EHIP, "%s: %s", #x, hipGetErrorString(e_));    \
+    } while (0)
+
+template <class F>
+int guard(F &&f) {
+    try {
+        f();
+        return MRG_OK;
+    } catch (const MrgError &e) {
+        g_err = e.msg;
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        g_err = "host out of memory";
+        return MRG_ENOMEM;
+    } catch (...) {
+        g_err = "unexpected internal error";
+        return MRG_EINVAL;
+    }
+}
+
+// ---------------------------------------------------------------- caching device allocator
+class Pool : public DevPool {
+   public:
+    void *get(size_t bytes) override {
+        const size_t c = cls(bytes ? bytes : 1);
+        auto it = free_.find(c);
+        if (it != free_.end()) {
+            void *p = it->second;
+            free_.erase(it);
+            return p;
+        }
+        void *p = nullptr;
+        if (hipMalloc(&p, c) != hipSuccess) {
+            (void)hipGetLastError();
+            trim();
+            if (hipMalloc(&p, c) != hipSuccess) {
+                (void)hipGetLastError();
+                raise(MRG_ENOMEM, "device allocation of %zu bytes failed", c);
+            }
+        }
+        size_[p] = c;
+        return p;
+    }
+    void put(void *p) override {
+        if (!p) return;
+        auto it = size_.find(p);
+        if (it != size_.end()) free_.insert({it->second, p});
+    }
+    void trim() {
+        (void)hipDeviceSynchronize();
+        for (auto &kv : free_) {
+            (void)hipFree(kv.second);
+            size_.erase(kv.second);
+        }
+        free_.clear();
+    }
+    ~Pool() override {
+        (void)hipDeviceSynchronize();
+        for (auto &kv : size_) (void)hipFree(kv.first);
+    }
+
+   private:
+    static size_t cls(size_t b) {
+        if (b <= 4096) return (b + 255) & ~(size_t)255;
+        size_t p = 4096;
+        while (p < b) p <<= 1;
+        const size_t step = p >> 3;  // 8 classes per octave: <= 12.5% slack
+        return ((b + step - 1) / step) * step;
+    }
+    std::multimap<size_t, void *> free_;
+    std::unordered_map<void *, size_t> size_;
+};
+
+template <class T>
+T *pget(Pool &p, uint64_t n) {
+    return (T *)p.get(sizeof(T) * (n ? n : 1));
+}
+
+struct KeysBuf {
+    KeySet ks{};
+    uint64_t n = 0, cap = 0;
+    uint8_t *heap = nullptr;
+    uint64_t heap_bytes = 0;
+    bool any_long = false;
+};
+
+}  // namespace
+
+struct mrg_ctx {
+    int device = 0;
+    hipStream_t own = nullptr, stream = nullptr;
+    Pool pool;
+    unsigned long long *d_cnt = nullptr;  // CNT_N counters
+    unsigned long long *h_cnt = nullptr;  // pinned mirror
+    bool timing = false;
+    hipEvent_t ev[8] = {};
+    int lds_cap = 2048;
+    int map_grid = 0;
+    uint64_t rec_hint = 0, long_hint = 0;
+    // job
+    bool job = false;
+    int app = 0;
+    uint32_t R = 0, flags = 0;
+    const uint8_t *d_in = nullptr;
+    std::vector<uint64_t> doc_off;
+    std::vector<uint32_t> doc_ids;
+    std::vector<std::string> names;
+    KeysBuf keys;
+    bool mapped = false;
+    uint32_t n_owners = 0;
+    std::vector<uint64_t> exp_rec, exp_heap;
+    uint8_t *d_out = nullptr;
+    uint64_t out_cap = 0, out_bytes = 0;
+    std::vector<uint64_t> part_off;
+    bool reduced = false;
+    mrg_stats st{};
+};
+
+struct mrg_parts {
+    uint32_t R = 0;
+    std::vector<uint64_t> rec_off, heap_off;  // [R + 1]
+    std::vector<uint8_t> recs, heap;
+};
+
+namespace {
+
+uint32_t hash_bits(const mrg_ctx *c) { return (c->flags >> 8) & 0xFFu; }
+bool is_idx(const mrg_ctx *c) { return c->app == MRG_APP_INDEXER; }
+
+void sync(mrg_ctx *c) { HIPCHK(hipStreamSynchronize(c->stream)); }
+
+void read_counters(mrg_ctx *c) {
+    HIPCHK(hipMemcpyAsync(c->h_cnt, c->d_cnt, sizeof(unsigned long long) * CNT_N, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+}
+
+void ev_rec(mrg_ctx *c, int i) {
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[i], c->stream));
+}
+double ev_ms(mrg_ctx *c, int a, int b) {
+    if (!c->timing) return 0.0;
+    float ms = 0;
+    HIPCHK(hipEventSynchronize(c->ev[b]));
+    HIPCHK(hipEventElapsedTime(&ms, c->ev[a], c->ev[b]));
+    return ms;
+}
+
+void keys_release(mrg_ctx *c) {
+    KeysBuf &k = c->keys;
+    Pool &p = c->pool;
+    p.put(k.ks.k0); p.put(k.ks.k1); p.put(k.ks.cnt); p.put(k.ks.hoff);
+    p.put(k.ks.doc); p.put(k.ks.len); p.put(k.ks.part);
+    p.put(k.heap);
+    k = KeysBuf{};
+}
+
+void keys_reserve(mrg_ctx *c, uint64_t cap) {
+    keys_release(c);
+    KeysBuf &k = c->keys;
+    Pool &p = c->pool;
+    k.ks.k0 = pget<uint64_t>(p, cap);
+    k.ks.k1 = pget<uint64_t>(p, cap);
+    k.ks.cnt = pget<uint64_t>(p, cap);
+    k.ks.hoff = pget<uint64_t>(p, cap);
+    k.ks.doc = pget<uint32_t>(p, cap);
+    k.ks.len = pget<uint32_t>(p, cap);
+    k.ks.part = pget<uint32_t>(p, cap);
+    k.cap = cap;
+}
+
+uint64_t pow2_at_least(uint64_t x) {
+    uint64_t p = 1024;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+struct ShortSrc {
+    const uint64_t *k0 = nullptr, *k1 = nullptr;
+    const uint32_t *cnt = nullptr, *doc = nullptr;
+    const XRec *x = nullptr;
+    uint64_t n = 0;
+};
+
+// Aggregate short-key records and long items into c->keys (distinct keys, counts, partitions).
+void aggregate(mrg_ctx *c, const ShortSrc &src, LongItems li) {
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const bool idx = is_idx(c);
+    keys_reserve(c, src.n + li.n + 1);
+    HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, sizeof(unsigned long long), s));
+
+    if (src.n) {
+        TableArgs T{};
+        T.cap = pow2_at_least(2 * src.n);
+        T.tk0 = pget<uint64_t>(p, T.cap);
+        T.tk1 = pget<uint64_t>(p, T.cap);
+        T.tcnt = pget<uint64_t>(p, T.cap);
+        T.tdoc = idx ? pget<uint32_t>(p, T.cap) : nullptr;
+        T.hash_bits = hash_bits(c);
+        mrg_launch_table_clear(T, idx, s);
+        if (src.x) mrg_launch_table_insert_x(T, src.x, src.n, idx, s);
+        else mrg_launch_table_insert(T, src.k0, src.k1, src.cnt, src.doc, src.n, idx, s);
+        mrg_launch_table_compact(T, idx, c->keys.ks, &c->d_cnt[CNT_KEYS], s);
+        p.put(T.tk0); p.put(T.tk1); p.put(T.tcnt); p.put(T.tdoc);
+    }
+
+    if (li.n) {
+        const uint64_t n = li.n;
+        uint64_t *k0 = pget<uint64_t>(p, n), *k1 = pget<uint64_t>(p, n), *fp = pget<uint64_t>(p, n);
+        uint64_t *fl64 = pget<uint64_t>(p, n), *hoff = pget<uint64_t>(p, n), *acc = pget<uint64_t>(p, n);
+        uint32_t *fl = pget<uint32_t>(p, n), *ix = pget<uint32_t>(p, n), *rep = pget<uint32_t>(p, n);
+        uint64_t *scantmp = pget<uint64_t>(p, mrg_scan_tmp_elems(n));
+        mrg_launch_long_prep(li.base, li.start, li.rawlen, n, k0, k1, fl, fl64, fp, hash_bits(c), s);
+        mrg_scan_u64(fl64, hoff, n, scantmp, s);
+        uint64_t last[2];
+        HIPCHK(hipMemcpyAsync(&last[0], hoff + (n - 1), 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&last[1], fl64 + (n - 1), 8, hipMemcpyDeviceToHost, s));
+        sync(c);
+        const uint64_t heap_bytes = last[0] + last[1];
+        c->keys.heap = pget<uint8_t>(p, heap_bytes + 16);
+        c->keys.heap_bytes = heap_bytes;
+        mrg_launch_long_gather(li.base, li.start, li.rawlen, n, hoff, c->keys.heap, s);
+        // fingerprint sort (collision-safe: k_long_group compares full bytes inside equal runs)
+        uint64_t *fps = pget<uint64_t>(p, n);
+        HIPCHK(hipMemcpyAsync(fps, fp, 8 * n, hipMemcpyDeviceToDevice, s));
+        mrg_launch_iota_u32(ix, n, s);
+        uint64_t *kv = pget<uint64_t>(p, 4 * n);
+        void *stmp = p.get(mrg_sort_tmp_bytes(n));
+        mrg_radix_sort_u64(fps, ix, kv, n, stmp, s);
+        mrg_launch_long_group(fps, ix, idx ? li.doc : nullptr, c->keys.heap, hoff, fl, n, rep, s);
+        HIPCHK(hipMemsetAsync(acc, 0, 8 * n, s));
+        mrg_launch_long_emit(rep, li.cnt, k0, k1, fl, hoff, li.doc, n, (unsigned long long *)acc, c->keys.ks,
+                             &c->d_cnt[CNT_KEYS], idx, s);
+        p.put(k0); p.put(k1); p.put(fp); p.put(fl64); p.put(hoff); p.put(acc);
+        p.put(fl); p.put(ix); p.put(rep); p.put(scantmp); p.put(fps); p.put(kv); p.put(stmp);
+        c->keys.any_long = true;
+    }
+    read_counters(c);
+    c->keys.n = c->h_cnt[CNT_KEYS];
+    mrg_launch_partition(c->keys.ks, c->keys.heap, c->keys.n, c->R, s);
+    c->st.distinct_keys = c->keys.n;
+}
+
+void need_job(mrg_ctx *c) {
+    if (!c) raise(MRG_EINVAL, "null context");
+    if (!c->job) raise(MRG_EINVAL, "no job: call mrg_job_begin first");
+}
+
+void job_begin(mrg_ctx *c, int app, uint32_t R, uint32_t flags) {
+    if (app != MRG_APP_WC && app != MRG_APP_INDEXER) raise(MRG_EINVAL, "unknown app %d", app);
+    if (R == 0) raise(MRG_EINVAL, "n_reduce must be > 0");
+    sync(c);
+    keys_release(c);
+    c->job = true;
+    c->app = app;
+    c->R = R;
+    c->flags = flags;
+    c->d_in = nullptr;
+    c->doc_off.clear();
+    c->doc_ids.clear();
+    c->mapped = c->reduced = false;
+    c->n_owners = 0;
+    c->out_bytes = 0;
+    c->part_off.assign(R + 1, 0);
+    c->st = mrg_stats{};
+}
+
+void job_map(mrg_ctx *c) {
+    need_job(c);
+    if (c->doc_off.empty()) raise(MRG_EINVAL, "no input: call mrg_job_set_input first");
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const uint32_t nd = (uint32_t)c->doc_off.size() - 1;
+    const uint64_t total = c->doc_off[nd] - c->doc_off[0];
+    std::vector<uint64_t> cb(nd + 1, 0);
+    for (uint32_t d = 0; d < nd; ++d) cb[d + 1] = cb[d] + (c->doc_off[d + 1] - c->doc_off[d] + MRG_MAP_TILE - 1) / MRG_MAP_TILE;
+    const uint64_t n_chunks = cb[nd];
+    std::vector<uint32_t> ids = c->doc_ids;
+    if (ids.empty()) for (uint32_t d = 0; d < nd; ++d) ids.push_back(d);
+
+    uint64_t *d_doc_off = pget<uint64_t>(p, nd + 1), *d_cb = pget<uint64_t>(p, nd + 1);
+    uint32_t *d_ids = pget<uint32_t>(p, nd);
+    HIPCHK(hipMemcpyAsync(d_doc_off, c->doc_off.data(), 8ull * (nd + 1), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_cb, cb.data(), 8ull * (nd + 1), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_ids, ids.data(), 4ull * nd, hipMemcpyHostToDevice, s));
+
+    if (!c->map_grid) c->map_grid = mrg_map_max_grid(c->app, c->lds_cap, c->device);
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->map_grid, n_chunks));
+    uint64_t rcap = std::max<uint64_t>(c->rec_hint, total / 32 + (uint64_t)grid * c->lds_cap + 4096);
+    uint64_t lcap = std::max<uint64_t>(c->long_hint, total / 1024 + 1024);
+    MapArgs A{};
+    uint32_t launches = 0;
+    for (;;) {
+        A.in = c->d_in;
+        A.doc_off = d_doc_off;
+        A.chunk_base = d_cb;
+        A.doc_id = d_ids;
+        A.n_docs = nd;
+        A.n_chunks = n_chunks;
+        A.rk0 = pget<uint64_t>(p, rcap);
+        A.rk1 = pget<uint64_t>(p, rcap);
+        A.rcnt = pget<uint32_t>(p, rcap);
+        A.rdoc = is_idx(c) ? pget<uint32_t>(p, rcap) : nullptr;
+        A.rcap = rcap;
+        A.lstart = pget<uint64_t>(p, lcap);
+        A.llen = pget<uint32_t>(p, lcap);
+        A.ldoc = pget<uint32_t>(p, lcap);
+        A.lcap = lcap;
+        A.counters = c->d_cnt;
+        A.hash_bits = hash_bits(c);
+        HIPCHK(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long) * CNT_N, s));
+        HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_ERRPOS], 0xFF, sizeof(unsigned long long), s));
+        ev_rec(c, 0);
+        if (n_chunks) mrg_launch_map(A, c->app, grid, c->lds_cap, s);
+        ev_rec(c, 1);
+        HIPCHK(hipGetLastError());
+        ++launches;
+        read_counters(c);
+        const uint64_t nr = c->h_cnt[CNT_REC], nl = c->h_cnt[CNT_LONG];
+        if (nr <= rcap && nl <= lcap) break;
+        // capacity exceeded: grow (remembered for later jobs) and run the map again
+        p.put(A.rk0); p.put(A.rk1); p.put(A.rcnt); p.put(A.rdoc);
+        p.put(A.lstart); p.put(A.llen); p.put(A.ldoc);
+        if (nr > rcap) rcap = c->rec_hint = nr + nr / 8 + 4096;
+        if (nl > lcap) lcap = c->long_hint = nl + nl / 8 + 1024;
+    }
+    c->st.ms_map = ev_ms(c, 0, 1);
+    c->st.map_launches = launches;
+    c->st.input_bytes = total;
+    c->st.tokens = c->h_cnt[CNT_TOKENS];
+    c->st.long_tokens = c->h_cnt[CNT_LONG];
+    c->st.map_records = c->h_cnt[CNT_REC];
+    const uint64_t errpos = c->h_cnt[CNT_ERRPOS];
+    auto release_map = [&]() {
+        p.put(A.rk0); p.put(A.rk1); p.put(A.rcnt); p.put(A.rdoc);
+        p.put(A.lstart); p.put(A.llen); p.put(A.ldoc);
+        p.put(d_doc_off); p.put(d_cb); p.put(d_ids);
+    };
+    if (errpos != ~0ull) {
+        release_map();
+        uint32_t d = 0;
+        while (d + 1 < nd && c->doc_off[d + 1] <= errpos) ++d;
+        raise(MRG_EUTF8, "stream did not contain valid UTF-8: document %u (id %u), byte offset %llu", d, ids[d],
+              (unsigned long long)(errpos - c->doc_off[d]));
+    }
+    ev_rec(c, 2);
+    ShortSrc src;
+    src.k0 = A.rk0; src.k1 = A.rk1; src.cnt = A.rcnt; src.doc = A.rdoc; src.n = c->h_cnt[CNT_REC];
+    LongItems li{};
+    li.base = c->d_in; li.start = A.lstart; li.rawlen = A.llen; li.doc = A.ldoc; li.cnt = nullptr;
+    li.n = c->h_cnt[CNT_LONG];
+    aggregate(c, src, li);
+    ev_rec(c, 3);
+    release_map();
+    c->st.ms_aggregate = ev_ms(c, 2, 3);
+    c->mapped = true;
+}
+
+uint32_t bytes_for(uint64_t maxval) {
+    uint32_t b = 0;
+    while (maxval) { ++b; maxval >>= 8; }
+    return b;
+}
+
+void job_reduce(mrg_ctx *c) {
+    need_job(c);
+    if (!c->mapped) raise(MRG_EINVAL, "nothing to reduce: call mrg_job_map or mrg_job_import first");
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const uint64_t n = c->keys.n;
+    const bool idx = is_idx(c);
+    // indexer: document order = bytewise order of the names (indexer reduce sorts its values)
+    uint32_t *d_rank = nullptr;
+    uint8_t *d_names = nullptr;
+    uint64_t *d_name_off = nullptr;
+    std::vector<uint32_t> order;
+    if (idx) {
+        const uint32_t nn = (uint32_t)c->names.size();
+        if (nn == 0) raise(MRG_EINVAL, "indexer needs document names (mrg_job_set_doc_names)");
+        order.resize(nn);
+        for (uint32_t i = 0; i < nn; ++i) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c->names[a] < c->names[b]; });
+        std::vector<uint32_t> rank(nn);
+        std::vector<uint64_t> noff(nn + 1, 0);
+        std::string cat;
+        for (uint32_t r = 0; r < nn; ++r) {
+            rank[order[r]] = r;
+            cat += c->names[order[r]];
+            noff[r + 1] = cat.size();
+        }
+        d_rank = pget<uint32_t>(p, nn);
+        d_names = pget<uint8_t>(p, cat.size() + 1);
+        d_name_off = pget<uint64_t>(p, nn + 1);
+        HIPCHK(hipMemcpyAsync(d_rank, rank.data(), 4ull * nn, hipMemcpyHostToDevice, s));
+        if (!cat.empty()) HIPCHK(hipMemcpyAsync(d_names, cat.data(), cat.size(), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(d_name_off, noff.data(), 8ull * (nn + 1), hipMemcpyHostToDevice, s));
+        sync(c);  // host vectors go out of scope
+    }
+    ev_rec(c, 4);
+    SortRec *a = pget<SortRec>(p, n), *b = pget<SortRec>(p, n);
+    void *stmp = p.get(mrg_sort_tmp_bytes(n));
+    mrg_launch_make_sortrec(c->keys.ks, n, d_rank, a, s);
+    SortPlan plan{};
+    plan.use_part = c->R > 1;
+    plan.part_bytes = bytes_for(c->R - 1);
+    plan.use_k0 = plan.use_k1 = true;
+    plan.use_doc = idx;
+    plan.doc_bytes = idx ? bytes_for(c->names.size() - 1) : 0;
+    int passes = 0;
+    SortRec *sorted = mrg_radix_sort(a, b, n, plan, stmp, s, &passes);
+    ev_rec(c, 5);
+    FormatArgs f{};
+    f.recs = sorted;
+    f.n = n;
+    f.ks = c->keys.ks;
+    f.heap = c->keys.heap;
+    f.n_reduce = c->R;
+    f.drop_last = (c->flags & MRG_FLAG_NO_COMPAT_DROP_LAST) ? 0 : 1;
+    f.indexer = idx;
+    f.any_long = c->keys.any_long;
+    f.names = d_names;
+    f.name_off = d_name_off;
+    c->part_off.assign(c->R + 1, 0);
+    c->out_bytes = mrg_format(f, p, &c->d_out, &c->out_cap, c->part_off.data(), s);
+    ev_rec(c, 6);
+    HIPCHK(hipGetLastError());
+    p.put(a); p.put(b); p.put(stmp);
+    p.put(d_rank); p.put(d_names); p.put(d_name_off);
+    c->st.ms_sort = ev_ms(c, 4, 5);
+    c->st.ms_format = ev_ms(c, 5, 6);
+    c->st.output_bytes = c->out_bytes;
+    c->reduced = true;
+}
+
+void export_sizes(mrg_ctx *c, uint32_t n_owners, uint64_t *h_rec, uint64_t *h_heap) {
+    need_job(c);
+    if (!c->mapped) raise(MRG_EINVAL, "export before map");
+    if (n_owners == 0) raise(MRG_EINVAL, "n_owners must be > 0");
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    unsigned long long *d = pget<unsigned long long>(p, 2ull * n_owners);
+    HIPCHK(hipMemsetAsync(d, 0, 16ull * n_owners, s));
+    mrg_launch_export_count(c->keys.ks, c->keys.n, n_owners, d, d + n_owners, s);
+    std::vector<uint64_t> h(2ull * n_owners);
+    HIPCHK(hipMemcpyAsync(h.data(), d, 16ull * n_owners, hipMemcpyDeviceToHost, s));
+    sync(c);
+    p.put(d);
+    c->n_owners = n_owners;
+    c->exp_rec.assign(h.begin(), h.begin() + n_owners);
+    c->exp_heap.assign(h.begin() + n_owners, h.end());
+    if (h_rec) memcpy(h_rec, c->exp_rec.data(), 8ull * n_owners);
+    if (h_heap) memcpy(h_heap, c->exp_heap.data(), 8ull * n_owners);
+}
+
+void export_pack(mrg_ctx *c, void *d_rec, void *d_heap) {
+    need_job(c);
+    if (!c->n_owners) raise(MRG_EINVAL, "call mrg_job_export_sizes first");
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const uint32_t G = c->n_owners;
+    std::vector<uint64_t> base(2ull * G, 0);
+    for (uint32_t o = 1; o < G; ++o) {
+        base[o] = base[o - 1] + c->exp_rec[o - 1];
+        base[G + o] = base[G + o - 1] + c->exp_heap[o - 1];
+    }
+    uint64_t *d_base = pget<uint64_t>(p, 2ull * G);
+    unsigned long long *cur = pget<unsigned long long>(p, 2ull * G);
+    HIPCHK(hipMemcpyAsync(d_base, base.data(), 16ull * G, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(cur, 0, 16ull * G, s));
+    mrg_launch_export_pack(c->keys.ks, c->keys.heap, c->keys.n, G, d_base, d_base + G, cur, cur + G, (XRec *)d_rec,
+                           (uint8_t *)d_heap, s);
+    sync(c);
+    p.put(d_base);
+    p.put(cur);
+}
+
+void job_import(mrg_ctx *c, const void *d_rec, uint64_t n_rec, const void *d_heap, uint64_t heap_bytes,
+                const uint64_t *seg_recs, const uint64_t *seg_heap, uint32_t n_segs) {
+    need_job(c);
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    std::vector<uint64_t> rec_end, heap_base;
+    if (n_segs == 0) {
+        rec_end.push_back(n_rec);
+        heap_base.push_back(0);
+        n_segs = 1;
+    } else {
+        uint64_t r = 0, h = 0;
+        for (uint32_t i = 0; i < n_segs; ++i) {
+            heap_base.push_back(h);
+            r += seg_recs[i];
+            h += seg_heap[i];
+            rec_end.push_back(r);
+        }
+        if (r != n_rec || h != heap_bytes) raise(MRG_EINVAL, "segment sizes do not add up to n_rec / heap_bytes");
+    }
+    uint64_t *d_seg = pget<uint64_t>(p, 2ull * n_segs);
+    HIPCHK(hipMemcpyAsync(d_seg, rec_end.data(), 8ull * n_segs, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_seg + n_segs, heap_base.data(), 8ull * n_segs, hipMemcpyHostToDevice, s));
+    LongItems li{};
+    li.base = (const uint8_t *)d_heap;
+    li.start = pget<uint64_t>(p, n_rec);
+    li.rawlen = pget<uint32_t>(p, n_rec);
+    li.doc = pget<uint32_t>(p, n_rec);
+    li.cnt = pget<uint64_t>(p, n_rec);
+    HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_LONG], 0, 8, s));
+    mrg_launch_x_split_long((const XRec *)d_rec, n_rec, d_seg, d_seg + n_segs, n_segs, li, &c->d_cnt[CNT_LONG], s);
+    read_counters(c);
+    li.n = c->h_cnt[CNT_LONG];
+    ShortSrc src;
+    src.x = (const XRec *)d_rec;
+    src.n = n_rec;
+    ev_rec(c, 2);
+    aggregate(c, src, li);
+    ev_rec(c, 3);
+    sync(c);
+    p.put(d_seg); p.put(li.start); p.put(li.rawlen); p.put(li.doc); p.put(li.cnt);
+    c->st.ms_aggregate = ev_ms(c, 2, 3);
+    c->mapped = true;
+    c->reduced = false;
+}
+
+void check_names(const char *const *names, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!names[i]) raise(MRG_EINVAL, "null document name %u", i);
+        for (const char *q = names[i]; *q; ++q)
+            if (*q == ' ' || *q == ',' || *q == '\n')
+                raise(MRG_EINVAL, "document name '%s' contains ' ', ',' or newline", names[i]);
+    }
+}
+
+}  // namespace
+
+// ===================================================================== C ABI
+
+extern "C" {
+
+const char *mrg_last_error(void) { return g_err.c_str(); }
+const char *mrg_version(void) { return "mrgpu 0.1 (gfx950)"; }
+
+int mrg_open(int device, mrg_ctx **out) {
+    return guard([&] {
+        if (!out) raise(MRG_EINVAL, "null out");
+        int ndev = 0;
+        HIPCHK(hipGetDeviceCount(&ndev));
+        if (device < 0 || device >= ndev) raise(MRG_EINVAL, "device %d not present (%d devices)", device, ndev);
+        HIPCHK(hipSetDevice(device));
+        mrg_ctx *c = new mrg_ctx();
+        c->device = device;
+        HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+        c->stream = c->own;
+        HIPCHK(hipMalloc(&c->d_cnt, sizeof(unsigned long long) * CNT_N));
+        HIPCHK(hipHostMalloc(&c->h_cnt, sizeof(unsigned long long) * CNT_N, hipHostMallocDefault));
+        for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
+        if (const char *v = getenv("MRG_LDS_CAP")) c->lds_cap = atoi(v);
+        *out = c;
+    });
+}
+
+int mrg_close(mrg_ctx *c) {
+    return guard([&] {
+        if (!c) return;
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+        for (auto &e : c->ev) (void)hipEventDestroy(e);
+        (void)hipFree(c->d_cnt);
+        (void)hipHostFree(c->h_cnt);
+        if (c->own) (void)hipStreamDestroy(c->own);
+        delete c;
+    });
+}
+
+int mrg_set_stream(mrg_ctx *c, void *hip_stream) {
+    return guard([&] {
+        if (!c) raise(MRG_EINVAL, "null context");
+        sync(c);
+        c->stream = hip_stream ? (hipStream_t)hip_stream : c->own;
+    });
+}
+
+int mrg_set_timing(mrg_ctx *c, int enable) {
+    return guard([&] {
+        if (!c) raise(MRG_EINVAL, "null context");
+        c->timing = enable != 0;
+    });
+}
+
+int mrg_get_stats(mrg_ctx *c, mrg_stats *out) {
+    return guard([&] {
+        if (!c || !out) raise(MRG_EINVAL, "null argument");
+        *out = c->st;
+    });
+}
+
+int mrg_job_begin(mrg_ctx *c, int app, uint32_t n_reduce, uint32_t flags) {
+    return guard([&] {
+        if (!c) raise(MRG_EINVAL, "null context");
+        HIPCHK(hipSetDevice(c->device));
+        job_begin(c, app, n_reduce, flags);
+    });
+}
+
+int mrg_job_set_doc_names(mrg_ctx *c, const char *const *names, uint32_t n_names) {
+    return guard([&] {
+        need_job(c);
+        check_names(names, n_names);
+        c->names.assign(names, names + n_names);
+    });
+}
+
+int mrg_job_set_input(mrg_ctx *c, const uint8_t *d_bytes, const uint64_t *h_doc_off, uint32_t n_docs,
+                      const uint32_t *h_doc_ids) {
+    return guard([&] {
+        need_job(c);
+        if (n_docs && (!d_bytes || !h_doc_off)) raise(MRG_EINVAL, "null input");
+        if ((uintptr_t)d_bytes & 15u) raise(MRG_EINVAL, "input buffer must be 16-byte aligned");
+        for (uint32_t i = 0; i < n_docs; ++i)
+            if (h_doc_off[i + 1] < h_doc_off[i]) raise(MRG_EINVAL, "document offsets must be non-decreasing");
+        c->d_in = d_bytes;
+        c->doc_off.assign(h_doc_off, h_doc_off + n_docs + 1);
+        if (h_doc_ids) c->doc_ids.assign(h_doc_ids, h_doc_ids + n_docs);
+        else c->doc_ids.clear();
+        c->mapped = c->reduced = false;
+    });
+}
+
+int mrg_job_map(mrg_ctx *c) {
+    return guard([&] { job_map(c); });
+}
+
+int mrg_job_export_sizes(mrg_ctx *c, uint32_t n_owners, uint64_t *h_rec_counts, uint64_t *h_heap_bytes) {
+    return guard([&] { export_sizes(c, n_owners, h_rec_counts, h_heap_bytes); });
+}
+
+int mrg_job_export(mrg_ctx *c, void *d_rec, void *d_heap) {
+    return guard([&] { export_pack(c, d_rec, d_heap); });
+}
+
+int mrg_job_import(mrg_ctx *c, const void *d_rec, uint64_t n_rec, const void *d_heap, uint64_t heap_bytes,
+                   const uint64_t *h_seg_recs, const uint64_t *h_seg_heap, uint32_t n_segs) {
+    return guard([&] { job_import(c, d_rec, n_rec, d_heap, heap_bytes, h_seg_recs, h_seg_heap, n_segs); });
+}
+
+int mrg_job_reduce(mrg_ctx *c, uint64_t *h_out_bytes) {
+    return guard([&] {
+        job_reduce(c);
+        if (h_out_bytes) *h_out_bytes = c->out_bytes;
+    });
+}
+
+int mrg_job_output(mrg_ctx *c, const uint8_t **d_out, uint64_t *h_part_off) {
+    return guard([&] {
+        need_job(c);
+        if (!c->reduced) raise(MRG_EINVAL, "no output: call mrg_job_reduce first");
+        if (d_out) *d_out = c->d_out;
+        if (h_part_off) memcpy(h_part_off, c->part_off.data(), 8ull * (c->R + 1));
+    });
+}
+
+int mrg_job_copy_output(mrg_ctx *c, uint8_t *h_dst, uint64_t cap) {
+    return guard([&] {
+        need_job(c);
+        if (!c->reduced) raise(MRG_EINVAL, "no output: call mrg_job_reduce first");
+        if (cap < c->out_bytes) raise(MRG_EINVAL, "destination too small (%llu < %llu)", (unsigned long long)cap,
+                                      (unsigned long long)c->out_bytes);
+        if (c->out_bytes)
+            HIPCHK(hipMemcpyAsync(h_dst, c->d_out, c->out_bytes, hipMemcpyDeviceToHost, c->stream));
+        sync(c);
+    });
+}
+
+// ---- plugin surface (host buffers)
+
+int mrg_map(mrg_ctx *c, int app, const uint8_t *h_bytes, size_t n, const char *doc, uint32_t doc_id,
+            uint32_t n_reduce, uint32_t flags, mrg_parts **out) {
+    return guard([&] {
+        if (!c || !out || (n && !h_bytes)) raise(MRG_EINVAL, "null argument");
+        (void)doc;
+        HIPCHK(hipSetDevice(c->device));
+        job_begin(c, app, n_reduce, flags);
+        uint8_t *d = pget<uint8_t>(c->pool, n + 64);
+        if (n) HIPCHK(hipMemcpyAsync(d, h_bytes, n, hipMemcpyHostToDevice, c->stream));
+        const uint64_t off[2] = {0, n};
+        c->d_in = d;
+        c->doc_off.assign(off, off + 2);
+        c->doc_ids.assign(1, doc_id);
+        try {
+            job_map(c);
+        } catch (...) {
+            c->pool.put(d);
+            throw;
+        }
+        export_sizes(c, n_reduce, nullptr, nullptr);
+        mrg_parts *P = new mrg_parts();
+        P->R = n_reduce;
+        P->rec_off.assign(n_reduce + 1, 0);
+        P->heap_off.assign(n_reduce + 1, 0);
+        for (uint32_t r = 0; r < n_reduce; ++r) {
+            P->rec_off[r + 1] = P->rec_off[r] + c->exp_rec[r];
+            P->heap_off[r + 1] = P->heap_off[r] + c->exp_heap[r];
+        }
+        XRec *dx = pget<XRec>(c->pool, P->rec_off[n_reduce]);
+        uint8_t *dh = pget<uint8_t>(c->pool, P->heap_off[n_reduce] + 1);
+        export_pack(c, dx, dh);
+        P->recs.resize(P->rec_off[n_reduce] * sizeof(XRec));
+        P->heap.resize(P->heap_off[n_reduce]);
+        if (!P->recs.empty())
+            HIPCHK(hipMemcpyAsync(P->recs.data(), dx, P->recs.size(), hipMemcpyDeviceToHost, c->stream));
+        if (!P->heap.empty())
+            HIPCHK(hipMemcpyAsync(P->heap.data(), dh, P->heap.size(), hipMemcpyDeviceToHost, c->stream));
+        sync(c);
+        c->pool.put(dx);
+        c->pool.put(dh);
+        c->pool.put(d);
+        *out = P;
+    });
+}
+
+int mrg_parts_get(const mrg_parts *P, uint32_t r, const uint8_t **h_rec, uint64_t *n_rec, const uint8_t **h_heap,
+                  uint64_t *heap_bytes) {
+    return guard([&] {
+        if (!P || r >= P->R) raise(MRG_EINVAL, "bad parts / partition");
+        if (h_rec) *h_rec = P->recs.data() + P->rec_off[r] * sizeof(XRec);
+        if (n_rec) *n_rec = P->rec_off[r + 1] - P->rec_off[r];
+        if (h_heap) *h_heap = P->heap.data() + P->heap_off[r];
+        if (heap_bytes) *heap_bytes = P->heap_off[r + 1] - P->heap_off[r];
+    });
+}
+
+void mrg_parts_free(mrg_parts *P) { delete P; }
+
+int mrg_reduce(mrg_ctx *c, int app, uint32_t r, const mrg_parts *const *in, size_t k, uint32_t n_reduce,
+               uint32_t flags, const char *const *doc_names, uint32_t n_docs, uint8_t **h_out, size_t *h_out_len) {
+    return guard([&] {
+        if (!c || !h_out || !h_out_len || (k && !in)) raise(MRG_EINVAL, "null argument");
+        if (r >= n_reduce) raise(MRG_EINVAL, "partition %u >= n_reduce %u", r, n_reduce);
+        HIPCHK(hipSetDevice(c->device));
+        job_begin(c, app, n_reduce, flags);
+        if (app == MRG_APP_INDEXER) {
+            check_names(doc_names, n_docs);
+            c->names.assign(doc_names, doc_names + n_docs);
+        }
+        std::vector<uint64_t> seg_rec, seg_heap;
+        std::vector<uint8_t> recs, heap;
+        for (size_t i = 0; i < k; ++i) {
+            const mrg_parts *P = in[i];
+            if (!P || P->R != n_reduce) raise(MRG_EINVAL, "map output %zu has a different n_reduce", i);
+            const uint64_t a = P->rec_off[r], b = P->rec_off[r + 1];
+            const uint64_t ha = P->heap_off[r], hb = P->heap_off[r + 1];
+            recs.insert(recs.end(), P->recs.begin() + a * sizeof(XRec), P->recs.begin() + b * sizeof(XRec));
+            heap.insert(heap.end(), P->heap.begin() + ha, P->heap.begin() + hb);
+            seg_rec.push_back(b - a);
+            seg_heap.push_back(hb - ha);
+        }
+        const uint64_t nrec = recs.size() / sizeof(XRec);
+        uint8_t *dr = pget<uint8_t>(c->pool, recs.size() + 16);
+        uint8_t *dh = pget<uint8_t>(c->pool, heap.size() + 16);
+        if (!recs.empty()) HIPCHK(hipMemcpyAsync(dr, recs.data(), recs.size(), hipMemcpyHostToDevice, c->stream));
+        if (!heap.empty()) HIPCHK(hipMemcpyAsync(dh, heap.data(), heap.size(), hipMemcpyHostToDevice, c->stream));
+        job_import(c, dr, nrec, dh, heap.size(), seg_rec.data(), seg_heap.data(), (uint32_t)seg_rec.size());
+        job_reduce(c);
+        const uint64_t a = c->part_off[r], b = c->part_off[r + 1];
+        uint8_t *o = (uint8_t *)malloc(b - a + 1);
+        if (!o) raise(MRG_ENOMEM, "host allocation failed");
+        if (b > a) HIPCHK(hipMemcpyAsync(o, c->d_out + a, b - a, hipMemcpyDeviceToHost, c->stream));
+        sync(c);
+        c->pool.put(dr);
+        c->pool.put(dh);
+        *h_out = o;
+        *h_out_len = b - a;
+    });
+}
+
+int mrg_run_job(const char *const *files, size_t n_files, uint32_t n_reduce, int app, const char *out_dir,
+                uint32_t flags, int device) {
+    mrg_ctx *c = nullptr;
+    int rc = mrg_open(device, &c);
+    if (rc) return rc;
+    rc = guard([&] {
+        std::vector<uint64_t> off(1, 0);
+        std::vector<std::vector<uint8_t>> data(n_files);
+        for (size_t i = 0; i < n_files; ++i) {
+            FILE *f = fopen(files[i], "rb");   // worker.rs:73 File::open(..).unwrap()
+            if (!f) raise(MRG_EIO, "cannot open %s", files[i]);
+            fseek(f, 0, SEEK_END);
+            const long sz = ftell(f);
+            fseek(f, 0, SEEK_SET);
+            data[i].resize((size_t)sz);
+            const size_t got = sz ? fread(data[i].data(), 1, (size_t)sz, f) : 0;
+            fclose(f);
+            if (got != (size_t)sz) raise(MRG_EIO, "short read on %s", files[i]);
+            off.push_back(off.back() + (uint64_t)sz);
+        }
+        job_begin(c, app, n_reduce, flags);
+        std::vector<const char *> nm(files, files + n_files);
+        check_names(nm.data(), (uint32_t)n_files);
+        c->names.assign(files, files + n_files);
+        uint8_t *d = pget<uint8_t>(c->pool, off.back() + 64);
+        for (size_t i = 0; i < n_files; ++i)
+            if (!data[i].empty())
+                HIPCHK(hipMemcpyAsync(d + off[i], data[i].data(), data[i].size(), hipMemcpyHostToDevice, c->stream));
+        sync(c);
+        c->d_in = d;
+        c->doc_off = off;
+        job_map(c);
+        job_reduce(c);
+        std::vector<uint8_t> out(c->out_bytes);
+        if (c->out_bytes)
+            HIPCHK(hipMemcpyAsync(out.data(), c->d_out, c->out_bytes, hipMemcpyDeviceToHost, c->stream));
+        sync(c);
+        for (uint32_t r = 0; r < n_reduce; ++r) {   // worker.rs:167-168 File::create("mr-{r}.txt")
+            const std::string path = std::string(out_dir) + "/mr-" + std::to_string(r) + ".txt";
+            FILE *f = fopen(path.c_str(), "wb");
+            if (!f) raise(MRG_EIO, "cannot create %s", path.c_str());
+            const uint64_t a = c->part_off[r], b = c->part_off[r + 1];
+            const size_t w = b > a ? fwrite(out.data() + a, 1, b - a, f) : 0;
+            fclose(f);
+            if (w != b - a) raise(MRG_EIO, "short write on %s", path.c_str());
+        }
+        c->pool.put(d);
+    });
+    std::string err = g_err;
+    mrg_close(c);
+    g_err = err;
+    return rc;
+}
+
+void mrg_free(void *p) { free(p); }
+
+int mrg_gen_zipf(mrg_ctx *c, uint8_t *d_dst, uint64_t n_bytes, uint64_t seed, uint64_t file_index, uint32_t vocab,
+                 double s) {
+    return guard([&] {
+        if (!c || (n_bytes && !d_dst)) raise(MRG_EINVAL, "null argument");
+        HIPCHK(hipSetDevice(c->device));
+        if (mrg_gen_zipf_impl(d_dst, n_bytes, seed, file_index, vocab, s, c->stream))
+            raise(MRG_EHIP, "zipf generator failed: %s", hipGetErrorString(hipGetLastError()));
+    });
+}
+
+int mrg_gen_unique(mrg_ctx *c, uint8_t *d_dst, uint64_t n_bytes, uint64_t seed, uint64_t file_index) {
+    return guard([&] {
+        if (!c || (n_bytes && !d_dst)) raise(MRG_EINVAL, "null argument");
+        HIPCHK(hipSetDevice(c->device));
+        if (mrg_gen_unique_impl(d_dst, n_bytes, seed, file_index, c->stream))
+            raise(MRG_EHIP, "unique generator failed: %s", hipGetErrorString(hipGetLastError()));
+    });
+}
+
+}  // extern "C"

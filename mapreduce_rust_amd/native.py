@@ -1,0 +1,256 @@
+"""ctypes binding of libmrgpu.so (include/mrgpu.h).  No CPU fallback: a missing library raises.
+
+Every entry point of the C ABI is bound here with its exact signature; MrgError carries the
+status code and mrg_last_error() text.  Device buffers are passed as raw device pointers (ints);
+callers typically own them as torch CUDA tensors (plumbing only, never in the ABI).
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+APP_WC = 0
+APP_INDEXER = 1
+FLAG_NO_COMPAT_DROP_LAST = 0x1
+XREC_BYTES = 40
+
+OK, EINVAL, EUTF8, EHIP, ENOMEM, EIO = 0, -1, -2, -3, -4, -5
+_CODES = {EINVAL: "EINVAL", EUTF8: "EUTF8", EHIP: "EHIP", ENOMEM: "ENOMEM", EIO: "EIO"}
+
+
+def debug_hash_bits(n):
+    """MRG_FLAG_DEBUG_HASH_BITS(n): truncate internal hashes to n bits (forces collisions)."""
+    return (n & 0xFF) << 8
+
+
+def lib_path():
+    return os.environ.get("MRG_LIB", os.path.join(_HERE, "lib", "libmrgpu.so"))
+
+
+class MrgError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{_CODES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Stats(C.Structure):
+    _fields_ = [("input_bytes", C.c_uint64), ("tokens", C.c_uint64), ("long_tokens", C.c_uint64),
+                ("map_records", C.c_uint64), ("distinct_keys", C.c_uint64), ("output_bytes", C.c_uint64),
+                ("ms_map", C.c_double), ("ms_aggregate", C.c_double), ("ms_sort", C.c_double),
+                ("ms_format", C.c_double), ("map_launches", C.c_uint32), ("reserved", C.c_uint32)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+
+
+_lib = None
+_vp = C.c_void_p
+_u8p = C.POINTER(C.c_uint8)
+_u64p = C.POINTER(C.c_uint64)
+_u32p = C.POINTER(C.c_uint32)
+
+_SIGS = {
+    "mrg_last_error": (C.c_char_p, []),
+    "mrg_version": (C.c_char_p, []),
+    "mrg_open": (C.c_int, [C.c_int, C.POINTER(_vp)]),
+    "mrg_close": (C.c_int, [_vp]),
+    "mrg_set_stream": (C.c_int, [_vp, _vp]),
+    "mrg_get_stats": (C.c_int, [_vp, C.POINTER(Stats)]),
+    "mrg_set_timing": (C.c_int, [_vp, C.c_int]),
+    "mrg_job_begin": (C.c_int, [_vp, C.c_int, C.c_uint32, C.c_uint32]),
+    "mrg_job_set_doc_names": (C.c_int, [_vp, C.POINTER(C.c_char_p), C.c_uint32]),
+    "mrg_job_set_input": (C.c_int, [_vp, _vp, _u64p, C.c_uint32, _u32p]),
+    "mrg_job_map": (C.c_int, [_vp]),
+    "mrg_job_export_sizes": (C.c_int, [_vp, C.c_uint32, _u64p, _u64p]),
+    "mrg_job_export": (C.c_int, [_vp, _vp, _vp]),
+    "mrg_job_import": (C.c_int, [_vp, _vp, C.c_uint64, _vp, C.c_uint64, _u64p, _u64p, C.c_uint32]),
+    "mrg_job_reduce": (C.c_int, [_vp, _u64p]),
+    "mrg_job_output": (C.c_int, [_vp, C.POINTER(_vp), _u64p]),
+    "mrg_job_copy_output": (C.c_int, [_vp, _vp, C.c_uint64]),
+    "mrg_map": (C.c_int, [_vp, C.c_int, C.c_char_p, C.c_size_t, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                          C.POINTER(_vp)]),
+    "mrg_parts_get": (C.c_int, [_vp, C.c_uint32, C.POINTER(_vp), _u64p, C.POINTER(_vp), _u64p]),
+    "mrg_parts_free": (None, [_vp]),
+    "mrg_reduce": (C.c_int, [_vp, C.c_int, C.c_uint32, C.POINTER(_vp), C.c_size_t, C.c_uint32, C.c_uint32,
+                             C.POINTER(C.c_char_p), C.c_uint32, C.POINTER(_vp), C.POINTER(C.c_size_t)]),
+    "mrg_run_job": (C.c_int, [C.POINTER(C.c_char_p), C.c_size_t, C.c_uint32, C.c_int, C.c_char_p, C.c_uint32,
+                              C.c_int]),
+    "mrg_free": (None, [_vp]),
+    "mrg_gen_zipf": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_double]),
+    "mrg_gen_unique": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64]),
+}
+
+
+def load():
+    """Load libmrgpu.so and bind every exported entry point (raises if it is missing)."""
+    global _lib
+    if _lib is None:
+        path = lib_path()
+        if not os.path.exists(path):
+            raise RuntimeError(f"libmrgpu.so not built ({path}); run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(path)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def _check(rc):
+    if rc != OK:
+        raise MrgError(rc, load().mrg_last_error().decode(errors="replace"))
+
+
+def _u64arr(xs):
+    return (C.c_uint64 * max(len(xs), 1))(*xs)
+
+
+class Parts:
+    """One map task's output (mrg_parts): per-partition exchange records + long-key heap."""
+
+    def __init__(self, handle, n_reduce):
+        self.h = handle
+        self.n_reduce = n_reduce
+
+    def get(self, r):
+        L = load()
+        rec, heap = _vp(), _vp()
+        nrec, nheap = C.c_uint64(), C.c_uint64()
+        _check(L.mrg_parts_get(self.h, r, C.byref(rec), C.byref(nrec), C.byref(heap), C.byref(nheap)))
+        return (C.string_at(rec, nrec.value * XREC_BYTES) if nrec.value else b"",
+                C.string_at(heap, nheap.value) if nheap.value else b"")
+
+    def free(self):
+        if self.h:
+            load().mrg_parts_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Context:
+    """One mrg_ctx: a device, a stream, device workspaces, and the current job."""
+
+    def __init__(self, device=0):
+        L = load()
+        h = _vp()
+        _check(L.mrg_open(device, C.byref(h)))
+        self.h = h
+        self.device = device
+        self.n_reduce = 0
+
+    def close(self):
+        if self.h:
+            load().mrg_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_stream(self, stream_ptr):
+        _check(load().mrg_set_stream(self.h, stream_ptr))
+
+    def set_timing(self, on=True):
+        _check(load().mrg_set_timing(self.h, 1 if on else 0))
+
+    def stats(self):
+        s = Stats()
+        _check(load().mrg_get_stats(self.h, C.byref(s)))
+        return s.as_dict()
+
+    # ---- device-resident job
+    def job_begin(self, app, n_reduce, flags=0):
+        _check(load().mrg_job_begin(self.h, app, n_reduce, flags))
+        self.n_reduce = n_reduce
+
+    def set_doc_names(self, names):
+        arr = (C.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
+        _check(load().mrg_job_set_doc_names(self.h, arr, len(names)))
+
+    def set_input(self, dev_ptr, doc_off, doc_ids=None):
+        n = len(doc_off) - 1
+        off = _u64arr(doc_off)
+        ids = (C.c_uint32 * max(n, 1))(*doc_ids) if doc_ids is not None else None
+        _check(load().mrg_job_set_input(self.h, dev_ptr, off, n, ids))
+
+    def map(self):
+        _check(load().mrg_job_map(self.h))
+
+    def export_sizes(self, n_owners):
+        rec = (C.c_uint64 * n_owners)()
+        heap = (C.c_uint64 * n_owners)()
+        _check(load().mrg_job_export_sizes(self.h, n_owners, rec, heap))
+        return list(rec), list(heap)
+
+    def export(self, d_rec, d_heap):
+        _check(load().mrg_job_export(self.h, d_rec, d_heap))
+
+    def import_(self, d_rec, n_rec, d_heap, heap_bytes, seg_recs=None, seg_heap=None):
+        if seg_recs is None:
+            _check(load().mrg_job_import(self.h, d_rec, n_rec, d_heap, heap_bytes, None, None, 0))
+        else:
+            _check(load().mrg_job_import(self.h, d_rec, n_rec, d_heap, heap_bytes, _u64arr(seg_recs),
+                                         _u64arr(seg_heap), len(seg_recs)))
+
+    def reduce(self):
+        n = C.c_uint64()
+        _check(load().mrg_job_reduce(self.h, C.byref(n)))
+        return n.value
+
+    def output(self):
+        d = _vp()
+        off = (C.c_uint64 * (self.n_reduce + 1))()
+        _check(load().mrg_job_output(self.h, C.byref(d), off))
+        return d.value, list(off)
+
+    def copy_output(self):
+        _, off = self.output()
+        buf = C.create_string_buffer(max(off[-1], 1))
+        _check(load().mrg_job_copy_output(self.h, buf, off[-1]))
+        return buf.raw[:off[-1]], off
+
+    def outputs(self):
+        """mr-{r}.txt contents for every partition r."""
+        data, off = self.copy_output()
+        return [data[off[r]:off[r + 1]] for r in range(self.n_reduce)]
+
+    # ---- plugin surface (host buffers)
+    def map_task(self, app, data, doc, doc_id, n_reduce, flags=0):
+        h = _vp()
+        _check(load().mrg_map(self.h, app, data, len(data), doc.encode(), doc_id, n_reduce, flags, C.byref(h)))
+        return Parts(h, n_reduce)
+
+    def reduce_task(self, app, r, parts, n_reduce, flags=0, doc_names=()):
+        arr = (_vp * max(len(parts), 1))(*[p.h for p in parts])
+        names = (C.c_char_p * max(len(doc_names), 1))(*[n.encode() for n in doc_names])
+        out = _vp()
+        n = C.c_size_t()
+        _check(load().mrg_reduce(self.h, app, r, arr, len(parts), n_reduce, flags, names, len(doc_names),
+                                 C.byref(out), C.byref(n)))
+        data = C.string_at(out, n.value) if n.value else b""
+        load().mrg_free(out)
+        return data
+
+    # ---- synthetic inputs (bench)
+    def gen_zipf(self, dev_ptr, n_bytes, seed, file_index, vocab=1 << 20, s=1.1):
+        _check(load().mrg_gen_zipf(self.h, dev_ptr, n_bytes, seed, file_index, vocab, s))
+
+    def gen_unique(self, dev_ptr, n_bytes, seed, file_index):
+        _check(load().mrg_gen_unique(self.h, dev_ptr, n_bytes, seed, file_index))
+
+
+def run_job(files, n_reduce, app=APP_WC, out_dir=".", flags=0, device=0):
+    arr = (C.c_char_p * max(len(files), 1))(*[f.encode() for f in files])
+    _check(load().mrg_run_job(arr, len(files), n_reduce, app, out_dir.encode(), flags, device))

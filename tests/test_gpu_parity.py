@@ -1,0 +1,249 @@
+"""GPU parity: libmrgpu.so (HIP, gfx950) against the committed golden digests and the C oracle.
+
+Bar: bit-exact mr-{r}.txt bytes.  Everything goes through the C ABI (mapreduce_rust_amd.native).
+"""
+import gzip
+import hashlib
+import json
+import os
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = json.load(open(os.path.join(HERE, "golden", "golden.json")))
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import mapreduce_rust_amd as M
+    c = M.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    return [gzip.open(os.path.join(HERE, "golden", "corpus", f"gut-{m}.txt.gz")).read() for m in range(6)]
+
+
+@pytest.mark.parametrize("R", ["10", "1", "3", "64"])
+def test_c1_wc_golden(ctx, corpus, R):
+    from gpu_util import run_wc
+    outs = run_wc(ctx, corpus, int(R))
+    g = GOLDEN["wc"][R]
+    bad = [r for r in range(int(R)) if sha(outs[r]) != g[f"mr-{r}.txt"]]
+    assert not bad, f"partitions differ: {bad}"
+    st = ctx.stats()
+    assert st["tokens"] == sum(GOLDEN["corpus"]["tokens"])
+
+
+def test_c1_matches_oracle_bytes(ctx, corpus):
+    import oracle_lib as O
+    from gpu_util import run_wc
+    outs = run_wc(ctx, corpus, 10)
+    exp = O.wc(corpus, 10, O.FAST)
+    for r in range(10):
+        assert outs[r] == exp[r], r
+
+
+def test_c2_indexer_golden(ctx, corpus):
+    import mapreduce_rust_amd as M
+    from gpu_util import run_wc
+    names = [f"data/gut-{m}.txt" for m in range(6)]
+    outs = run_wc(ctx, corpus, 10, app=M.APP_INDEXER, names=names)
+    for r in range(10):
+        assert sha(outs[r]) == GOLDEN["indexer"]["10"][f"mr-{r}.txt"], r
+
+
+def test_tokenizer_kats(ctx):
+    """Each KAT input as a one-document job, R=1, last group kept: lines = sorted distinct tokens."""
+    import mapreduce_rust_amd as M
+    import oracle_lib as O
+    from gpu_util import run_wc
+    for case in GOLDEN["tokenizer"]:
+        data = case["input"].encode()
+        outs = run_wc(ctx, [data], 1, flags=M.FLAG_NO_COMPAT_DROP_LAST)
+        counts = {}
+        for t in case["tokens"]:
+            counts[t.encode()] = counts.get(t.encode(), 0) + 1
+        exp = b"".join(k + b" " + str(v).encode() + b"\n" for k, v in sorted(counts.items()))
+        assert outs[0] == exp, case["input"]
+        assert O.wc([data], 1)[0] == run_wc(ctx, [data], 1)[0]
+
+
+def test_invalid_utf8_is_an_error(ctx):
+    import mapreduce_rust_amd as M
+    from gpu_util import run_wc
+    for bad in [b"\xff", b"ab\xc0\x80 cd", b"\xed\xa0\x80", b"\xf4\x90\x80\x80", b"abc \xe2\x82", b"\x80x",
+                b"x" * 5000 + b"\xe2\x82" + b" y" * 10, b"a" * 4095 + b"\xa9"]:
+        with pytest.raises(M.MrgError) as ei:
+            run_wc(ctx, [b"fine text", bad], 3)
+        assert ei.value.code == -2
+
+
+def _rand_text(rng, n_tokens, alphabet, seps, max_len=30):
+    out = []
+    for _ in range(n_tokens):
+        L = rng.randint(1, max_len)
+        out.append("".join(rng.choice(alphabet) for _ in range(L)))
+        out.append(rng.choice(seps))
+    return "".join(out).encode("utf-8")
+
+
+ALPHA = list("abcdeXYZ09_") + ["é", "ß", "ж", "中", "̸", "‍", "'", "-", "’", ".", "\u001c", "😀", "²", "ſ", "Å"]
+SEPS = [" ", "\n", "\t", " ", " ", "　", " ", "\u0085", "  ", "\r\n"]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_unicode_vs_oracle(ctx, seed):
+    import oracle_lib as O
+    from gpu_util import run_wc
+    rng = random.Random(seed)
+    docs = [_rand_text(rng, rng.randint(0, 3000), ALPHA[: 6 + seed * 3], SEPS, max_len=[5, 12, 40][seed % 3])
+            for _ in range(rng.randint(1, 5))]
+    for R in (1, 7):
+        assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST)
+
+
+def test_tile_boundaries_and_long_tokens(ctx):
+    """Tokens straddling 4 KiB tiles / 16 B lane segments / the 256 B halo, and > 16 B keys."""
+    import oracle_lib as O
+    from gpu_util import run_wc
+    rng = random.Random(7)
+    parts = []
+    for i in range(3000):
+        L = rng.choice([1, 2, 15, 16, 17, 31, 300, 700, 5000])
+        parts.append(("k%d" % (i % 50)) * (L // 3 + 1))
+        parts.append(rng.choice([" ", "-", " ", "\n", "’", "é "]))
+    data = "".join(parts).encode()
+    for R in (1, 5):
+        assert run_wc(ctx, [data], R) == O.wc([data], R, O.FAST)
+
+
+@pytest.mark.parametrize("bits", [1, 4, 12, 20])
+def test_forced_hash_collisions(ctx, corpus, bits):
+    """Truncated internal hashes: output must be identical (collision-safe tie-breaks)."""
+    import mapreduce_rust_amd as M
+    from gpu_util import run_wc
+    docs = corpus[:2] + [("".join("longprefix_shared_%05d " % (i % 700) for i in range(6000))).encode()]
+    base = run_wc(ctx, docs, 10)
+    got = run_wc(ctx, docs, 10, flags=M.debug_hash_bits(bits))
+    assert got == base
+
+
+def test_empty_inputs(ctx):
+    from gpu_util import run_wc
+    assert run_wc(ctx, [b""], 4) == [b""] * 4
+    assert run_wc(ctx, [b"   \n\t "], 2) == [b""] * 2
+    assert run_wc(ctx, [b"a a a"], 1) == [b""]
+    assert run_wc(ctx, [b"b a a c"], 1) == [b"a 2\nb 1\n"]
+
+
+def test_plugin_surface_map_reduce(ctx, corpus):
+    """mrg_map per file + mrg_reduce per partition == the whole job (worker.rs task structure)."""
+    import mapreduce_rust_amd as M
+    parts = [ctx.map_task(M.APP_WC, corpus[m], f"data/gut-{m}.txt", m, 10) for m in range(6)]
+    for r in range(10):
+        out = ctx.reduce_task(M.APP_WC, r, parts, 10)
+        assert sha(out) == GOLDEN["wc"]["10"][f"mr-{r}.txt"], r
+    for p in parts:
+        p.free()
+
+
+def test_two_owner_exchange_on_one_gpu(ctx, corpus):
+    """Static plan with 2 owners (r % 2): two map shards exported, cross-imported, reduced."""
+    import torch
+    import mapreduce_rust_amd as M
+    from gpu_util import to_device
+    shards = [corpus[0:3], corpus[3:6]]
+    sends = []
+    for sh in shards:
+        t, off = to_device(sh)
+        ctx.job_begin(M.APP_WC, 10)
+        ctx.set_input(t.data_ptr(), off)
+        ctx.map()
+        rec, heap = ctx.export_sizes(2)
+        drec = torch.empty(max(sum(rec), 1) * 40, dtype=torch.uint8, device="cuda:0")
+        dheap = torch.empty(max(sum(heap), 1), dtype=torch.uint8, device="cuda:0")
+        ctx.export(drec.data_ptr(), dheap.data_ptr())
+        sends.append((drec.cpu(), dheap.cpu(), rec, heap))
+    outs = {}
+    for owner in range(2):
+        recs, heaps, sr, sh = [], [], [], []
+        for drec, dheap, rec, heap in sends:
+            ro = sum(rec[:owner]) * 40
+            ho = sum(heap[:owner])
+            recs.append(drec[ro:ro + rec[owner] * 40])
+            heaps.append(dheap[ho:ho + heap[owner]])
+            sr.append(rec[owner])
+            sh.append(heap[owner])
+        R = torch.cat(recs).to("cuda:0")
+        H = torch.cat(heaps + [torch.zeros(1, dtype=torch.uint8)]).to("cuda:0")
+        ctx.job_begin(M.APP_WC, 10)
+        ctx.import_(R.data_ptr(), sum(sr), H.data_ptr(), sum(sh), sr, sh)
+        ctx.reduce()
+        o = ctx.outputs()
+        for r in range(10):
+            if r % 2 == owner:
+                outs[r] = o[r]
+            else:
+                assert o[r] == b""
+    for r in range(10):
+        assert sha(outs[r]) == GOLDEN["wc"]["10"][f"mr-{r}.txt"], r
+
+
+def test_zipf_synthetic_vs_oracle(ctx):
+    import torch
+    import mapreduce_rust_amd as M
+    import oracle_lib as O
+    n = 24 << 20
+    t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
+    ctx.gen_zipf(t.data_ptr(), n, 0x5EED2026, 0, 1 << 16, 1.1)
+    host = t[:n].cpu().numpy().tobytes()
+    ctx.job_begin(M.APP_WC, 64)
+    ctx.set_input(t.data_ptr(), [0, n])
+    ctx.map()
+    ctx.reduce()
+    got = ctx.outputs()
+    exp = O.wc([host], 64, O.FAST)
+    assert got == exp
+
+
+def test_unique_synthetic_vs_oracle(ctx):
+    import torch
+    import mapreduce_rust_amd as M
+    import oracle_lib as O
+    n = 8 << 20
+    t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
+    ctx.gen_unique(t.data_ptr(), n, 0xC5, 3)
+    host = t[:n].cpu().numpy().tobytes()
+    ctx.job_begin(M.APP_WC, 16)
+    ctx.set_input(t.data_ptr(), [0, n])
+    ctx.map()
+    ctx.reduce()
+    assert ctx.outputs() == O.wc([host], 16, O.FAST)
+
+
+def test_run_job_cli_files(tmp_path, corpus):
+    import mapreduce_rust_amd as M
+    d = tmp_path / "data"
+    d.mkdir()
+    files = []
+    for m in range(6):
+        (d / f"gut-{m}.txt").write_bytes(corpus[m])
+        files.append(f"data/gut-{m}.txt")
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        M.native.run_job(files, 10, M.APP_WC, ".")
+    finally:
+        os.chdir(cwd)
+    for r in range(10):
+        assert sha((tmp_path / f"mr-{r}.txt").read_bytes()) == GOLDEN["wc"]["10"][f"mr-{r}.txt"]
