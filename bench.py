@@ -86,6 +86,10 @@ def cpu_baseline(sample, n_reduce):
     return res
 
 
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,6 +117,9 @@ def main():
             ctx.gen_zipf(p, fbytes, a.seed, fi, a.vocab, a.zipf_s)
         else:
             ctx.gen_unique(p, fbytes, a.seed, fi)
+        if rank == 0 and (i % 8 == 7 or i == files - 1):
+            torch.cuda.synchronize(dev)
+            log(f"generated {i + 1}/{files} files of {a.file_mib} MiB")
     torch.cuda.synchronize(dev)
     doc_off = [i * fbytes for i in range(files + 1)]
     doc_ids = [rank * files + i for i in range(files)]
@@ -125,8 +132,11 @@ def main():
             exchange(ctx, world, dev)
         return ctx.reduce()
 
-    for _ in range(a.warmup):
+    for w in range(a.warmup):
+        t_w = time.perf_counter()
         step()
+        if rank == 0:
+            log(f"warmup {w + 1}/{a.warmup}: {time.perf_counter() - t_w:.3f} s  {ctx.stats()}")
     ctx.set_timing(True)
     map_ms = []
     stage = {"ms_map": 0.0, "ms_aggregate": 0.0, "ms_sort": 0.0, "ms_format": 0.0}
@@ -141,6 +151,9 @@ def main():
         map_ms.append(s["ms_map"])
         for k in stage:
             stage[k] += s[k] / a.steps
+        if rank == 0:
+            log(f"step: map {s['ms_map']:.2f} ms, agg {s['ms_aggregate']:.2f}, sort {s['ms_sort']:.2f}, "
+                f"format {s['ms_format']:.2f}")
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -195,6 +208,7 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         n = min(a.cpu_sample_mib * MIB, shard)
         sample = buf[:n].cpu().numpy().tobytes()
+        log(f"cpu baseline on {n // MIB} MiB ...")
         cb = cpu_baseline(sample, a.reduce)
         line["cpu_baseline"] = {"value": round(n / cb["faithful_s"] / 1e9, 6), "unit": "GB/s", "cores": 1,
                                 "kind": "port",

@@ -195,7 +195,7 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
             my_tokens += have ? 1u : 0u;
             const bool is_long = have && tlen > 16u;
             bool tail = false;
-            if (have && !is_long) tail = !table.insert(tk0, tk1, docid, A.hash_bits);
+            if (have && !is_long) tail = !table.insert(tk0, tk1, IDX ? docid : MRG_EMPTY_DOC, A.hash_bits);
             const uint64_t ri = mrg_wave_append(&A.counters[CNT_REC], tail);
             if (tail && ri < A.rcap) {
                 A.rk0[ri] = tk0; A.rk1[ri] = tk1; A.rcnt[ri] = 1u;

@@ -85,6 +85,13 @@ def load():
     """Load libmrgpu.so and bind every exported entry point (raises if it is missing)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: when torch (the device-memory / stream / torch.distributed
+        # plumbing) is present, import it first so libmrgpu.so binds to the libamdhip64.so.7 torch
+        # already mapped (same soname) instead of loading a second runtime beside it.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         path = lib_path()
         if not os.path.exists(path):
             raise RuntimeError(f"libmrgpu.so not built ({path}); run `python -c 'import __graft_entry__ as g; g.build()'`")
