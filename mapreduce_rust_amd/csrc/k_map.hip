@@ -4,18 +4,25 @@
 // White_Space -- fused with the per-token part of write_key_value_to_file (src/mr/worker.rs:127-131).
 // The partition index (worker.rs:129) is computed later, once per DISTINCT key (k_keys.hip), since
 // SipHash(key) % R is a pure function of the key.  Also validates UTF-8 like read_to_string
-// (worker.rs:75): the first invalid byte offset is reported, the job fails with MRG_EUTF8.
+// (worker.rs:75): the first invalid byte offset is reported and the job fails with MRG_EUTF8.
 //
-// Layout: documents back to back in one HBM buffer; each document is cut into 4 KiB tiles; a
-// persistent grid of 256-thread workgroups walks the tiles.  Per tile the workgroup stages
-// [tile - 16 B, tile + 4 KiB + 256 B) into LDS with 16-byte loads (coalesced), then every lane owns a
-// 16-byte segment: tokens whose first codepoint starts in the segment are the lane's; a lane walks
-// its tokens (continuing past the segment end through LDS, or HBM beyond the halo) and packs the
-// first 16 key bytes big-endian into (k0, k1).
-// Keys of <= 16 bytes are inserted into a workgroup-private LDS hash table (exact: the packed key
-// IS the identity, no fingerprint); count += 1.  Insert misses (table region full) become records
-// in HBM.  Keys > 16 bytes become long-token records (start, raw length, doc) resolved by the
-// collision-safe fingerprint sort (k_keys.hip).  At the end every LDS table is flushed as records.
+// Layout: documents back to back in one HBM buffer; each document is cut into 4 KiB
+// tiles on a 16-byte-aligned grid; a persistent grid of 256-thread workgroups walks the tiles.  Per
+// tile the workgroup stages [tile - 16 B, tile + 4 KiB + 256 B) into LDS with 16-byte loads.
+//
+// ASCII tiles (the common case; wave-uniform test) take the fast path:
+//   1. every lane classifies one 16-byte segment through a 128-entry LDS LUT into an interleaved
+//      32-bit mask (bit 2k = byte k is \w, bit 2k+1 = byte k is White_Space);
+//   2. token starts = non-space bytes after a space: mask arithmetic; each wave compacts its starts
+//      into an LDS queue (wave prefix sum) so that all 64 lanes then work on one token each;
+//   3. per token: end = next space bit, key = the \w bytes -- contiguous in > 98% of tokens
+//      (deleted X bytes only at the edges, e.g. "word,"), read as 3 x 8 B from LDS and packed
+//      big-endian into (k0, k1); anything else (interior deletions like "don't", > 16 B, tokens
+//      running past the halo) takes the exact per-codepoint walker.
+// Non-ASCII tiles use the per-codepoint walker for every token (UTF-8 decode + class table).
+// Keys of <= 16 bytes are inserted into a workgroup-private LDS hash table (exact: the packed key IS
+// the identity, no fingerprint); misses become records in HBM.  Keys > 16 bytes become long-token
+// records (start, raw length, doc) resolved by the collision-safe fingerprint sort (k_keys.hip).
 #include "mrg_device.h"
 #include "mrg_internal.h"
 
@@ -26,9 +33,14 @@ constexpr int SEG = MRG_MAP_SEG;
 constexpr int TILE = MRG_MAP_TILE;
 constexpr int HALO = MRG_MAP_HALO;
 constexpr int BEHIND = MRG_MAP_BEHIND;
-constexpr int TILE_LDS = BEHIND + TILE + HALO + 32;   // staged window incl. 16-B alignment slack
+constexpr int NSEG = (TILE + HALO) / SEG;           // classified segments: tile + halo
+constexpr int LDS_BYTES = BEHIND + TILE + HALO + 32;
+constexpr int QCAP = WG / 4 * SEG / 2;              // tokens per wave per tile <= 512
 constexpr int MAX_PROBE = 8;
+constexpr uint64_t SBITS = 0xAAAAAAAAAAAAAAAAull;    // odd bits: White_Space flags
+constexpr uint64_t WBITS = 0x5555555555555555ull;    // even bits: \w flags
 
+// LDS-staged window: byte a lives at lds[a - wbase] when lo <= a < hi, else it is read from HBM.
 struct Window {
     const uint8_t *lds;
     const uint8_t *g;
@@ -42,10 +54,9 @@ __device__ __forceinline__ void report_error(unsigned long long *counters, uint6
     atomicMin(&counters[CNT_ERRPOS], (unsigned long long)pos);
 }
 
-// Workgroup LDS table, open addressing with a monotone claim protocol:
-// a slot goes EMPTY -> k0 set -> k1 set (-> doc set) and never back; a key may complete a slot
-// whose already-set words equal its own.  Two lanes racing on one slot therefore agree on its
-// owner, and every key lives in exactly one slot without locks.
+// Workgroup LDS table, open addressing with a monotone claim protocol: a slot goes
+// EMPTY -> k0 set -> k1 set (-> doc set) and never back; a key may complete a slot whose set words
+// equal its own.  Lanes racing on one slot agree on its owner; every key lives in one slot; no locks.
 template <int CAP, bool IDX>
 struct LdsTable {
     unsigned long long *k0, *k1;
@@ -77,21 +88,83 @@ struct LdsTable {
     }
 };
 
+// Walk ONE token whose first codepoint starts at `a` (the codepoint before `a` is White_Space or the
+// document start): decode codepoints until White_Space or the document end, keep \w bytes.
+// Returns false on invalid UTF-8 (reported).  *end = first byte after the token.
+template <class RD>
+__device__ __forceinline__ bool walk_token(const RD &rd, uint64_t a, uint64_t doc_hi, unsigned long long *counters,
+                                           uint64_t &k0, uint64_t &k1, uint32_t &L, uint64_t &end) {
+    k0 = 0;
+    k1 = 0;
+    L = 0;
+    uint64_t p = a;
+    while (p < doc_hi) {
+        uint32_t cp, raw;
+        const int l = mrg_utf8_decode(rd, p, doc_hi, &cp, &raw);
+        if (!l) {
+            report_error(counters, p);
+            end = p;
+            return false;
+        }
+        const uint32_t c = mrg_uclass(cp);
+        if (c == MRG_CLS_S) break;
+        if (c == MRG_CLS_W) {
+            for (int b = 0; b < l; ++b) {
+                mrg_key_append(k0, k1, L, (raw >> (8 * b)) & 0xFFu);
+                ++L;
+            }
+        }
+        p += (uint64_t)l;
+    }
+    end = p;
+    return true;
+}
+
+// One round of token emission by a whole wave (all 64 lanes must call it): LDS-table insert of short
+// keys, HBM records for misses and for long keys.
+template <int CAP, bool IDX>
+__device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> &table, bool have, uint64_t tk0,
+                                           uint64_t tk1, uint32_t tlen, uint64_t tstart, uint32_t traw,
+                                           uint32_t docid) {
+    const bool is_long = have && tlen > 16u;
+    bool tail = false;
+    if (have && !is_long) tail = !table.insert(tk0, tk1, IDX ? docid : MRG_EMPTY_DOC, A.hash_bits);
+    const uint64_t ri = mrg_wave_append(&A.counters[CNT_REC], tail);
+    if (tail && ri < A.rcap) {
+        A.rk0[ri] = tk0;
+        A.rk1[ri] = tk1;
+        A.rcnt[ri] = 1u;
+        if (IDX) A.rdoc[ri] = docid;
+    }
+    const uint64_t li = mrg_wave_append(&A.counters[CNT_LONG], is_long);
+    if (is_long && li < A.lcap) {
+        A.lstart[li] = tstart;
+        A.llen[li] = traw;
+        A.ldoc[li] = docid;
+    }
+}
+
 template <int CAP, bool IDX>
 __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_tile[TILE_LDS];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[LDS_BYTES];
+    __shared__ uint32_t s_mask[NSEG + 2];
+    __shared__ uint16_t s_queue[WG / 64][QCAP];
+    __shared__ uint8_t s_lut[128];
     __shared__ unsigned long long s_k0[CAP];
     __shared__ unsigned long long s_k1[CAP];
     __shared__ unsigned int s_cnt[CAP];
     __shared__ unsigned int s_doc[IDX ? CAP : 1];
 
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
     for (int i = tid; i < CAP; i += WG) {
         s_k0[i] = MRG_EMPTY_K0;
         s_k1[i] = MRG_EMPTY_K1;
         s_cnt[i] = 0;
         if (IDX) s_doc[i] = MRG_EMPTY_DOC;
     }
+    if (tid < 128) s_lut[tid] = (uint8_t)(mrg_uclass((uint32_t)tid) == MRG_CLS_W ? 1u
+                                          : (mrg_uclass((uint32_t)tid) == MRG_CLS_S ? 2u : 0u));
     LdsTable<CAP, IDX> table{s_k0, s_k1, s_cnt, s_doc};
     uint64_t my_tokens = 0;
 
@@ -104,106 +177,193 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
         }
         const uint32_t d = lo_d;
         const uint64_t doc_lo = A.doc_off[d], doc_hi = A.doc_off[d + 1];
-        const uint64_t t0 = doc_lo + (c - A.chunk_base[d]) * (uint64_t)TILE;
-        const uint64_t t1 = min(t0 + (uint64_t)TILE, doc_hi);
+        const uint64_t At = (doc_lo & ~15ull) + (c - A.chunk_base[d]) * (uint64_t)TILE;  // aligned tile base
+        const uint64_t t0 = max(At, doc_lo);
+        const uint64_t t1 = min(At + (uint64_t)TILE, doc_hi);
         const uint32_t docid = A.doc_id ? A.doc_id[d] : d;
 
         Window W;
         W.lds = s_tile;
         W.g = A.in;
-        W.lo = t0 - min((uint64_t)BEHIND, t0 - doc_lo);
+        W.wbase = At - (uint64_t)BEHIND;                 // may wrap below 0: only differences are used
+        W.lo = max(doc_lo, At >= (uint64_t)BEHIND ? At - BEHIND : 0ull);
         W.hi = min(t1 + (uint64_t)HALO, doc_hi);
-        W.wbase = W.lo & ~15ull;
-        const uint32_t nvec = (uint32_t)((((W.hi + 15u) & ~15ull) - W.wbase) >> 4);
+        const uint64_t load_lo = W.lo & ~15ull;
+        const uint32_t v0 = (uint32_t)((load_lo - W.wbase) >> 4);
+        const uint32_t v1 = (uint32_t)((((W.hi + 15u) & ~15ull) - W.wbase) >> 4);
 
         __syncthreads();  // previous tile fully consumed
-        for (uint32_t v = tid; v < nvec; v += WG)
-            reinterpret_cast<uint4 *>(s_tile)[v] = reinterpret_cast<const uint4 *>(A.in + W.wbase)[v];
-        __syncthreads();
-
-        // ---- lane segment
-        const uint64_t s0 = t0 + (uint64_t)tid * SEG;
-        const uint64_t s1 = min(s0 + (uint64_t)SEG, t1);
-        bool done = s0 >= t1;
-        uint64_t p = s0;
-        bool prevS = true;
-        if (!done && s0 > doc_lo) {
-            // skip continuation bytes: they belong to a codepoint that starts before s0
-            uint32_t j = 0;
-            while (s0 + j < s1 && mrg_is_cont(W(s0 + j))) ++j;
-            p = s0 + j;
-            // find the lead of the codepoint ending at p - 1 (at most 3 continuation bytes back)
-            uint32_t k = 1;
-            while (k <= 3 && p - k >= doc_lo && mrg_is_cont(W(p - k))) ++k;
-            const uint64_t q = p - k;
-            if (q < doc_lo || mrg_is_cont(W(q))) {
-                report_error(A.counters, s0);   // orphan continuation bytes
-                done = true;
-            } else {
-                uint32_t cp, raw;
-                const int l = mrg_utf8_decode(W, q, doc_hi, &cp, &raw);
-                if (j > 0 && (l == 0 || q + (uint64_t)l != p)) {
-                    report_error(A.counters, s0);   // continuation bytes not covered by their lead
+        bool nonascii = false;
+        for (uint32_t v = v0 + tid; v < v1; v += WG) {
+            const uint4 x = reinterpret_cast<const uint4 *>(A.in + W.wbase)[v];
+            reinterpret_cast<uint4 *>(s_tile)[v] = x;
+            nonascii |= ((x.x | x.y | x.z | x.w) & 0x80808080u) != 0u;
+        }
+        if (__syncthreads_or(nonascii)) {
+            // ================= generic path: per-lane codepoint walker =================
+            const uint64_t sg0 = At + (uint64_t)tid * SEG;
+            const uint64_t s0 = max(sg0, t0);
+            const uint64_t s1 = min(sg0 + (uint64_t)SEG, t1);
+            bool done = s0 >= s1;
+            uint64_t p = s0;
+            bool prevS = true;
+            if (!done && s0 > doc_lo) {
+                uint32_t j = 0;  // continuation bytes belong to a codepoint that starts before s0
+                while (s0 + j < s1 && mrg_is_cont(W(s0 + j))) ++j;
+                p = s0 + j;
+                uint32_t k = 1;  // lead of the codepoint ending at p - 1 (at most 3 continuation bytes back)
+                while (k <= 3 && p - k >= doc_lo && mrg_is_cont(W(p - k))) ++k;
+                const uint64_t q = p - k;
+                if (q < doc_lo || mrg_is_cont(W(q))) {
+                    report_error(A.counters, s0);  // orphan continuation bytes
                     done = true;
+                } else {
+                    uint32_t cp, raw;
+                    const int l = mrg_utf8_decode(W, q, doc_hi, &cp, &raw);
+                    if (j > 0 && (l == 0 || q + (uint64_t)l != p)) {
+                        report_error(A.counters, s0);
+                        done = true;
+                    }
+                    prevS = (l > 0 && q + (uint64_t)l == p) ? (mrg_uclass(cp) == MRG_CLS_S) : false;
                 }
-                // an invalid lead itself is reported by the lane that owns it
-                prevS = (l > 0 && q + (uint64_t)l == p) ? (mrg_uclass(cp) == MRG_CLS_S) : false;
+                if (p >= s1) done = true;
             }
-            if (p >= s1) done = true;
+            for (;;) {
+                bool have = false;
+                uint64_t tk0 = 0, tk1 = 0, tstart = 0;
+                uint32_t tlen = 0, traw = 0;
+                while (!done) {
+                    if (p >= s1) { done = true; break; }
+                    uint32_t cp, raw;
+                    const int l = mrg_utf8_decode(W, p, doc_hi, &cp, &raw);
+                    if (!l) { report_error(A.counters, p); done = true; break; }
+                    const uint32_t cl = mrg_uclass(cp);
+                    if (cl == MRG_CLS_S) { prevS = true; p += (uint64_t)l; continue; }
+                    if (!prevS) { p += (uint64_t)l; continue; }
+                    uint64_t a0, a1, e;
+                    uint32_t L;
+                    if (!walk_token(W, p, doc_hi, A.counters, a0, a1, L, e)) { done = true; break; }
+                    prevS = false;
+                    const uint64_t start = p;
+                    p = e;
+                    if (L > 0) {
+                        have = true;
+                        tk0 = a0; tk1 = a1; tlen = L; tstart = start; traw = (uint32_t)(e - start);
+                        break;
+                    }
+                }
+                if (!__any(have)) break;
+                my_tokens += have ? 1u : 0u;
+                emit_round(A, table, have, tk0, tk1, tlen, tstart, traw, docid);
+            }
+            continue;
         }
 
-        // ---- token rounds: every lane produces at most one token per round, then the wave
-        //      inserts all of them together (full-wave LDS atomics instead of 1-lane divergence)
-        for (;;) {
-            bool have = false;
-            uint64_t tk0 = 0, tk1 = 0, tstart = 0;
-            uint32_t tlen = 0, traw = 0;
-            while (!done) {
-                if (p >= s1) { done = true; break; }
-                uint32_t cp, raw;
-                int l = mrg_utf8_decode(W, p, doc_hi, &cp, &raw);
-                if (!l) { report_error(A.counters, p); done = true; break; }
-                uint32_t c = mrg_uclass(cp);
-                if (c == MRG_CLS_S) { prevS = true; p += (uint64_t)l; continue; }
-                if (!prevS) { p += (uint64_t)l; continue; }
-                // token starts at p: walk to the next White_Space codepoint or the document end
-                const uint64_t start = p;
-                uint64_t a0 = 0, a1 = 0;
-                uint32_t L = 0;
-                for (;;) {
-                    if (c == MRG_CLS_W) {
-                        for (int b = 0; b < l; ++b) {
-                            mrg_key_append(a0, a1, L, (raw >> (8 * b)) & 0xFFu);
-                            ++L;
+        // ================= ASCII fast path =================
+        // 1. classify: segment g covers [At + 16 g, +16); bytes outside [doc_lo, W.hi) count as space
+        for (int g = tid; g < NSEG + 2; g += WG) {
+            const uint64_t B = At + (uint64_t)g * SEG;
+            uint32_t m = 0xAAAAAAAAu;
+            if (g < NSEG && B < W.hi) {
+                const uint4 x = reinterpret_cast<const uint4 *>(s_tile)[1 + g];
+                const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+                m = 0;
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    m |= (uint32_t)s_lut[(xs[k >> 2] >> (8 * (k & 3))) & 0x7Fu] << (2 * k);
+                const uint32_t lo_inv = doc_lo > B ? (uint32_t)min<uint64_t>(doc_lo - B, 16) : 0u;
+                const uint32_t hi_ok = (uint32_t)min<uint64_t>(W.hi - B, 16);
+                const uint32_t vhi = hi_ok >= 16u ? 0xFFFFFFFFu : ((1u << (2u * hi_ok)) - 1u);
+                const uint32_t vlo = lo_inv >= 16u ? 0xFFFFFFFFu : ((1u << (2u * lo_inv)) - 1u);
+                const uint32_t valid = vhi & ~vlo;
+                m = (m & valid) | (0xAAAAAAAAu & ~valid);
+            }
+            s_mask[g] = m;
+        }
+        uint32_t prevS_tile = 1u;  // class of the byte before the tile
+        if (At > doc_lo) prevS_tile = (s_lut[s_tile[BEHIND - 1] & 0x7Fu] >> 1) & 1u;
+        __syncthreads();
+
+        // 2. token starts of this lane's tile segment -> per-wave queue
+        {
+            const uint32_t m = s_mask[tid];
+            const uint32_t prev = tid ? (s_mask[tid - 1] >> 31) : prevS_tile;
+            const uint32_t IS = m & 0xAAAAAAAAu;
+            uint32_t st = ~IS & ((IS << 2) | (prev << 1)) & 0xAAAAAAAAu;
+            if (At + (uint64_t)tid * SEG >= t1) st = 0;
+            const uint32_t cnt = __popc(st);
+            uint32_t incl = cnt;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = __shfl_up(incl, o);
+                if (lane >= o) incl += u;
+            }
+            uint32_t pos = incl - cnt;
+            while (st) {
+                const uint32_t k = (uint32_t)__builtin_ctz(st) >> 1;
+                s_queue[wv][pos++] = (uint16_t)(tid * SEG + k);
+                st &= st - 1u;
+            }
+            const uint32_t total = __shfl(incl, 63);
+            __syncthreads();
+
+            // 3. tokens of the queue, one per lane per round
+            for (uint32_t base = 0; base < total; base += 64) {
+                const uint32_t q = base + lane;
+                bool have = false;
+                uint64_t tk0 = 0, tk1 = 0, tstart = 0;
+                uint32_t tlen = 0, traw = 0;
+                if (q < total) {
+                    const uint32_t s = s_queue[wv][q];
+                    const uint32_t g = s >> 4, i = s & 15u;
+                    const uint64_t win = (uint64_t)s_mask[g] | ((uint64_t)s_mask[g + 1] << 32);
+                    const uint64_t sr = (win & SBITS) >> (2u * i + 2u);
+                    bool slow = true;
+                    uint32_t n = 0;
+                    if (sr) {
+                        n = ((uint32_t)__builtin_ctzll(sr) >> 1) + 1u;  // raw length
+                        const uint64_t e = At + s + n;
+                        slow = (e >= W.hi) && (W.hi < doc_hi);        // ended at the staged edge
+                    }
+                    if (!slow) {
+                        const uint64_t w = (win >> (2u * i)) & WBITS & ((1ull << (2u * n)) - 1u);
+                        if (w) {
+                            const uint32_t first = (uint32_t)__builtin_ctzll(w) >> 1;
+                            const uint32_t last = (63u - (uint32_t)__builtin_clzll(w)) >> 1;
+                            const uint32_t L = last - first + 1u;
+                            const uint64_t pat = (WBITS >> (64u - 2u * L)) << (2u * first);
+                            if (w != pat) {
+                                slow = true;  // a deleted byte inside the token: exact walker
+                            } else {
+                                have = true;
+                                tlen = L;
+                                tstart = At + s;
+                                traw = n;
+                                if (L <= 16u) {
+                                    const uint32_t off = BEHIND + s + first;
+                                    const uint64_t *q64 = reinterpret_cast<const uint64_t *>(s_tile + (off & ~7u));
+                                    const uint64_t x0 = q64[0], x1 = q64[1], x2 = q64[2];
+                                    const uint32_t sh = (off & 7u) * 8u;
+                                    uint64_t lo = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
+                                    uint64_t hi = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
+                                    if (L < 8u) { lo &= (1ull << (8u * L)) - 1u; hi = 0; }
+                                    else if (L < 16u) hi &= (1ull << (8u * (L - 8u))) - 1u;
+                                    tk0 = __builtin_bswap64(lo);
+                                    tk1 = __builtin_bswap64(hi);
+                                }
+                            }
                         }
                     }
-                    p += (uint64_t)l;
-                    if (p >= doc_hi) break;
-                    l = mrg_utf8_decode(W, p, doc_hi, &cp, &raw);
-                    if (!l) { report_error(A.counters, p); done = true; break; }
-                    c = mrg_uclass(cp);
-                    if (c == MRG_CLS_S) break;
+                    if (slow) {
+                        uint64_t a0, a1, e;
+                        uint32_t L;
+                        if (walk_token(W, At + s, doc_hi, A.counters, a0, a1, L, e) && L > 0) {
+                            have = true;
+                            tk0 = a0; tk1 = a1; tlen = L; tstart = At + s; traw = (uint32_t)(e - (At + s));
+                        }
+                    }
                 }
-                prevS = false;
-                if (L > 0 && !done) {
-                    have = true;
-                    tk0 = a0; tk1 = a1; tlen = L; tstart = start; traw = (uint32_t)(p - start);
-                    break;
-                }
-            }
-            if (!__any(have)) break;
-            my_tokens += have ? 1u : 0u;
-            const bool is_long = have && tlen > 16u;
-            bool tail = false;
-            if (have && !is_long) tail = !table.insert(tk0, tk1, IDX ? docid : MRG_EMPTY_DOC, A.hash_bits);
-            const uint64_t ri = mrg_wave_append(&A.counters[CNT_REC], tail);
-            if (tail && ri < A.rcap) {
-                A.rk0[ri] = tk0; A.rk1[ri] = tk1; A.rcnt[ri] = 1u;
-                if (IDX) A.rdoc[ri] = docid;
-            }
-            const uint64_t li = mrg_wave_append(&A.counters[CNT_LONG], is_long);
-            if (is_long && li < A.lcap) {
-                A.lstart[li] = tstart; A.llen[li] = traw; A.ldoc[li] = docid;
+                my_tokens += have ? 1u : 0u;
+                emit_round(A, table, have, tk0, tk1, tlen, tstart, traw, docid);
             }
         }
     }
@@ -215,14 +375,15 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
         const bool full = s_k0[i] != MRG_EMPTY_K0;
         const uint64_t ri = mrg_wave_append(&A.counters[CNT_REC], full);
         if (full && ri < A.rcap) {
-            A.rk0[ri] = s_k0[i]; A.rk1[ri] = s_k1[i]; A.rcnt[ri] = s_cnt[i];
+            A.rk0[ri] = s_k0[i];
+            A.rk1[ri] = s_k1[i];
+            A.rcnt[ri] = s_cnt[i];
             if (IDX) A.rdoc[ri] = s_doc[i];
         }
     }
-    // token count
     uint64_t t = my_tokens;
     for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off);
-    if (mrg_lane() == 0) atomicAdd(&A.counters[CNT_TOKENS], (unsigned long long)t);
+    if (lane == 0) atomicAdd(&A.counters[CNT_TOKENS], (unsigned long long)t);
 }
 
 // Long tokens: filter the raw token bytes (drop X codepoints), fingerprint (FNV-1a-64 of the key
@@ -286,6 +447,12 @@ void mrg_launch_map(const MapArgs &a, int app, int grid, int lds_cap, hipStream_
     else { if (idx) launch_map_t<1024, true>(a, grid, s); else launch_map_t<1024, false>(a, grid, s); }
 }
 
+// tiles of a document [lo, hi): on the 16-byte grid starting at lo & ~15
+uint64_t mrg_map_tiles(uint64_t lo, uint64_t hi) {
+    if (hi <= lo) return 0;
+    return (hi - (lo & ~15ull) + TILE - 1) / TILE;
+}
+
 int mrg_map_max_grid(int app, int lds_cap, int device) {
     int ncu = 256;
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
@@ -310,9 +477,9 @@ void mrg_launch_long_prep(const uint8_t *base, const uint64_t *start, const uint
                        k1, flen, flen64, fp, hash_bits);
 }
 
-void mrg_launch_long_gather(const uint8_t *in, const uint64_t *lstart, const uint32_t *llen, uint64_t n,
+void mrg_launch_long_gather(const uint8_t *base, const uint64_t *start, const uint32_t *rawlen, uint64_t n,
                             const uint64_t *dst_off, uint8_t *heap, hipStream_t s) {
     if (!n) return;
-    hipLaunchKernelGGL(k_long_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, lstart, llen, n,
+    hipLaunchKernelGGL(k_long_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, base, start, rawlen, n,
                        dst_off, heap);
 }

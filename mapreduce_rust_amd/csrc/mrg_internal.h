@@ -72,6 +72,7 @@ struct LongItems {
 
 // ---- k_map.hip
 void mrg_launch_map(const MapArgs &a, int app, int grid, int lds_cap, hipStream_t s);
+uint64_t mrg_map_tiles(uint64_t doc_lo, uint64_t doc_hi);  // 4 KiB tiles of a document (16-B grid)
 int mrg_map_max_grid(int app, int lds_cap, int device);
 void mrg_launch_long_prep(const uint8_t *base, const uint64_t *start, const uint32_t *rawlen, uint64_t n,
                           uint64_t *k0, uint64_t *k1, uint32_t *flen, uint64_t *flen64, uint64_t *fp,

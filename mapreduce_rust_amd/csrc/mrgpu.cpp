@@ -317,7 +317,7 @@ void job_map(mrg_ctx *c) {
     const uint32_t nd = (uint32_t)c->doc_off.size() - 1;
     const uint64_t total = c->doc_off[nd] - c->doc_off[0];
     std::vector<uint64_t> cb(nd + 1, 0);
-    for (uint32_t d = 0; d < nd; ++d) cb[d + 1] = cb[d] + (c->doc_off[d + 1] - c->doc_off[d] + MRG_MAP_TILE - 1) / MRG_MAP_TILE;
+    for (uint32_t d = 0; d < nd; ++d) cb[d + 1] = cb[d] + mrg_map_tiles(c->doc_off[d], c->doc_off[d + 1]);
     const uint64_t n_chunks = cb[nd];
     std::vector<uint32_t> ids = c->doc_ids;
     if (ids.empty()) for (uint32_t d = 0; d < nd; ++d) ids.push_back(d);
