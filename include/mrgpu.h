@@ -73,6 +73,7 @@ typedef struct {
     double ms_format;          /* output formatting */
     uint32_t map_launches;     /* map kernel launches in the last mrg_job_map */
     uint32_t reserved;
+    uint64_t overflow_keys;    /* records that took the exact HBM-table overflow path */
 } mrg_stats;
 
 const char *mrg_last_error(void);

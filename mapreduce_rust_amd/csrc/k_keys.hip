@@ -14,6 +14,134 @@ namespace {
 
 inline dim3 grid_for(uint64_t n, int b = 256) { return dim3((unsigned)((n + b - 1) / b)); }
 
+// ---------------------------------------------------------------- per-bucket LDS aggregation
+// One workgroup per hash bucket sums every record of its bucket -- the map kernel's tail chunks
+// (count 1 each) and the bucket's slice of every map workgroup's flushed LDS table -- in an LDS
+// table with the monotone claim protocol.  A key that finds no slot (more distinct keys in the
+// bucket than the table holds) is written to the overflow list; since slots only ever fill, a key
+// that failed once fails always, so the LDS table and the overflow path never share a key.
+constexpr int BA_WG = 512;
+constexpr int BA_CAP = MRG_BA_CAP;
+constexpr int BA_PROBE = 64;
+
+template <bool IDX>
+__device__ __forceinline__ bool ba_insert(unsigned long long *k0, unsigned long long *k1, unsigned long long *cnt,
+                                          unsigned int *doc, uint64_t a, uint64_t b, uint32_t d, uint64_t c,
+                                          uint64_t h) {
+    uint32_t slot = (uint32_t)(h >> 17) & (BA_CAP - 1);
+    for (int p = 0; p < BA_PROBE; ++p) {
+        const unsigned long long x = atomicCAS(&k0[slot], MRG_EMPTY_K0, (unsigned long long)a);
+        if (x == MRG_EMPTY_K0 || x == a) {
+            const unsigned long long y = atomicCAS(&k1[slot], MRG_EMPTY_K1, (unsigned long long)b);
+            if (y == MRG_EMPTY_K1 || y == b) {
+                bool ok = true;
+                if (IDX) {
+                    const unsigned int z = atomicCAS(&doc[slot], MRG_EMPTY_DOC, d);
+                    ok = (z == MRG_EMPTY_DOC || z == d);
+                }
+                if (ok) {
+                    atomicAdd(&cnt[slot], (unsigned long long)c);
+                    return true;
+                }
+            }
+        }
+        slot = (slot + 1u) & (BA_CAP - 1);
+    }
+    return false;
+}
+
+template <bool IDX>
+__global__ __launch_bounds__(BA_WG) void k_bucket_agg(BucketArgs A) {
+    __shared__ unsigned long long s_k0[BA_CAP];
+    __shared__ unsigned long long s_k1[BA_CAP];
+    __shared__ unsigned long long s_cnt[BA_CAP];
+    __shared__ unsigned int s_doc[IDX ? BA_CAP : 1];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int i = tid; i < BA_CAP; i += BA_WG) {
+        s_k0[i] = MRG_EMPTY_K0;
+        s_k1[i] = MRG_EMPTY_K1;
+        s_cnt[i] = 0;
+        if (IDX) s_doc[i] = MRG_EMPTY_DOC;
+    }
+    __syncthreads();
+    const uint32_t b = blockIdx.x;
+    constexpr uint32_t CH = MRG_CHUNK_RECS;
+    constexpr uint32_t RW = IDX ? 3u : 2u;
+    const uint32_t nch = min(A.bucket_next[b], A.cb);
+    const uint64_t total = (uint64_t)nch * CH;
+    const uint64_t *pool = A.pool + (uint64_t)b * A.cb * CH * RW;
+    const uint32_t *fill = A.chunk_fill + (uint64_t)b * A.cb;
+    // tail chunks
+    for (uint64_t base = 0; base < total; base += BA_WG) {
+        const uint64_t i = base + tid;
+        bool valid = false;
+        uint64_t a = 0, c = 0;
+        uint32_t d = MRG_EMPTY_DOC;
+        if (i < total) {
+            const uint32_t ch = (uint32_t)(i / CH), off = (uint32_t)(i % CH);
+            if (off < fill[ch]) {
+                valid = true;
+                const uint64_t *r = pool + i * RW;
+                a = r[0];
+                c = r[1];
+                if (IDX) d = (uint32_t)r[2];
+            }
+        }
+        bool ovf = false;
+        if (valid) {
+            uint64_t h = mrg_key_mix(a, c, d);
+            if (A.hash_bits) h &= (1ull << A.hash_bits) - 1u;
+            ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, 1ull, h);
+        }
+        const uint64_t j = mrg_wave_append(&A.counters[CNT_OVF2], ovf);
+        if (ovf && j < A.ocap) {
+            A.ok0[j] = a; A.ok1[j] = c; A.ocnt[j] = 1u;
+            if (IDX) A.odoc[j] = d;
+        }
+    }
+    // flushed LDS tables of the map workgroups: this bucket's slice of every region
+    for (uint32_t r = wv; r < A.nreg; r += BA_WG / 64) {
+        const uint32_t *fo = A.foff + (uint64_t)r * (MRG_NBUCKET + 1);
+        const uint32_t lo = fo[b], hi = fo[b + 1];
+        const uint64_t reg = (uint64_t)r * A.regcap;
+        for (uint32_t base = lo; base < hi; base += 64) {
+            const uint32_t k = base + lane;
+            bool ovf = false;
+            uint64_t a = 0, c = 0;
+            uint32_t d = MRG_EMPTY_DOC, n = 0;
+            if (k < hi) {
+                a = A.fk0[reg + k];
+                c = A.fk1[reg + k];
+                n = A.fcnt[reg + k];
+                if (IDX) d = A.fdoc[reg + k];
+                uint64_t h = mrg_key_mix(a, c, d);
+                if (A.hash_bits) h &= (1ull << A.hash_bits) - 1u;
+                ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, n, h);
+            }
+            const uint64_t j = mrg_wave_append(&A.counters[CNT_OVF2], ovf);
+            if (ovf && j < A.ocap) {
+                A.ok0[j] = a; A.ok1[j] = c; A.ocnt[j] = n;
+                if (IDX) A.odoc[j] = d;
+            }
+        }
+    }
+    __syncthreads();
+    for (int i0 = 0; i0 < BA_CAP; i0 += BA_WG) {
+        const int i = i0 + tid;
+        const bool full = s_k0[i] != MRG_EMPTY_K0;
+        const uint64_t j = mrg_wave_append(&A.counters[CNT_KEYS], full);
+        if (full) {
+            const uint64_t a = s_k0[i], c = s_k1[i];
+            A.out.k0[j] = a;
+            A.out.k1[j] = c;
+            A.out.cnt[j] = s_cnt[i];
+            A.out.doc[j] = IDX ? s_doc[i] : MRG_EMPTY_DOC;
+            A.out.len[j] = mrg_short_len(a, c);
+            A.out.hoff[j] = MRG_NO_HEAP;
+        }
+    }
+}
+
 __global__ void k_table_clear(TableArgs T, bool idx) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= T.cap) return;
@@ -210,6 +338,11 @@ __global__ void k_iota(uint32_t *p, uint64_t n) {
 }
 
 }  // namespace
+
+void mrg_launch_bucket_agg(const BucketArgs &a, bool indexer, hipStream_t s) {
+    if (indexer) hipLaunchKernelGGL(k_bucket_agg<true>, dim3(MRG_NBUCKET), dim3(BA_WG), 0, s, a);
+    else hipLaunchKernelGGL(k_bucket_agg<false>, dim3(MRG_NBUCKET), dim3(BA_WG), 0, s, a);
+}
 
 void mrg_launch_table_clear(const TableArgs &t, bool indexer, hipStream_t s) {
     hipLaunchKernelGGL(k_table_clear, grid_for(t.cap), dim3(256), 0, s, t, indexer);

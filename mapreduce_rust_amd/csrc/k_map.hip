@@ -62,9 +62,7 @@ struct LdsTable {
     unsigned long long *k0, *k1;
     unsigned int *cnt, *doc;
 
-    __device__ __forceinline__ bool insert(uint64_t a, uint64_t b, uint32_t d, uint32_t hash_bits) {
-        uint64_t h = mrg_key_mix(a, b, d);
-        if (hash_bits) h &= (1ull << hash_bits) - 1u;
+    __device__ __forceinline__ bool insert(uint64_t a, uint64_t b, uint32_t d, uint64_t h) {
         uint32_t slot = (uint32_t)(h ^ (h >> 29)) & (CAP - 1);
         for (int p = 0; p < MAX_PROBE; ++p) {
             const unsigned long long x = atomicCAS(&k0[slot], MRG_EMPTY_K0, (unsigned long long)a);
@@ -120,21 +118,65 @@ __device__ __forceinline__ bool walk_token(const RD &rd, uint64_t a, uint64_t do
     return true;
 }
 
+__device__ __forceinline__ uint64_t key_hash(uint64_t k0, uint64_t k1, uint32_t d, uint32_t hash_bits) {
+    uint64_t h = mrg_key_mix(k0, k1, d);
+    if (hash_bits) h &= (1ull << hash_bits) - 1u;
+    return h;
+}
+__device__ __forceinline__ uint32_t bucket_of(uint64_t h) { return (uint32_t)(h >> (64 - MRG_NBUCKET_LOG2)); }
+
+__device__ __forceinline__ uint32_t lds_ld(uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // One round of token emission by a whole wave (all 64 lanes must call it): LDS-table insert of short
-// keys, HBM records for misses and for long keys.
+// keys; misses are appended to their hash bucket through this wave's private chunk cursors
+// (wchunk/wfill, in LDS): one HBM atomic per MRG_CHUNK_RECS records, never per round.
 template <int CAP, bool IDX>
-__device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> &table, bool have, uint64_t tk0,
-                                           uint64_t tk1, uint32_t tlen, uint64_t tstart, uint32_t traw,
-                                           uint32_t docid) {
+__device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> &table, uint32_t *wchunk,
+                                           uint32_t *wfill, bool have, uint64_t tk0, uint64_t tk1, uint32_t tlen,
+                                           uint64_t tstart, uint32_t traw, uint32_t docid, uint32_t &my_tail) {
     const bool is_long = have && tlen > 16u;
     bool tail = false;
-    if (have && !is_long) tail = !table.insert(tk0, tk1, IDX ? docid : MRG_EMPTY_DOC, A.hash_bits);
-    const uint64_t ri = mrg_wave_append(&A.counters[CNT_REC], tail);
-    if (tail && ri < A.rcap) {
-        A.rk0[ri] = tk0;
-        A.rk1[ri] = tk1;
-        A.rcnt[ri] = 1u;
-        if (IDX) A.rdoc[ri] = docid;
+    uint64_t h = 0;
+    const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
+    if (have && !is_long) {
+        h = key_hash(tk0, tk1, dkey, A.hash_bits);
+        tail = !table.insert(tk0, tk1, dkey, h);
+    }
+    if (__any(tail)) {
+        constexpr uint32_t CH = MRG_CHUNK_RECS;
+        const uint32_t b = bucket_of(h);
+        uint32_t slot = 0, c_old = MRG_NO_CHUNK;
+        if (tail) {
+            c_old = lds_ld(&wchunk[b]);
+            slot = atomicAdd(&wfill[b], 1u);
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (tail && slot == CH) {  // this lane found the chunk full: it opens the next one
+            const uint32_t fin = lds_ld(&wfill[b]);
+            if (c_old != MRG_NO_CHUNK && c_old < A.cb) A.chunk_fill[(uint64_t)b * A.cb + c_old] = CH;
+            const uint32_t nc = atomicAdd(&A.bucket_next[b], 1u);
+            lds_st(&wchunk[b], nc);
+            lds_st(&wfill[b], fin - CH);
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (tail) {
+            const uint32_t c = slot < CH ? c_old : lds_ld(&wchunk[b]);
+            const uint32_t off = slot < CH ? slot : slot - CH;
+            if (c < A.cb) {
+                uint64_t *dst = A.pool + (((uint64_t)b * A.cb + c) * CH + off) * (IDX ? 3u : 2u);
+                dst[0] = tk0;
+                dst[1] = tk1;
+                if (IDX) dst[2] = docid;
+            } else {
+                atomicAdd(&A.counters[CNT_OVF], 1ull);
+            }
+            ++my_tail;
+        }
     }
     const uint64_t li = mrg_wave_append(&A.counters[CNT_LONG], is_long);
     if (is_long && li < A.lcap) {
@@ -154,6 +196,10 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
     __shared__ unsigned long long s_k1[CAP];
     __shared__ unsigned int s_cnt[CAP];
     __shared__ unsigned int s_doc[IDX ? CAP : 1];
+    __shared__ uint32_t s_wchunk[WG / 64][MRG_NBUCKET];  // per-wave current chunk of each bucket
+    __shared__ uint32_t s_wfill[WG / 64][MRG_NBUCKET];   // records in it
+    __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
+    __shared__ uint16_t s_rank[CAP];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
@@ -163,6 +209,11 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
         s_cnt[i] = 0;
         if (IDX) s_doc[i] = MRG_EMPTY_DOC;
     }
+    for (int i = tid; i < (WG / 64) * MRG_NBUCKET; i += WG) {
+        (&s_wchunk[0][0])[i] = MRG_NO_CHUNK;
+        (&s_wfill[0][0])[i] = MRG_CHUNK_RECS;  // "full": the first record opens a chunk
+    }
+    uint32_t my_tail = 0;
     if (tid < 128) s_lut[tid] = (uint8_t)(mrg_uclass((uint32_t)tid) == MRG_CLS_W ? 1u
                                           : (mrg_uclass((uint32_t)tid) == MRG_CLS_S ? 2u : 0u));
     LdsTable<CAP, IDX> table{s_k0, s_k1, s_cnt, s_doc};
@@ -254,7 +305,7 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
                 }
                 if (!__any(have)) break;
                 my_tokens += have ? 1u : 0u;
-                emit_round(A, table, have, tk0, tk1, tlen, tstart, traw, docid);
+                emit_round(A, table, s_wchunk[wv], s_wfill[wv], have, tk0, tk1, tlen, tstart, traw, docid, my_tail);
             }
             continue;
         }
@@ -363,27 +414,64 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
                     }
                 }
                 my_tokens += have ? 1u : 0u;
-                emit_round(A, table, have, tk0, tk1, tlen, tstart, traw, docid);
+                emit_round(A, table, s_wchunk[wv], s_wfill[wv], have, tk0, tk1, tlen, tstart, traw, docid, my_tail);
             }
         }
     }
 
-    // ---- flush the LDS table as records
+    // ---- close this wave's open chunks
+    for (int b = lane; b < MRG_NBUCKET; b += 64) {
+        const uint32_t cch = s_wchunk[wv][b];
+        if (cch != MRG_NO_CHUNK && cch < A.cb) A.chunk_fill[(uint64_t)b * A.cb + cch] = s_wfill[wv][b];
+    }
+    // ---- flush the LDS table into this workgroup's region, sorted by bucket
     __syncthreads();
-    for (int i0 = 0; i0 < CAP; i0 += WG) {
-        const int i = i0 + tid;
-        const bool full = s_k0[i] != MRG_EMPTY_K0;
-        const uint64_t ri = mrg_wave_append(&A.counters[CNT_REC], full);
-        if (full && ri < A.rcap) {
-            A.rk0[ri] = s_k0[i];
-            A.rk1[ri] = s_k1[i];
-            A.rcnt[ri] = s_cnt[i];
-            if (IDX) A.rdoc[ri] = s_doc[i];
+    for (int b = tid; b <= MRG_NBUCKET; b += WG) s_hist[b] = 0;
+    __syncthreads();
+    for (int i = tid; i < CAP; i += WG) {
+        if (s_k0[i] == MRG_EMPTY_K0) continue;
+        const uint32_t b = bucket_of(key_hash(s_k0[i], s_k1[i], IDX ? s_doc[i] : MRG_EMPTY_DOC, A.hash_bits));
+        s_rank[i] = (uint16_t)atomicAdd(&s_hist[b], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the bucket histogram by one wave
+        uint32_t run = 0;
+        for (int b0 = 0; b0 < MRG_NBUCKET; b0 += 64) {
+            const uint32_t v = s_hist[b0 + lane];
+            uint32_t incl = v;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = __shfl_up(incl, o);
+                if (lane >= o) incl += u;
+            }
+            s_hist[b0 + lane] = run + incl - v;
+            run += __shfl(incl, 63);
         }
+        if (lane == 0) s_hist[MRG_NBUCKET] = run;
+    }
+    __syncthreads();
+    uint32_t *foff = A.foff + (uint64_t)blockIdx.x * (MRG_NBUCKET + 1);
+    for (int b = tid; b <= MRG_NBUCKET; b += WG) foff[b] = s_hist[b];
+    const uint64_t reg = (uint64_t)blockIdx.x * CAP;
+    for (int i = tid; i < CAP; i += WG) {
+        if (s_k0[i] == MRG_EMPTY_K0) continue;
+        const uint32_t d = IDX ? s_doc[i] : MRG_EMPTY_DOC;
+        const uint32_t b = bucket_of(key_hash(s_k0[i], s_k1[i], d, A.hash_bits));
+        const uint64_t pos = reg + s_hist[b] + s_rank[i];
+        A.fk0[pos] = s_k0[i];
+        A.fk1[pos] = s_k1[i];
+        A.fcnt[pos] = s_cnt[i];
+        if (IDX) A.fdoc[pos] = d;
     }
     uint64_t t = my_tokens;
-    for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off);
-    if (lane == 0) atomicAdd(&A.counters[CNT_TOKENS], (unsigned long long)t);
+    uint64_t tl = my_tail;
+    for (int off = 32; off > 0; off >>= 1) {
+        t += __shfl_down(t, off);
+        tl += __shfl_down(tl, off);
+    }
+    if (lane == 0) {
+        atomicAdd(&A.counters[CNT_TOKENS], (unsigned long long)t);
+        atomicAdd(&A.counters[CNT_REC], (unsigned long long)tl);
+    }
 }
 
 // Long tokens: filter the raw token bytes (drop X codepoints), fingerprint (FNV-1a-64 of the key
@@ -446,6 +534,8 @@ void mrg_launch_map(const MapArgs &a, int app, int grid, int lds_cap, hipStream_
     else if (lds_cap >= 2048) { if (idx) launch_map_t<2048, true>(a, grid, s); else launch_map_t<2048, false>(a, grid, s); }
     else { if (idx) launch_map_t<1024, true>(a, grid, s); else launch_map_t<1024, false>(a, grid, s); }
 }
+
+int mrg_map_cap(int lds_cap) { return lds_cap >= 4096 ? 4096 : (lds_cap >= 2048 ? 2048 : 1024); }
 
 // tiles of a document [lo, hi): on the 16-byte grid starting at lo & ~15
 uint64_t mrg_map_tiles(uint64_t lo, uint64_t hi) {

@@ -10,8 +10,25 @@
 #define MRG_MAP_HALO 256        // bytes after the tile staged in LDS (tokens crossing the tile end)
 #define MRG_MAP_BEHIND 16       // bytes before the tile staged in LDS (previous codepoint)
 
+// Tail records (LDS-table misses) are bucketed by key hash into MRG_NBUCKET buckets of chunks of
+// MRG_CHUNK_RECS records; one workgroup per bucket later sums them in LDS (k_keys.hip).
+#define MRG_NBUCKET_LOG2 9
+#define MRG_NBUCKET (1 << MRG_NBUCKET_LOG2)
+#define MRG_CHUNK_RECS 128
+#define MRG_NO_CHUNK 0xFFFFFFFFu
+#define MRG_BA_CAP 4096          // LDS table slots of the per-bucket aggregation kernel
+
 // counters[] slots written by the kernels
-enum { CNT_REC = 0, CNT_LONG = 1, CNT_TOKENS = 2, CNT_ERRPOS = 3, CNT_KEYS = 4, CNT_N = 8 };
+enum {
+    CNT_REC = 0,      // tail records written by the map kernel
+    CNT_LONG = 1,     // long-token records
+    CNT_TOKENS = 2,   // tokens
+    CNT_ERRPOS = 3,   // first invalid UTF-8 byte (atomicMin), ~0 if none
+    CNT_KEYS = 4,     // distinct keys appended to the KeySet
+    CNT_OVF = 5,      // tail records that found no chunk (pool too small: rerun)
+    CNT_OVF2 = 6,     // keys that did not fit their bucket's LDS table (exact overflow path)
+    CNT_N = 8
+};
 
 // Stream-ordered caching allocator interface (all work of a context runs on one stream, so a
 // buffer released after its last enqueued use can be handed out again immediately).
@@ -28,10 +45,15 @@ struct MapArgs {
     const uint32_t *doc_id;      // [n_docs] global document id
     uint32_t n_docs;
     uint64_t n_chunks;
-    // short-key records (LDS-combine misses and the final LDS flush)
-    uint64_t *rk0, *rk1;
-    uint32_t *rcnt, *rdoc;
-    uint64_t rcap;
+    // tail records (LDS-table misses, count 1): pool[((b * cb + chunk) * CHUNK + off) * RECW + w]
+    uint64_t *pool;
+    uint32_t cb;                 // chunks per bucket
+    uint32_t *bucket_next;       // [NBUCKET] chunks handed out per bucket
+    uint32_t *chunk_fill;        // [NBUCKET * cb] records in each chunk
+    // LDS-table flush: workgroup g writes its entries to [g * CAP, ...) sorted by bucket;
+    // foff[g * (NBUCKET + 1) + b] = start of bucket b in that region
+    uint64_t *fk0, *fk1;
+    uint32_t *fcnt, *fdoc, *foff;
     // long-key token records (> 16 key bytes)
     uint64_t *lstart;
     uint32_t *llen, *ldoc;
@@ -73,6 +95,7 @@ struct LongItems {
 // ---- k_map.hip
 void mrg_launch_map(const MapArgs &a, int app, int grid, int lds_cap, hipStream_t s);
 uint64_t mrg_map_tiles(uint64_t doc_lo, uint64_t doc_hi);  // 4 KiB tiles of a document (16-B grid)
+int mrg_map_cap(int lds_cap);  // LDS-table entries per map workgroup actually used for lds_cap
 int mrg_map_max_grid(int app, int lds_cap, int device);
 void mrg_launch_long_prep(const uint8_t *base, const uint64_t *start, const uint32_t *rawlen, uint64_t n,
                           uint64_t *k0, uint64_t *k1, uint32_t *flen, uint64_t *flen64, uint64_t *fp,
@@ -81,6 +104,22 @@ void mrg_launch_long_gather(const uint8_t *base, const uint64_t *start, const ui
                             const uint64_t *dst_off, uint8_t *heap, hipStream_t s);
 
 // ---- k_keys.hip
+struct BucketArgs {
+    const uint64_t *pool;
+    uint32_t cb;
+    const uint32_t *bucket_next, *chunk_fill;
+    const uint64_t *fk0, *fk1;
+    const uint32_t *fcnt, *fdoc, *foff;
+    uint32_t nreg, regcap;       // map workgroups (flush regions) and entries per region
+    // keys that do not fit a bucket's LDS table (exact overflow, aggregated in the HBM table)
+    uint64_t *ok0, *ok1;
+    uint32_t *ocnt, *odoc;
+    uint64_t ocap;
+    KeySet out;
+    unsigned long long *counters;
+    uint32_t hash_bits;
+};
+void mrg_launch_bucket_agg(const BucketArgs &a, bool indexer, hipStream_t s);
 void mrg_launch_table_clear(const TableArgs &t, bool indexer, hipStream_t s);
 void mrg_launch_table_insert(const TableArgs &t, const uint64_t *k0, const uint64_t *k1, const uint32_t *cnt32,
                              const uint32_t *doc, uint64_t n, bool indexer, hipStream_t s);

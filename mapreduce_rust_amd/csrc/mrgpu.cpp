@@ -140,7 +140,7 @@ struct mrg_ctx {
     hipEvent_t ev[8] = {};
     int lds_cap = 2048;
     int map_grid = 0;
-    uint64_t rec_hint = 0, long_hint = 0;
+    uint64_t tail_hint = 0, long_hint = 0, ovf_hint = 0;
     // job
     bool job = false;
     int app = 0;
@@ -225,14 +225,12 @@ struct ShortSrc {
     uint64_t n = 0;
 };
 
-// Aggregate short-key records and long items into c->keys (distinct keys, counts, partitions).
-void aggregate(mrg_ctx *c, const ShortSrc &src, LongItems li) {
+// Sum short-key records in the HBM table (exact; device-scope CAS) and append the distinct keys to
+// c->keys (counter CNT_KEYS, which the caller has initialised).
+void table_aggregate(mrg_ctx *c, const ShortSrc &src) {
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     const bool idx = is_idx(c);
-    keys_reserve(c, src.n + li.n + 1);
-    HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, sizeof(unsigned long long), s));
-
     if (src.n) {
         TableArgs T{};
         T.cap = pow2_at_least(2 * src.n);
@@ -247,7 +245,13 @@ void aggregate(mrg_ctx *c, const ShortSrc &src, LongItems li) {
         mrg_launch_table_compact(T, idx, c->keys.ks, &c->d_cnt[CNT_KEYS], s);
         p.put(T.tk0); p.put(T.tk1); p.put(T.tcnt); p.put(T.tdoc);
     }
+}
 
+// Long keys: fingerprint sort + full-byte tie-break grouping; appends to c->keys and owns the heap.
+void long_aggregate(mrg_ctx *c, LongItems li) {
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const bool idx = is_idx(c);
     if (li.n) {
         const uint64_t n = li.n;
         uint64_t *k0 = pget<uint64_t>(p, n), *k1 = pget<uint64_t>(p, n), *fp = pget<uint64_t>(p, n);
@@ -279,10 +283,81 @@ void aggregate(mrg_ctx *c, const ShortSrc &src, LongItems li) {
         p.put(fl); p.put(ix); p.put(rep); p.put(scantmp); p.put(fps); p.put(kv); p.put(stmp);
         c->keys.any_long = true;
     }
+}
+
+// Distinct-key count + partition of every key (worker.rs:129).
+void finish_keys(mrg_ctx *c) {
     read_counters(c);
     c->keys.n = c->h_cnt[CNT_KEYS];
-    mrg_launch_partition(c->keys.ks, c->keys.heap, c->keys.n, c->R, s);
+    if (c->keys.n > c->keys.cap) raise(MRG_EINVAL, "internal: key set overflow");
+    mrg_launch_partition(c->keys.ks, c->keys.heap, c->keys.n, c->R, c->stream);
     c->st.distinct_keys = c->keys.n;
+}
+
+// Records that arrive as exchange records (shuffle import / plugin reduce): table + long path.
+void aggregate(mrg_ctx *c, const ShortSrc &src, LongItems li) {
+    keys_reserve(c, src.n + li.n + 1);
+    HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, sizeof(unsigned long long), c->stream));
+    table_aggregate(c, src);
+    long_aggregate(c, li);
+    finish_keys(c);
+}
+
+struct MapBufs {
+    uint64_t *pool = nullptr;
+    uint32_t *bucket_next = nullptr, *chunk_fill = nullptr;
+    uint64_t *fk0 = nullptr, *fk1 = nullptr;
+    uint32_t *fcnt = nullptr, *fdoc = nullptr, *foff = nullptr;
+    uint64_t *lstart = nullptr;
+    uint32_t *llen = nullptr, *ldoc = nullptr;
+    void release(Pool &p) {
+        p.put(pool); p.put(bucket_next); p.put(chunk_fill);
+        p.put(fk0); p.put(fk1); p.put(fcnt); p.put(fdoc); p.put(foff);
+        p.put(lstart); p.put(llen); p.put(ldoc);
+        *this = MapBufs{};
+    }
+};
+
+// Map-side records: per-bucket LDS aggregation of tail chunks + flushed map tables, exact overflow
+// through the HBM table, then the long keys.
+void bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap, LongItems li) {
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const bool idx = is_idx(c);
+    uint64_t ocap = std::max<uint64_t>(c->ovf_hint, 1u << 20);
+    for (;;) {
+        keys_reserve(c, (uint64_t)MRG_NBUCKET * MRG_BA_CAP + ocap + li.n + 1);
+        BucketArgs B{};
+        B.pool = A.pool; B.cb = A.cb; B.bucket_next = A.bucket_next; B.chunk_fill = A.chunk_fill;
+        B.fk0 = A.fk0; B.fk1 = A.fk1; B.fcnt = A.fcnt; B.fdoc = A.fdoc; B.foff = A.foff;
+        B.nreg = nreg; B.regcap = regcap;
+        B.ok0 = pget<uint64_t>(p, ocap); B.ok1 = pget<uint64_t>(p, ocap);
+        B.ocnt = pget<uint32_t>(p, ocap); B.odoc = idx ? pget<uint32_t>(p, ocap) : nullptr;
+        B.ocap = ocap;
+        B.out = c->keys.ks;
+        B.counters = c->d_cnt;
+        B.hash_bits = hash_bits(c);
+        HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
+        HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
+        mrg_launch_bucket_agg(B, idx, s);
+        read_counters(c);
+        const uint64_t novf = c->h_cnt[CNT_OVF2];
+        if (novf > ocap) {  // overflow list too small: grow (remembered) and run again
+            p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
+            ocap = c->ovf_hint = novf + novf / 8 + 1024;
+            continue;
+        }
+        if (novf) {
+            ShortSrc src;
+            src.k0 = B.ok0; src.k1 = B.ok1; src.cnt = B.ocnt; src.doc = B.odoc; src.n = novf;
+            table_aggregate(c, src);
+        }
+        p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
+        c->st.overflow_keys = novf;
+        break;
+    }
+    long_aggregate(c, li);
+    finish_keys(c);
 }
 
 void need_job(mrg_ctx *c) {
@@ -330,42 +405,54 @@ void job_map(mrg_ctx *c) {
 
     if (!c->map_grid) c->map_grid = mrg_map_max_grid(c->app, c->lds_cap, c->device);
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->map_grid, n_chunks));
-    uint64_t rcap = std::max<uint64_t>(c->rec_hint, total / 32 + (uint64_t)grid * c->lds_cap + 4096);
+    const uint32_t cap = (uint32_t)mrg_map_cap(c->lds_cap);
+    const bool idx = is_idx(c);
+    const uint32_t RW = idx ? 3u : 2u;
+    uint64_t tail_est = std::max<uint64_t>(c->tail_hint, total / 20 + 4096);
     uint64_t lcap = std::max<uint64_t>(c->long_hint, total / 1024 + 1024);
     MapArgs A{};
+    MapBufs M;
     uint32_t launches = 0;
     for (;;) {
+        // chunks per bucket: the expected tail + one open chunk per map wave
+        const uint64_t cbk = tail_est / ((uint64_t)MRG_NBUCKET * MRG_CHUNK_RECS) + (uint64_t)grid * (MRG_MAP_WG / 64) + 4;
+        if (cbk > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
         A.in = c->d_in;
         A.doc_off = d_doc_off;
         A.chunk_base = d_cb;
         A.doc_id = d_ids;
         A.n_docs = nd;
         A.n_chunks = n_chunks;
-        A.rk0 = pget<uint64_t>(p, rcap);
-        A.rk1 = pget<uint64_t>(p, rcap);
-        A.rcnt = pget<uint32_t>(p, rcap);
-        A.rdoc = is_idx(c) ? pget<uint32_t>(p, rcap) : nullptr;
-        A.rcap = rcap;
-        A.lstart = pget<uint64_t>(p, lcap);
-        A.llen = pget<uint32_t>(p, lcap);
-        A.ldoc = pget<uint32_t>(p, lcap);
-        A.lcap = lcap;
+        M.pool = pget<uint64_t>(p, (uint64_t)MRG_NBUCKET * cbk * MRG_CHUNK_RECS * RW);
+        M.bucket_next = pget<uint32_t>(p, MRG_NBUCKET);
+        M.chunk_fill = pget<uint32_t>(p, (uint64_t)MRG_NBUCKET * cbk);
+        M.fk0 = pget<uint64_t>(p, (uint64_t)grid * cap);
+        M.fk1 = pget<uint64_t>(p, (uint64_t)grid * cap);
+        M.fcnt = pget<uint32_t>(p, (uint64_t)grid * cap);
+        M.fdoc = idx ? pget<uint32_t>(p, (uint64_t)grid * cap) : nullptr;
+        M.foff = pget<uint32_t>(p, (uint64_t)grid * (MRG_NBUCKET + 1));
+        M.lstart = pget<uint64_t>(p, lcap);
+        M.llen = pget<uint32_t>(p, lcap);
+        M.ldoc = pget<uint32_t>(p, lcap);
+        A.pool = M.pool; A.cb = (uint32_t)cbk; A.bucket_next = M.bucket_next; A.chunk_fill = M.chunk_fill;
+        A.fk0 = M.fk0; A.fk1 = M.fk1; A.fcnt = M.fcnt; A.fdoc = M.fdoc; A.foff = M.foff;
+        A.lstart = M.lstart; A.llen = M.llen; A.ldoc = M.ldoc; A.lcap = lcap;
         A.counters = c->d_cnt;
         A.hash_bits = hash_bits(c);
         HIPCHK(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long) * CNT_N, s));
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_ERRPOS], 0xFF, sizeof(unsigned long long), s));
+        HIPCHK(hipMemsetAsync(M.bucket_next, 0, 4ull * MRG_NBUCKET, s));
         ev_rec(c, 0);
         if (n_chunks) mrg_launch_map(A, c->app, grid, c->lds_cap, s);
         ev_rec(c, 1);
         HIPCHK(hipGetLastError());
         ++launches;
         read_counters(c);
-        const uint64_t nr = c->h_cnt[CNT_REC], nl = c->h_cnt[CNT_LONG];
-        if (nr <= rcap && nl <= lcap) break;
+        const uint64_t nt = c->h_cnt[CNT_REC], nl = c->h_cnt[CNT_LONG];
+        if (c->h_cnt[CNT_OVF] == 0 && nl <= lcap) break;
         // capacity exceeded: grow (remembered for later jobs) and run the map again
-        p.put(A.rk0); p.put(A.rk1); p.put(A.rcnt); p.put(A.rdoc);
-        p.put(A.lstart); p.put(A.llen); p.put(A.ldoc);
-        if (nr > rcap) rcap = c->rec_hint = nr + nr / 8 + 4096;
+        M.release(p);
+        if (c->h_cnt[CNT_OVF]) tail_est = c->tail_hint = nt + nt / 4 + 4096;
         if (nl > lcap) lcap = c->long_hint = nl + nl / 8 + 1024;
     }
     c->st.ms_map = ev_ms(c, 0, 1);
@@ -376,8 +463,7 @@ void job_map(mrg_ctx *c) {
     c->st.map_records = c->h_cnt[CNT_REC];
     const uint64_t errpos = c->h_cnt[CNT_ERRPOS];
     auto release_map = [&]() {
-        p.put(A.rk0); p.put(A.rk1); p.put(A.rcnt); p.put(A.rdoc);
-        p.put(A.lstart); p.put(A.llen); p.put(A.ldoc);
+        M.release(p);
         p.put(d_doc_off); p.put(d_cb); p.put(d_ids);
     };
     if (errpos != ~0ull) {
@@ -388,12 +474,10 @@ void job_map(mrg_ctx *c) {
               (unsigned long long)(errpos - c->doc_off[d]));
     }
     ev_rec(c, 2);
-    ShortSrc src;
-    src.k0 = A.rk0; src.k1 = A.rk1; src.cnt = A.rcnt; src.doc = A.rdoc; src.n = c->h_cnt[CNT_REC];
     LongItems li{};
-    li.base = c->d_in; li.start = A.lstart; li.rawlen = A.llen; li.doc = A.ldoc; li.cnt = nullptr;
+    li.base = c->d_in; li.start = M.lstart; li.rawlen = M.llen; li.doc = M.ldoc; li.cnt = nullptr;
     li.n = c->h_cnt[CNT_LONG];
-    aggregate(c, src, li);
+    bucket_aggregate(c, A, (uint32_t)grid, cap, li);
     ev_rec(c, 3);
     release_map();
     c->st.ms_aggregate = ev_ms(c, 2, 3);

@@ -37,7 +37,8 @@ class Stats(C.Structure):
     _fields_ = [("input_bytes", C.c_uint64), ("tokens", C.c_uint64), ("long_tokens", C.c_uint64),
                 ("map_records", C.c_uint64), ("distinct_keys", C.c_uint64), ("output_bytes", C.c_uint64),
                 ("ms_map", C.c_double), ("ms_aggregate", C.c_double), ("ms_sort", C.c_double),
-                ("ms_format", C.c_double), ("map_launches", C.c_uint32), ("reserved", C.c_uint32)]
+                ("ms_format", C.c_double), ("map_launches", C.c_uint32), ("reserved", C.c_uint32),
+                ("overflow_keys", C.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
