@@ -67,10 +67,10 @@ __global__ __launch_bounds__(BA_WG) void k_bucket_agg(BucketArgs A) {
     const uint32_t b = blockIdx.x;
     constexpr uint32_t CH = MRG_CHUNK_RECS;
     constexpr uint32_t RW = IDX ? 3u : 2u;
-    const uint32_t nch = min(A.bucket_next[b], A.cb);
-    const uint64_t total = (uint64_t)nch * CH;
-    const uint64_t *pool = A.pool + (uint64_t)b * A.cb * CH * RW;
-    const uint32_t *fill = A.chunk_fill + (uint64_t)b * A.cb;
+    const uint64_t nch = min((uint64_t)A.bucket_next[b], A.cbase[b + 1] - A.cbase[b]);
+    const uint64_t total = nch * CH;
+    const uint64_t *pool = A.pool + A.cbase[b] * CH * RW;
+    const uint32_t *fill = A.chunk_fill + A.cbase[b];
     // tail chunks
     for (uint64_t base = 0; base < total; base += BA_WG) {
         const uint64_t i = base + tid;

@@ -158,7 +158,7 @@ __device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> 
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         if (tail && slot == CH) {  // this lane found the chunk full: it opens the next one
             const uint32_t fin = lds_ld(&wfill[b]);
-            if (c_old != MRG_NO_CHUNK && c_old < A.cb) A.chunk_fill[(uint64_t)b * A.cb + c_old] = CH;
+            if (c_old != MRG_NO_CHUNK && c_old < A.cbase[b + 1] - A.cbase[b]) A.chunk_fill[A.cbase[b] + c_old] = CH;
             const uint32_t nc = atomicAdd(&A.bucket_next[b], 1u);
             lds_st(&wchunk[b], nc);
             lds_st(&wfill[b], fin - CH);
@@ -167,8 +167,8 @@ __device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> 
         if (tail) {
             const uint32_t c = slot < CH ? c_old : lds_ld(&wchunk[b]);
             const uint32_t off = slot < CH ? slot : slot - CH;
-            if (c < A.cb) {
-                uint64_t *dst = A.pool + (((uint64_t)b * A.cb + c) * CH + off) * (IDX ? 3u : 2u);
+            if (c < A.cbase[b + 1] - A.cbase[b]) {
+                uint64_t *dst = A.pool + ((A.cbase[b] + c) * CH + off) * (IDX ? 3u : 2u);
                 dst[0] = tk0;
                 dst[1] = tk1;
                 if (IDX) dst[2] = docid;
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
     // ---- close this wave's open chunks
     for (int b = lane; b < MRG_NBUCKET; b += 64) {
         const uint32_t cch = s_wchunk[wv][b];
-        if (cch != MRG_NO_CHUNK && cch < A.cb) A.chunk_fill[(uint64_t)b * A.cb + cch] = s_wfill[wv][b];
+        if (cch != MRG_NO_CHUNK && cch < A.cbase[b + 1] - A.cbase[b]) A.chunk_fill[A.cbase[b] + cch] = s_wfill[wv][b];
     }
     // ---- flush the LDS table into this workgroup's region, sorted by bucket
     __syncthreads();

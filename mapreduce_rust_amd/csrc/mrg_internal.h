@@ -45,11 +45,12 @@ struct MapArgs {
     const uint32_t *doc_id;      // [n_docs] global document id
     uint32_t n_docs;
     uint64_t n_chunks;
-    // tail records (LDS-table misses, count 1): pool[((b * cb + chunk) * CHUNK + off) * RECW + w]
+    // tail records (LDS-table misses, count 1): bucket b owns chunks [cbase[b], cbase[b+1]) of the
+    // pool; record = pool[((cbase[b] + chunk) * CHUNK + off) * RECW + w]
     uint64_t *pool;
-    uint32_t cb;                 // chunks per bucket
-    uint32_t *bucket_next;       // [NBUCKET] chunks handed out per bucket
-    uint32_t *chunk_fill;        // [NBUCKET * cb] records in each chunk
+    const uint64_t *cbase;       // [NBUCKET + 1] first chunk of each bucket
+    uint32_t *bucket_next;       // [NBUCKET] chunks handed out per bucket (may exceed capacity)
+    uint32_t *chunk_fill;        // [cbase[NBUCKET]] records in each chunk
     // LDS-table flush: workgroup g writes its entries to [g * CAP, ...) sorted by bucket;
     // foff[g * (NBUCKET + 1) + b] = start of bucket b in that region
     uint64_t *fk0, *fk1;
@@ -106,7 +107,7 @@ void mrg_launch_long_gather(const uint8_t *base, const uint64_t *start, const ui
 // ---- k_keys.hip
 struct BucketArgs {
     const uint64_t *pool;
-    uint32_t cb;
+    const uint64_t *cbase;
     const uint32_t *bucket_next, *chunk_fill;
     const uint64_t *fk0, *fk1;
     const uint32_t *fcnt, *fdoc, *foff;

@@ -140,7 +140,8 @@ struct mrg_ctx {
     hipEvent_t ev[8] = {};
     int lds_cap = 2048;
     int map_grid = 0;
-    uint64_t tail_hint = 0, long_hint = 0, ovf_hint = 0;
+    uint64_t long_hint = 0, ovf_hint = 0;
+    std::vector<uint64_t> bcap_hint;  // chunks per tail bucket
     // job
     bool job = false;
     int app = 0;
@@ -304,14 +305,14 @@ void aggregate(mrg_ctx *c, const ShortSrc &src, LongItems li) {
 }
 
 struct MapBufs {
-    uint64_t *pool = nullptr;
+    uint64_t *pool = nullptr, *cbase = nullptr;
     uint32_t *bucket_next = nullptr, *chunk_fill = nullptr;
     uint64_t *fk0 = nullptr, *fk1 = nullptr;
     uint32_t *fcnt = nullptr, *fdoc = nullptr, *foff = nullptr;
     uint64_t *lstart = nullptr;
     uint32_t *llen = nullptr, *ldoc = nullptr;
     void release(Pool &p) {
-        p.put(pool); p.put(bucket_next); p.put(chunk_fill);
+        p.put(pool); p.put(cbase); p.put(bucket_next); p.put(chunk_fill);
         p.put(fk0); p.put(fk1); p.put(fcnt); p.put(fdoc); p.put(foff);
         p.put(lstart); p.put(llen); p.put(ldoc);
         *this = MapBufs{};
@@ -328,7 +329,7 @@ void bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
     for (;;) {
         keys_reserve(c, (uint64_t)MRG_NBUCKET * MRG_BA_CAP + ocap + li.n + 1);
         BucketArgs B{};
-        B.pool = A.pool; B.cb = A.cb; B.bucket_next = A.bucket_next; B.chunk_fill = A.chunk_fill;
+        B.pool = A.pool; B.cbase = A.cbase; B.bucket_next = A.bucket_next; B.chunk_fill = A.chunk_fill;
         B.fk0 = A.fk0; B.fk1 = A.fk1; B.fcnt = A.fcnt; B.fdoc = A.fdoc; B.foff = A.foff;
         B.nreg = nreg; B.regcap = regcap;
         B.ok0 = pget<uint64_t>(p, ocap); B.ok1 = pget<uint64_t>(p, ocap);
@@ -342,6 +343,9 @@ void bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         mrg_launch_bucket_agg(B, idx, s);
         read_counters(c);
         const uint64_t novf = c->h_cnt[CNT_OVF2];
+        if (getenv("MRG_DEBUG"))
+            fprintf(stderr, "[mrgpu] bucket agg: %llu keys, %llu overflow records (cap %llu)\n",
+                    (unsigned long long)c->h_cnt[CNT_KEYS], (unsigned long long)novf, (unsigned long long)ocap);
         if (novf > ocap) {  // overflow list too small: grow (remembered) and run again
             p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
             ocap = c->ovf_hint = novf + novf / 8 + 1024;
@@ -408,24 +412,34 @@ void job_map(mrg_ctx *c) {
     const uint32_t cap = (uint32_t)mrg_map_cap(c->lds_cap);
     const bool idx = is_idx(c);
     const uint32_t RW = idx ? 3u : 2u;
-    uint64_t tail_est = std::max<uint64_t>(c->tail_hint, total / 20 + 4096);
+    const uint64_t tail_est = total / 20 + 4096;
     uint64_t lcap = std::max<uint64_t>(c->long_hint, total / 1024 + 1024);
+    // chunks per bucket: the expected tail + one open chunk per map wave (grown per bucket on demand)
+    const uint64_t waves = (uint64_t)grid * (MRG_MAP_WG / 64);
+    std::vector<uint64_t> bcap(MRG_NBUCKET, tail_est / ((uint64_t)MRG_NBUCKET * MRG_CHUNK_RECS) + waves + 4);
+    if (c->bcap_hint.size() == MRG_NBUCKET)
+        for (int b = 0; b < MRG_NBUCKET; ++b) bcap[b] = std::max(bcap[b], c->bcap_hint[b]);
     MapArgs A{};
     MapBufs M;
     uint32_t launches = 0;
     for (;;) {
-        // chunks per bucket: the expected tail + one open chunk per map wave
-        const uint64_t cbk = tail_est / ((uint64_t)MRG_NBUCKET * MRG_CHUNK_RECS) + (uint64_t)grid * (MRG_MAP_WG / 64) + 4;
-        if (cbk > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
+        std::vector<uint64_t> cbase(MRG_NBUCKET + 1, 0);
+        for (int b = 0; b < MRG_NBUCKET; ++b) {
+            if (bcap[b] > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
+            cbase[b + 1] = cbase[b] + bcap[b];
+        }
+        const uint64_t cbk = cbase[MRG_NBUCKET];
+        M.cbase = pget<uint64_t>(p, MRG_NBUCKET + 1);
+        HIPCHK(hipMemcpyAsync(M.cbase, cbase.data(), 8ull * (MRG_NBUCKET + 1), hipMemcpyHostToDevice, s));
         A.in = c->d_in;
         A.doc_off = d_doc_off;
         A.chunk_base = d_cb;
         A.doc_id = d_ids;
         A.n_docs = nd;
         A.n_chunks = n_chunks;
-        M.pool = pget<uint64_t>(p, (uint64_t)MRG_NBUCKET * cbk * MRG_CHUNK_RECS * RW);
+        M.pool = pget<uint64_t>(p, cbk * MRG_CHUNK_RECS * RW);
         M.bucket_next = pget<uint32_t>(p, MRG_NBUCKET);
-        M.chunk_fill = pget<uint32_t>(p, (uint64_t)MRG_NBUCKET * cbk);
+        M.chunk_fill = pget<uint32_t>(p, cbk);
         M.fk0 = pget<uint64_t>(p, (uint64_t)grid * cap);
         M.fk1 = pget<uint64_t>(p, (uint64_t)grid * cap);
         M.fcnt = pget<uint32_t>(p, (uint64_t)grid * cap);
@@ -434,7 +448,7 @@ void job_map(mrg_ctx *c) {
         M.lstart = pget<uint64_t>(p, lcap);
         M.llen = pget<uint32_t>(p, lcap);
         M.ldoc = pget<uint32_t>(p, lcap);
-        A.pool = M.pool; A.cb = (uint32_t)cbk; A.bucket_next = M.bucket_next; A.chunk_fill = M.chunk_fill;
+        A.pool = M.pool; A.cbase = M.cbase; A.bucket_next = M.bucket_next; A.chunk_fill = M.chunk_fill;
         A.fk0 = M.fk0; A.fk1 = M.fk1; A.fcnt = M.fcnt; A.fdoc = M.fdoc; A.foff = M.foff;
         A.lstart = M.lstart; A.llen = M.llen; A.ldoc = M.ldoc; A.lcap = lcap;
         A.counters = c->d_cnt;
@@ -448,13 +462,26 @@ void job_map(mrg_ctx *c) {
         HIPCHK(hipGetLastError());
         ++launches;
         read_counters(c);
-        const uint64_t nt = c->h_cnt[CNT_REC], nl = c->h_cnt[CNT_LONG];
+        const uint64_t nl = c->h_cnt[CNT_LONG];
         if (c->h_cnt[CNT_OVF] == 0 && nl <= lcap) break;
-        // capacity exceeded: grow (remembered for later jobs) and run the map again
-        M.release(p);
-        if (c->h_cnt[CNT_OVF]) tail_est = c->tail_hint = nt + nt / 4 + 4096;
+        // capacity exceeded: grow each bucket to its demand (remembered for later jobs), run again
+        if (c->h_cnt[CNT_OVF]) {
+            std::vector<uint32_t> next(MRG_NBUCKET);
+            HIPCHK(hipMemcpyAsync(next.data(), M.bucket_next, 4ull * MRG_NBUCKET, hipMemcpyDeviceToHost, s));
+            sync(c);
+            for (int b = 0; b < MRG_NBUCKET; ++b) bcap[b] = std::max<uint64_t>(bcap[b], next[b] + next[b] / 8 + 4);
+            c->bcap_hint = bcap;
+        }
         if (nl > lcap) lcap = c->long_hint = nl + nl / 8 + 1024;
+        if (getenv("MRG_DEBUG"))
+            fprintf(stderr, "[mrgpu] map rerun: tail overflow %llu, long %llu/%llu\n",
+                    (unsigned long long)c->h_cnt[CNT_OVF], (unsigned long long)nl, (unsigned long long)lcap);
+        M.release(p);
     }
+    if (getenv("MRG_DEBUG"))
+        fprintf(stderr, "[mrgpu] map: %llu tokens, %llu tail records, %llu long, %u launches, grid %d\n",
+                (unsigned long long)c->h_cnt[CNT_TOKENS], (unsigned long long)c->h_cnt[CNT_REC],
+                (unsigned long long)c->h_cnt[CNT_LONG], launches, grid);
     c->st.ms_map = ev_ms(c, 0, 1);
     c->st.map_launches = launches;
     c->st.input_bytes = total;
