@@ -457,7 +457,7 @@ void job_map(mrg_ctx *c) {
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_ERRPOS], 0xFF, sizeof(unsigned long long), s));
         HIPCHK(hipMemsetAsync(M.bucket_next, 0, 4ull * MRG_NBUCKET, s));
         ev_rec(c, 0);
-        if (n_chunks) mrg_launch_map(A, c->app, grid, c->lds_cap, s);
+        mrg_launch_map(A, c->app, grid, c->lds_cap, s);  // also with no tiles: writes empty flush regions
         ev_rec(c, 1);
         HIPCHK(hipGetLastError());
         ++launches;
