@@ -24,11 +24,18 @@ constexpr int BA_WG = 512;
 constexpr int BA_CAP = MRG_BA_CAP;
 constexpr int BA_PROBE = 64;
 
+// the map kernel's key hash (k_map.hip key_hash): bucket = top 9 bits
+__device__ __forceinline__ uint32_t ba_hash(uint64_t a, uint64_t b, uint32_t d, uint32_t hash_bits) {
+    uint32_t h = mrg_key_hash32(a, b, d);
+    if (hash_bits && hash_bits < 32) h &= (1u << hash_bits) - 1u;
+    return h;
+}
+
 template <bool IDX>
 __device__ __forceinline__ bool ba_insert(unsigned long long *k0, unsigned long long *k1, unsigned long long *cnt,
                                           unsigned int *doc, uint64_t a, uint64_t b, uint32_t d, uint64_t c,
-                                          uint64_t h) {
-    uint32_t slot = (uint32_t)(h >> 17) & (BA_CAP - 1);
+                                          uint32_t h) {
+    uint32_t slot = (h >> 11) & (BA_CAP - 1);  // bits disjoint from the bucket (top 9) and map-group bits
     for (int p = 0; p < BA_PROBE; ++p) {
         const unsigned long long x = atomicCAS(&k0[slot], MRG_EMPTY_K0, (unsigned long long)a);
         if (x == MRG_EMPTY_K0 || x == a) {
@@ -89,9 +96,7 @@ __global__ __launch_bounds__(BA_WG) void k_bucket_agg(BucketArgs A) {
         }
         bool ovf = false;
         if (valid) {
-            uint64_t h = mrg_key_mix(a, c, d);
-            if (A.hash_bits) h &= (1ull << A.hash_bits) - 1u;
-            ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, 1ull, h);
+            ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
         }
         const uint64_t j = mrg_wave_append(&A.counters[CNT_OVF2], ovf);
         if (ovf && j < A.ocap) {
@@ -114,9 +119,7 @@ __global__ __launch_bounds__(BA_WG) void k_bucket_agg(BucketArgs A) {
                 c = A.fk1[reg + k];
                 n = A.fcnt[reg + k];
                 if (IDX) d = A.fdoc[reg + k];
-                uint64_t h = mrg_key_mix(a, c, d);
-                if (A.hash_bits) h &= (1ull << A.hash_bits) - 1u;
-                ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, n, h);
+                ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, n, ba_hash(a, c, d, A.hash_bits));
             }
             const uint64_t j = mrg_wave_append(&A.counters[CNT_OVF2], ovf);
             if (ovf && j < A.ocap) {

@@ -7,22 +7,24 @@
 // (worker.rs:75): the first invalid byte offset is reported and the job fails with MRG_EUTF8.
 //
 // Layout: documents back to back in one HBM buffer; each document is cut into 4 KiB
-// tiles on a 16-byte-aligned grid; a persistent grid of 256-thread workgroups walks the tiles.  Per
-// tile the workgroup stages [tile - 16 B, tile + 4 KiB + 256 B) into LDS with 16-byte loads.
+// tiles on a 16-byte-aligned grid; a persistent grid of 256-thread workgroups walks the tiles, the
+// next tile's 16-byte loads in flight (registers) while the current one is processed from LDS.
 //
 // ASCII tiles (the common case; wave-uniform test) take the fast path:
 //   1. every lane classifies one 16-byte segment through a 128-entry LDS LUT into an interleaved
 //      32-bit mask (bit 2k = byte k is \w, bit 2k+1 = byte k is White_Space);
 //   2. token starts = non-space bytes after a space: mask arithmetic; each wave compacts its starts
 //      into an LDS queue (wave prefix sum) so that all 64 lanes then work on one token each;
-//   3. per token: end = next space bit, key = the \w bytes -- contiguous in > 98% of tokens
-//      (deleted X bytes only at the edges, e.g. "word,"), read as 3 x 8 B from LDS and packed
-//      big-endian into (k0, k1); anything else (interior deletions like "don't", > 16 B, tokens
-//      running past the halo) takes the exact per-codepoint walker.
+//   3. per token: end = next space bit, key = the \w bytes -- contiguous unless a deleted byte sits
+//      inside the token ("don't") -- read as 3 x 8 B from LDS and packed big-endian into (k0, k1);
+//      interior deletions, > 31-byte raw tokens and tokens running past the halo take the exact
+//      per-codepoint walker.
 // Non-ASCII tiles use the per-codepoint walker for every token (UTF-8 decode + class table).
-// Keys of <= 16 bytes are inserted into a workgroup-private LDS hash table (exact: the packed key IS
-// the identity, no fingerprint); misses become records in HBM.  Keys > 16 bytes become long-token
-// records (start, raw length, doc) resolved by the collision-safe fingerprint sort (k_keys.hip).
+// Keys of <= 16 bytes go to a workgroup-private LDS hash table (exact: the packed key IS the
+// identity) of 8-slot groups probed with one batched read; misses are appended to one of 512 hash
+// buckets in HBM through per-wave chunk cursors.  Keys > 16 bytes become long-token records
+// (start, raw length, doc) resolved by the collision-safe fingerprint sort (k_keys.hip).  At the end
+// the LDS table is flushed, sorted by bucket, into the workgroup's region.
 #include "mrg_device.h"
 #include "mrg_internal.h"
 
@@ -35,10 +37,11 @@ constexpr int HALO = MRG_MAP_HALO;
 constexpr int BEHIND = MRG_MAP_BEHIND;
 constexpr int NSEG = (TILE + HALO) / SEG;           // classified segments: tile + halo
 constexpr int LDS_BYTES = BEHIND + TILE + HALO + 32;
+constexpr int NVEC_MAX = (LDS_BYTES + 15) / 16;     // 16-byte vectors per staged window (<= 2 per thread)
 constexpr int QCAP = WG / 4 * SEG / 2;              // tokens per wave per tile <= 512
-constexpr int MAX_PROBE = 8;
 constexpr uint64_t SBITS = 0xAAAAAAAAAAAAAAAAull;    // odd bits: White_Space flags
 constexpr uint64_t WBITS = 0x5555555555555555ull;    // even bits: \w flags
+static_assert(NVEC_MAX <= 2 * WG, "two prefetch vectors per thread");
 
 // LDS-staged window: byte a lives at lds[a - wbase] when lo <= a < hi, else it is read from HBM.
 struct Window {
@@ -50,37 +53,82 @@ struct Window {
     }
 };
 
+struct TileInfo {
+    uint64_t At, t0, t1, doc_lo, doc_hi, wlo, whi;
+    uint32_t docid, v0, v1;
+};
+
+__device__ __forceinline__ TileInfo locate(const MapArgs &A, uint64_t c) {
+    uint32_t lo_d = 0, hi_d = A.n_docs;  // chunk_base[d] <= c < chunk_base[d+1]
+    while (hi_d - lo_d > 1) {
+        const uint32_t mid = (lo_d + hi_d) >> 1;
+        if (A.chunk_base[mid] <= c) lo_d = mid; else hi_d = mid;
+    }
+    TileInfo t;
+    t.doc_lo = A.doc_off[lo_d];
+    t.doc_hi = A.doc_off[lo_d + 1];
+    t.At = (t.doc_lo & ~15ull) + (c - A.chunk_base[lo_d]) * (uint64_t)TILE;  // aligned tile base
+    t.t0 = max(t.At, t.doc_lo);
+    t.t1 = min(t.At + (uint64_t)TILE, t.doc_hi);
+    t.docid = A.doc_id ? A.doc_id[lo_d] : lo_d;
+    const uint64_t wbase = t.At - (uint64_t)BEHIND;  // may wrap below 0: only differences are used
+    t.wlo = max(t.doc_lo, t.At >= (uint64_t)BEHIND ? t.At - BEHIND : 0ull);
+    t.whi = min(t.t1 + (uint64_t)HALO, t.doc_hi);
+    t.v0 = (uint32_t)(((t.wlo & ~15ull) - wbase) >> 4);
+    t.v1 = (uint32_t)((((t.whi + 15u) & ~15ull) - wbase) >> 4);
+    return t;
+}
+
 __device__ __forceinline__ void report_error(unsigned long long *counters, uint64_t pos) {
     atomicMin(&counters[CNT_ERRPOS], (unsigned long long)pos);
 }
 
-// Workgroup LDS table, open addressing with a monotone claim protocol: a slot goes
+__device__ __forceinline__ uint32_t key_hash(uint64_t k0, uint64_t k1, uint32_t d, uint32_t hash_bits) {
+    uint32_t h = mrg_key_hash32(k0, k1, d);
+    if (hash_bits && hash_bits < 32) h &= (1u << hash_bits) - 1u;
+    return h;
+}
+__device__ __forceinline__ uint32_t bucket_of(uint32_t h) { return h >> (32 - MRG_NBUCKET_LOG2); }
+
+// Workgroup LDS table of 8-slot groups with a monotone claim protocol: a slot goes
 // EMPTY -> k0 set -> k1 set (-> doc set) and never back; a key may complete a slot whose set words
-// equal its own.  Lanes racing on one slot agree on its owner; every key lives in one slot; no locks.
+// equal its own; claims scan the group in slot order.  So a key lives in the first slot of its group
+// that was empty or its own when claimed, lanes racing on one slot agree on its owner, no locks.
+// The common cases -- the key's slot fully set (hit), or a full group without it (miss) -- are
+// decided from one snapshot of the group (8 + 8 LDS reads issued together); only claims use CAS.
 template <int CAP, bool IDX>
 struct LdsTable {
+    static constexpr uint32_t NG = CAP / 8;
     unsigned long long *k0, *k1;
     unsigned int *cnt, *doc;
 
-    __device__ __forceinline__ bool insert(uint64_t a, uint64_t b, uint32_t d, uint64_t h) {
-        uint32_t slot = (uint32_t)(h ^ (h >> 29)) & (CAP - 1);
-        for (int p = 0; p < MAX_PROBE; ++p) {
-            const unsigned long long x = atomicCAS(&k0[slot], MRG_EMPTY_K0, (unsigned long long)a);
-            if (x == MRG_EMPTY_K0 || x == a) {
-                const unsigned long long y = atomicCAS(&k1[slot], MRG_EMPTY_K1, (unsigned long long)b);
-                if (y == MRG_EMPTY_K1 || y == b) {
-                    bool ok = true;
-                    if (IDX) {
-                        const unsigned int z = atomicCAS(&doc[slot], MRG_EMPTY_DOC, d);
-                        ok = (z == MRG_EMPTY_DOC || z == d);
-                    }
-                    if (ok) {
-                        atomicAdd(&cnt[slot], 1u);
-                        return true;
-                    }
-                }
+    __device__ __forceinline__ bool insert(uint64_t a, uint64_t b, uint32_t d, uint32_t h) {
+        const uint32_t g = (h & (NG - 1)) * 8u;
+        uint32_t hit = 0, open = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint64_t x = k0[g + j], y = k1[g + j];
+            const bool dm = !IDX || doc[g + j] == d;
+            hit |= (uint32_t)(x == a && y == b && dm) << j;
+            open |= (uint32_t)(x == MRG_EMPTY_K0 || (x == a && (y == MRG_EMPTY_K1 || (y == b && !dm)))) << j;
+        }
+        if (hit) {
+            atomicAdd(&cnt[g + (uint32_t)__builtin_ctz(hit)], 1u);
+            return true;
+        }
+        if (!open) return false;  // group full of other keys: miss
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t s = g + j;
+            const unsigned long long x = atomicCAS(&k0[s], MRG_EMPTY_K0, (unsigned long long)a);
+            if (x != MRG_EMPTY_K0 && x != a) continue;
+            const unsigned long long y = atomicCAS(&k1[s], MRG_EMPTY_K1, (unsigned long long)b);
+            if (y != MRG_EMPTY_K1 && y != b) continue;
+            if (IDX) {
+                const unsigned int z = atomicCAS(&doc[s], MRG_EMPTY_DOC, d);
+                if (z != MRG_EMPTY_DOC && z != d) continue;
             }
-            slot = (slot + 1u) & (CAP - 1);
+            atomicAdd(&cnt[s], 1u);
+            return true;
         }
         return false;
     }
@@ -90,8 +138,8 @@ struct LdsTable {
 // document start): decode codepoints until White_Space or the document end, keep \w bytes.
 // Returns false on invalid UTF-8 (reported).  *end = first byte after the token.
 template <class RD>
-__device__ __forceinline__ bool walk_token(const RD &rd, uint64_t a, uint64_t doc_hi, unsigned long long *counters,
-                                           uint64_t &k0, uint64_t &k1, uint32_t &L, uint64_t &end) {
+__device__ __noinline__ bool walk_token(const RD &rd, uint64_t a, uint64_t doc_hi, unsigned long long *counters,
+                                        uint64_t &k0, uint64_t &k1, uint32_t &L, uint64_t &end) {
     k0 = 0;
     k1 = 0;
     L = 0;
@@ -118,13 +166,6 @@ __device__ __forceinline__ bool walk_token(const RD &rd, uint64_t a, uint64_t do
     return true;
 }
 
-__device__ __forceinline__ uint64_t key_hash(uint64_t k0, uint64_t k1, uint32_t d, uint32_t hash_bits) {
-    uint64_t h = mrg_key_mix(k0, k1, d);
-    if (hash_bits) h &= (1ull << hash_bits) - 1u;
-    return h;
-}
-__device__ __forceinline__ uint32_t bucket_of(uint64_t h) { return (uint32_t)(h >> (64 - MRG_NBUCKET_LOG2)); }
-
 __device__ __forceinline__ uint32_t lds_ld(uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -141,7 +182,7 @@ __device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> 
                                            uint64_t tstart, uint32_t traw, uint32_t docid, uint32_t &my_tail) {
     const bool is_long = have && tlen > 16u;
     bool tail = false;
-    uint64_t h = 0;
+    uint32_t h = 0;
     const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
     if (have && !is_long) {
         h = key_hash(tk0, tk1, dkey, A.hash_bits);
@@ -158,7 +199,8 @@ __device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> 
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         if (tail && slot == CH) {  // this lane found the chunk full: it opens the next one
             const uint32_t fin = lds_ld(&wfill[b]);
-            if (c_old != MRG_NO_CHUNK && c_old < A.cbase[b + 1] - A.cbase[b]) A.chunk_fill[A.cbase[b] + c_old] = CH;
+            const uint64_t cap = A.cbase[b + 1] - A.cbase[b];
+            if (c_old != MRG_NO_CHUNK && c_old < cap) A.chunk_fill[A.cbase[b] + c_old] = CH;
             const uint32_t nc = atomicAdd(&A.bucket_next[b], 1u);
             lds_st(&wchunk[b], nc);
             lds_st(&wfill[b], fin - CH);
@@ -192,10 +234,10 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
     __shared__ uint32_t s_mask[NSEG + 2];
     __shared__ uint16_t s_queue[WG / 64][QCAP];
     __shared__ uint8_t s_lut[128];
-    __shared__ unsigned long long s_k0[CAP];
-    __shared__ unsigned long long s_k1[CAP];
+    __shared__ __attribute__((aligned(16))) unsigned long long s_k0[CAP];
+    __shared__ __attribute__((aligned(16))) unsigned long long s_k1[CAP];
     __shared__ unsigned int s_cnt[CAP];
-    __shared__ unsigned int s_doc[IDX ? CAP : 1];
+    __shared__ __attribute__((aligned(16))) unsigned int s_doc[IDX ? CAP : 1];
     __shared__ uint32_t s_wchunk[WG / 64][MRG_NBUCKET];  // per-wave current chunk of each bucket
     __shared__ uint32_t s_wfill[WG / 64][MRG_NBUCKET];   // records in it
     __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
@@ -213,44 +255,53 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
         (&s_wchunk[0][0])[i] = MRG_NO_CHUNK;
         (&s_wfill[0][0])[i] = MRG_CHUNK_RECS;  // "full": the first record opens a chunk
     }
-    uint32_t my_tail = 0;
     if (tid < 128) s_lut[tid] = (uint8_t)(mrg_uclass((uint32_t)tid) == MRG_CLS_W ? 1u
                                           : (mrg_uclass((uint32_t)tid) == MRG_CLS_S ? 2u : 0u));
     LdsTable<CAP, IDX> table{s_k0, s_k1, s_cnt, s_doc};
-    uint64_t my_tokens = 0;
+    uint32_t my_tokens = 0, my_tail = 0;
 
-    for (uint64_t c = blockIdx.x; c < A.n_chunks; c += gridDim.x) {
-        // ---- locate the tile (uniform across the workgroup)
-        uint32_t lo_d = 0, hi_d = A.n_docs;  // chunk_base[d] <= c < chunk_base[d+1]
-        while (hi_d - lo_d > 1) {
-            const uint32_t mid = (lo_d + hi_d) >> 1;
-            if (A.chunk_base[mid] <= c) lo_d = mid; else hi_d = mid;
-        }
-        const uint32_t d = lo_d;
-        const uint64_t doc_lo = A.doc_off[d], doc_hi = A.doc_off[d + 1];
-        const uint64_t At = (doc_lo & ~15ull) + (c - A.chunk_base[d]) * (uint64_t)TILE;  // aligned tile base
-        const uint64_t t0 = max(At, doc_lo);
-        const uint64_t t1 = min(At + (uint64_t)TILE, doc_hi);
-        const uint32_t docid = A.doc_id ? A.doc_id[d] : d;
+    // prefetch of the first tile
+    uint64_t c = blockIdx.x;
+    TileInfo nx{};
+    uint4 pf0 = {0, 0, 0, 0}, pf1 = {0, 0, 0, 0};
+    if (c < A.n_chunks) {
+        nx = locate(A, c);
+        const uint4 *src = reinterpret_cast<const uint4 *>(A.in + (nx.At - (uint64_t)BEHIND));
+        if (nx.v0 + tid < nx.v1) pf0 = src[nx.v0 + tid];
+        if (nx.v0 + tid + WG < nx.v1) pf1 = src[nx.v0 + tid + WG];
+    }
 
+    for (; c < A.n_chunks; c += gridDim.x) {
+        const TileInfo T = nx;
         Window W;
         W.lds = s_tile;
         W.g = A.in;
-        W.wbase = At - (uint64_t)BEHIND;                 // may wrap below 0: only differences are used
-        W.lo = max(doc_lo, At >= (uint64_t)BEHIND ? At - BEHIND : 0ull);
-        W.hi = min(t1 + (uint64_t)HALO, doc_hi);
-        const uint64_t load_lo = W.lo & ~15ull;
-        const uint32_t v0 = (uint32_t)((load_lo - W.wbase) >> 4);
-        const uint32_t v1 = (uint32_t)((((W.hi + 15u) & ~15ull) - W.wbase) >> 4);
+        W.wbase = T.At - (uint64_t)BEHIND;
+        W.lo = T.wlo;
+        W.hi = T.whi;
 
         __syncthreads();  // previous tile fully consumed
         bool nonascii = false;
-        for (uint32_t v = v0 + tid; v < v1; v += WG) {
-            const uint4 x = reinterpret_cast<const uint4 *>(A.in + W.wbase)[v];
-            reinterpret_cast<uint4 *>(s_tile)[v] = x;
-            nonascii |= ((x.x | x.y | x.z | x.w) & 0x80808080u) != 0u;
+        if (T.v0 + tid < T.v1) {
+            reinterpret_cast<uint4 *>(s_tile)[T.v0 + tid] = pf0;
+            nonascii |= ((pf0.x | pf0.y | pf0.z | pf0.w) & 0x80808080u) != 0u;
         }
-        if (__syncthreads_or(nonascii)) {
+        if (T.v0 + tid + WG < T.v1) {
+            reinterpret_cast<uint4 *>(s_tile)[T.v0 + tid + WG] = pf1;
+            nonascii |= ((pf1.x | pf1.y | pf1.z | pf1.w) & 0x80808080u) != 0u;
+        }
+        const bool generic = __syncthreads_or(nonascii);
+        // next tile's loads fly while this one is processed
+        if (c + gridDim.x < A.n_chunks) {
+            nx = locate(A, c + gridDim.x);
+            const uint4 *src = reinterpret_cast<const uint4 *>(A.in + (nx.At - (uint64_t)BEHIND));
+            if (nx.v0 + tid < nx.v1) pf0 = src[nx.v0 + tid];
+            if (nx.v0 + tid + WG < nx.v1) pf1 = src[nx.v0 + tid + WG];
+        }
+        const uint64_t At = T.At, t0 = T.t0, t1 = T.t1, doc_lo = T.doc_lo, doc_hi = T.doc_hi;
+        const uint32_t docid = T.docid;
+
+        if (generic) {
             // ================= generic path: per-lane codepoint walker =================
             const uint64_t sg0 = At + (uint64_t)tid * SEG;
             const uint64_t s0 = max(sg0, t0);
@@ -317,11 +368,15 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
             uint32_t m = 0xAAAAAAAAu;
             if (g < NSEG && B < W.hi) {
                 const uint4 x = reinterpret_cast<const uint4 *>(s_tile)[1 + g];
-                const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
                 m = 0;
 #pragma unroll
-                for (int k = 0; k < 16; ++k)
-                    m |= (uint32_t)s_lut[(xs[k >> 2] >> (8 * (k & 3))) & 0x7Fu] << (2 * k);
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t w = k == 0 ? x.x : (k == 1 ? x.y : (k == 2 ? x.z : x.w));
+                    m |= (uint32_t)s_lut[w & 0x7Fu] << (8 * k);
+                    m |= (uint32_t)s_lut[(w >> 8) & 0x7Fu] << (8 * k + 2);
+                    m |= (uint32_t)s_lut[(w >> 16) & 0x7Fu] << (8 * k + 4);
+                    m |= (uint32_t)s_lut[w >> 24] << (8 * k + 6);
+                }
                 const uint32_t lo_inv = doc_lo > B ? (uint32_t)min<uint64_t>(doc_lo - B, 16) : 0u;
                 const uint32_t hi_ok = (uint32_t)min<uint64_t>(W.hi - B, 16);
                 const uint32_t vhi = hi_ok >= 16u ? 0xFFFFFFFFu : ((1u << (2u * hi_ok)) - 1u);
@@ -336,86 +391,85 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
         __syncthreads();
 
         // 2. token starts of this lane's tile segment -> per-wave queue
-        {
-            const uint32_t m = s_mask[tid];
-            const uint32_t prev = tid ? (s_mask[tid - 1] >> 31) : prevS_tile;
-            const uint32_t IS = m & 0xAAAAAAAAu;
-            uint32_t st = ~IS & ((IS << 2) | (prev << 1)) & 0xAAAAAAAAu;
-            if (At + (uint64_t)tid * SEG >= t1) st = 0;
-            const uint32_t cnt = __popc(st);
-            uint32_t incl = cnt;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t u = __shfl_up(incl, o);
-                if (lane >= o) incl += u;
-            }
-            uint32_t pos = incl - cnt;
-            while (st) {
-                const uint32_t k = (uint32_t)__builtin_ctz(st) >> 1;
-                s_queue[wv][pos++] = (uint16_t)(tid * SEG + k);
-                st &= st - 1u;
-            }
-            const uint32_t total = __shfl(incl, 63);
-            __syncthreads();
+        const uint32_t m = s_mask[tid];
+        const uint32_t prev = tid ? (s_mask[tid - 1] >> 31) : prevS_tile;
+        const uint32_t IS = m & 0xAAAAAAAAu;
+        uint32_t st = ~IS & ((IS << 2) | (prev << 1)) & 0xAAAAAAAAu;
+        if (At + (uint64_t)tid * SEG >= t1) st = 0;
+        const uint32_t cnt = __popc(st);
+        uint32_t incl = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o);
+            if (lane >= o) incl += u;
+        }
+        uint32_t pos = incl - cnt;
+        while (st) {
+            const uint32_t k = (uint32_t)__builtin_ctz(st) >> 1;
+            s_queue[wv][pos++] = (uint16_t)(tid * SEG + k);
+            st &= st - 1u;
+        }
+        const uint32_t total = __shfl(incl, 63);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-            // 3. tokens of the queue, one per lane per round
-            for (uint32_t base = 0; base < total; base += 64) {
-                const uint32_t q = base + lane;
-                bool have = false;
-                uint64_t tk0 = 0, tk1 = 0, tstart = 0;
-                uint32_t tlen = 0, traw = 0;
-                if (q < total) {
-                    const uint32_t s = s_queue[wv][q];
-                    const uint32_t g = s >> 4, i = s & 15u;
-                    const uint64_t win = (uint64_t)s_mask[g] | ((uint64_t)s_mask[g + 1] << 32);
-                    const uint64_t sr = (win & SBITS) >> (2u * i + 2u);
-                    bool slow = true;
-                    uint32_t n = 0;
-                    if (sr) {
-                        n = ((uint32_t)__builtin_ctzll(sr) >> 1) + 1u;  // raw length
-                        const uint64_t e = At + s + n;
-                        slow = (e >= W.hi) && (W.hi < doc_hi);        // ended at the staged edge
-                    }
-                    if (!slow) {
-                        const uint64_t w = (win >> (2u * i)) & WBITS & ((1ull << (2u * n)) - 1u);
-                        if (w) {
-                            const uint32_t first = (uint32_t)__builtin_ctzll(w) >> 1;
-                            const uint32_t last = (63u - (uint32_t)__builtin_clzll(w)) >> 1;
-                            const uint32_t L = last - first + 1u;
-                            const uint64_t pat = (WBITS >> (64u - 2u * L)) << (2u * first);
-                            if (w != pat) {
-                                slow = true;  // a deleted byte inside the token: exact walker
-                            } else {
-                                have = true;
-                                tlen = L;
-                                tstart = At + s;
-                                traw = n;
-                                if (L <= 16u) {
-                                    const uint32_t off = BEHIND + s + first;
-                                    const uint64_t *q64 = reinterpret_cast<const uint64_t *>(s_tile + (off & ~7u));
-                                    const uint64_t x0 = q64[0], x1 = q64[1], x2 = q64[2];
-                                    const uint32_t sh = (off & 7u) * 8u;
-                                    uint64_t lo = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
-                                    uint64_t hi = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
-                                    if (L < 8u) { lo &= (1ull << (8u * L)) - 1u; hi = 0; }
-                                    else if (L < 16u) hi &= (1ull << (8u * (L - 8u))) - 1u;
-                                    tk0 = __builtin_bswap64(lo);
-                                    tk1 = __builtin_bswap64(hi);
-                                }
+        // 3. tokens of the queue, one per lane per round (the queue and masks are read-only now)
+        for (uint32_t base = 0; base < total; base += 64) {
+            const uint32_t q = base + lane;
+            bool have = false;
+            uint64_t tk0 = 0, tk1 = 0, tstart = 0;
+            uint32_t tlen = 0, traw = 0;
+            if (q < total) {
+                const uint32_t s = s_queue[wv][q];
+                const uint32_t g = s >> 4, i = s & 15u;
+                const uint64_t win = (uint64_t)s_mask[g] | ((uint64_t)s_mask[g + 1] << 32);
+                const uint64_t sr = (win & SBITS) >> (2u * i + 2u);
+                bool slow = true;
+                uint32_t n = 0;
+                if (sr) {
+                    n = ((uint32_t)__builtin_ctzll(sr) >> 1) + 1u;  // raw length
+                    slow = (At + s + n >= W.hi) && (W.hi < doc_hi);  // ended at the staged edge
+                }
+                if (!slow) {
+                    const uint64_t w = (win >> (2u * i)) & WBITS & ((1ull << (2u * n)) - 1u);
+                    if (w) {
+                        const uint32_t first = (uint32_t)__builtin_ctzll(w) >> 1;
+                        const uint32_t last = (63u - (uint32_t)__builtin_clzll(w)) >> 1;
+                        const uint32_t L = last - first + 1u;
+                        const uint64_t pat = (WBITS >> (64u - 2u * L)) << (2u * first);
+                        if (w != pat) {
+                            slow = true;  // a deleted byte inside the token: exact walker
+                        } else {
+                            have = true;
+                            tlen = L;
+                            tstart = At + s;
+                            traw = n;
+                            if (L <= 16u) {
+                                const uint32_t off = BEHIND + s + first;
+                                const uint64_t *q64 = reinterpret_cast<const uint64_t *>(s_tile + (off & ~7u));
+                                const uint64_t x0 = q64[0], x1 = q64[1], x2 = q64[2];
+                                const uint32_t sh = (off & 7u) * 8u;
+                                uint64_t lo = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
+                                uint64_t hi = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
+                                if (L < 8u) { lo &= (1ull << (8u * L)) - 1u; hi = 0; }
+                                else if (L < 16u) hi &= (1ull << (8u * (L - 8u))) - 1u;
+                                tk0 = __builtin_bswap64(lo);
+                                tk1 = __builtin_bswap64(hi);
                             }
                         }
                     }
-                    if (slow) {
-                        uint64_t a0, a1, e;
-                        uint32_t L;
-                        if (walk_token(W, At + s, doc_hi, A.counters, a0, a1, L, e) && L > 0) {
-                            have = true;
-                            tk0 = a0; tk1 = a1; tlen = L; tstart = At + s; traw = (uint32_t)(e - (At + s));
-                        }
+                }
+                if (slow) {
+                    uint64_t a0, a1, e;
+                    uint32_t L;
+                    if (walk_token(W, At + s, doc_hi, A.counters, a0, a1, L, e) && L > 0) {
+                        have = true;
+                        tk0 = a0; tk1 = a1; tlen = L; tstart = At + s; traw = (uint32_t)(e - (At + s));
                     }
                 }
-                my_tokens += have ? 1u : 0u;
-                emit_round(A, table, s_wchunk[wv], s_wfill[wv], have, tk0, tk1, tlen, tstart, traw, docid, my_tail);
             }
+            my_tokens += have ? 1u : 0u;
+            emit_round(A, table, s_wchunk[wv], s_wfill[wv], have, tk0, tk1, tlen, tstart, traw, docid, my_tail);
         }
     }
 
@@ -438,13 +492,13 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
         uint32_t run = 0;
         for (int b0 = 0; b0 < MRG_NBUCKET; b0 += 64) {
             const uint32_t v = s_hist[b0 + lane];
-            uint32_t incl = v;
+            uint32_t inc = v;
             for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t u = __shfl_up(incl, o);
-                if (lane >= o) incl += u;
+                const uint32_t u = __shfl_up(inc, o);
+                if (lane >= o) inc += u;
             }
-            s_hist[b0 + lane] = run + incl - v;
-            run += __shfl(incl, 63);
+            s_hist[b0 + lane] = run + inc - v;
+            run += __shfl(inc, 63);
         }
         if (lane == 0) s_hist[MRG_NBUCKET] = run;
     }
@@ -456,14 +510,13 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
         if (s_k0[i] == MRG_EMPTY_K0) continue;
         const uint32_t d = IDX ? s_doc[i] : MRG_EMPTY_DOC;
         const uint32_t b = bucket_of(key_hash(s_k0[i], s_k1[i], d, A.hash_bits));
-        const uint64_t pos = reg + s_hist[b] + s_rank[i];
-        A.fk0[pos] = s_k0[i];
-        A.fk1[pos] = s_k1[i];
-        A.fcnt[pos] = s_cnt[i];
-        if (IDX) A.fdoc[pos] = d;
+        const uint64_t pos2 = reg + s_hist[b] + s_rank[i];
+        A.fk0[pos2] = s_k0[i];
+        A.fk1[pos2] = s_k1[i];
+        A.fcnt[pos2] = s_cnt[i];
+        if (IDX) A.fdoc[pos2] = d;
     }
-    uint64_t t = my_tokens;
-    uint64_t tl = my_tail;
+    uint32_t t = my_tokens, tl = my_tail;
     for (int off = 32; off > 0; off >>= 1) {
         t += __shfl_down(t, off);
         tl += __shfl_down(tl, off);
