@@ -178,7 +178,7 @@ __device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) {
 // (wchunk/wfill, in LDS): one HBM atomic per MRG_CHUNK_RECS records, never per round.
 template <int CAP, bool IDX>
 __device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> &table, uint32_t *wchunk,
-                                           uint32_t *wfill, bool have, uint64_t tk0, uint64_t tk1, uint32_t tlen,
+                                           uint32_t *wfill, const uint32_t *cbase, bool have, uint64_t tk0, uint64_t tk1, uint32_t tlen,
                                            uint64_t tstart, uint32_t traw, uint32_t docid, uint32_t &my_tail) {
     const bool is_long = have && tlen > 16u;
     bool tail = false;
@@ -199,8 +199,8 @@ __device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> 
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         if (tail && slot == CH) {  // this lane found the chunk full: it opens the next one
             const uint32_t fin = lds_ld(&wfill[b]);
-            const uint64_t cap = A.cbase[b + 1] - A.cbase[b];
-            if (c_old != MRG_NO_CHUNK && c_old < cap) A.chunk_fill[A.cbase[b] + c_old] = CH;
+            const uint32_t cap = cbase[b + 1] - cbase[b];
+            if (c_old != MRG_NO_CHUNK && c_old < cap) A.chunk_fill[(uint64_t)cbase[b] + c_old] = CH;
             const uint32_t nc = atomicAdd(&A.bucket_next[b], 1u);
             lds_st(&wchunk[b], nc);
             lds_st(&wfill[b], fin - CH);
@@ -209,8 +209,8 @@ __device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> 
         if (tail) {
             const uint32_t c = slot < CH ? c_old : lds_ld(&wchunk[b]);
             const uint32_t off = slot < CH ? slot : slot - CH;
-            if (c < A.cbase[b + 1] - A.cbase[b]) {
-                uint64_t *dst = A.pool + ((A.cbase[b] + c) * CH + off) * (IDX ? 3u : 2u);
+            if (c < cbase[b + 1] - cbase[b]) {
+                uint64_t *dst = A.pool + (((uint64_t)cbase[b] + c) * CH + off) * (IDX ? 3u : 2u);
                 dst[0] = tk0;
                 dst[1] = tk1;
                 if (IDX) dst[2] = docid;
@@ -241,6 +241,7 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
     __shared__ uint32_t s_wchunk[WG / 64][MRG_NBUCKET];  // per-wave current chunk of each bucket
     __shared__ uint32_t s_wfill[WG / 64][MRG_NBUCKET];   // records in it
     __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
+    __shared__ uint32_t s_cbase[MRG_NBUCKET + 1];       // first pool chunk of each bucket
     __shared__ uint16_t s_rank[CAP];
 
     const int tid = threadIdx.x;
@@ -255,6 +256,7 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
         (&s_wchunk[0][0])[i] = MRG_NO_CHUNK;
         (&s_wfill[0][0])[i] = MRG_CHUNK_RECS;  // "full": the first record opens a chunk
     }
+    for (int i = tid; i <= MRG_NBUCKET; i += WG) s_cbase[i] = (uint32_t)A.cbase[i];
     if (tid < 128) s_lut[tid] = (uint8_t)(mrg_uclass((uint32_t)tid) == MRG_CLS_W ? 1u
                                           : (mrg_uclass((uint32_t)tid) == MRG_CLS_S ? 2u : 0u));
     LdsTable<CAP, IDX> table{s_k0, s_k1, s_cnt, s_doc};
@@ -356,7 +358,7 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
                 }
                 if (!__any(have)) break;
                 my_tokens += have ? 1u : 0u;
-                emit_round(A, table, s_wchunk[wv], s_wfill[wv], have, tk0, tk1, tlen, tstart, traw, docid, my_tail);
+                emit_round(A, table, s_wchunk[wv], s_wfill[wv], s_cbase, have, tk0, tk1, tlen, tstart, traw, docid, my_tail);
             }
             continue;
         }
@@ -438,7 +440,21 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
                         const uint32_t L = last - first + 1u;
                         const uint64_t pat = (WBITS >> (64u - 2u * L)) << (2u * first);
                         if (w != pat) {
-                            slow = true;  // a deleted byte inside the token: exact walker
+                            // deleted (X) bytes inside an ASCII token ("don't"): keep the \w bytes
+                            uint64_t a0 = 0, a1 = 0;
+                            uint32_t LL = 0;
+                            for (uint32_t j = first; j <= last; ++j) {
+                                if ((w >> (2u * j)) & 1u) {
+                                    mrg_key_append(a0, a1, LL, s_tile[BEHIND + s + j]);
+                                    ++LL;
+                                }
+                            }
+                            have = true;
+                            tlen = LL;
+                            tstart = At + s;
+                            traw = n;
+                            tk0 = a0;
+                            tk1 = a1;
                         } else {
                             have = true;
                             tlen = L;
@@ -469,14 +485,14 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
                 }
             }
             my_tokens += have ? 1u : 0u;
-            emit_round(A, table, s_wchunk[wv], s_wfill[wv], have, tk0, tk1, tlen, tstart, traw, docid, my_tail);
+            emit_round(A, table, s_wchunk[wv], s_wfill[wv], s_cbase, have, tk0, tk1, tlen, tstart, traw, docid, my_tail);
         }
     }
 
     // ---- close this wave's open chunks
     for (int b = lane; b < MRG_NBUCKET; b += 64) {
         const uint32_t cch = s_wchunk[wv][b];
-        if (cch != MRG_NO_CHUNK && cch < A.cbase[b + 1] - A.cbase[b]) A.chunk_fill[A.cbase[b] + cch] = s_wfill[wv][b];
+        if (cch != MRG_NO_CHUNK && cch < s_cbase[b + 1] - s_cbase[b]) A.chunk_fill[(uint64_t)s_cbase[b] + cch] = s_wfill[wv][b];
     }
     // ---- flush the LDS table into this workgroup's region, sorted by bucket
     __syncthreads();

@@ -429,6 +429,7 @@ void job_map(mrg_ctx *c) {
             cbase[b + 1] = cbase[b] + bcap[b];
         }
         const uint64_t cbk = cbase[MRG_NBUCKET];
+        if (cbk > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
         M.cbase = pget<uint64_t>(p, MRG_NBUCKET + 1);
         HIPCHK(hipMemcpyAsync(M.cbase, cbase.data(), 8ull * (MRG_NBUCKET + 1), hipMemcpyHostToDevice, s));
         A.in = c->d_in;
