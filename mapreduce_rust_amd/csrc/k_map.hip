@@ -90,47 +90,70 @@ __device__ __forceinline__ uint32_t key_hash(uint64_t k0, uint64_t k1, uint32_t 
 }
 __device__ __forceinline__ uint32_t bucket_of(uint32_t h) { return h >> (32 - MRG_NBUCKET_LOG2); }
 
-// Workgroup LDS table of 8-slot groups with a monotone claim protocol: a slot goes
-// EMPTY -> k0 set -> k1 set (-> doc set) and never back; a key may complete a slot whose set words
-// equal its own; claims scan the group in slot order.  So a key lives in the first slot of its group
-// that was empty or its own when claimed, lanes racing on one slot agree on its owner, no locks.
-// The common cases -- the key's slot fully set (hit), or a full group without it (miss) -- are
-// decided from one snapshot of the group (8 + 8 LDS reads issued together); only claims use CAS.
+// exact per-byte zero test: bit 8j+7 set iff byte j of x is 0
+__device__ __forceinline__ uint64_t zero_bytes(uint64_t x) {
+    return ~(((x & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | x) & 0x8080808080808080ull;
+}
+
+// Workgroup LDS combine table: groups of 8 slots; a slot holds an 8-bit tag (0 =
+// empty), the packed key (k0, k1[, doc]) and a count.  Probe = one 8-byte read of the group's tags,
+// then the key of each tag-matching slot.  A new key claims an empty slot by CAS on its tag word and
+// then writes the key; a concurrent lookup that reads the slot before the key is written sees a
+// mismatch (an unwritten k0 is 0, which no key has) and goes on, so at worst one key occupies two
+// slots -- harmless, the table only pre-sums and every slot is flushed and summed again exactly.
+// A count is only ever added to a slot whose key equals the token's key.
 template <int CAP, bool IDX>
 struct LdsTable {
     static constexpr uint32_t NG = CAP / 8;
     unsigned long long *k0, *k1;
     unsigned int *cnt, *doc;
+    unsigned long long *tag;  // [NG]: the 8 tags of group g in bytes of tag[g]
+
+    __device__ __forceinline__ bool matches(uint32_t s, uint64_t a, uint64_t b, uint32_t d) const {
+        return k0[s] == a && k1[s] == b && (!IDX || doc[s] == d);
+    }
 
     __device__ __forceinline__ bool insert(uint64_t a, uint64_t b, uint32_t d, uint32_t h) {
-        const uint32_t g = (h & (NG - 1)) * 8u;
-        uint32_t hit = 0, open = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint64_t x = k0[g + j], y = k1[g + j];
-            const bool dm = !IDX || doc[g + j] == d;
-            hit |= (uint32_t)(x == a && y == b && dm) << j;
-            open |= (uint32_t)(x == MRG_EMPTY_K0 || (x == a && (y == MRG_EMPTY_K1 || (y == b && !dm)))) << j;
-        }
-        if (hit) {
-            atomicAdd(&cnt[g + (uint32_t)__builtin_ctz(hit)], 1u);
-            return true;
-        }
-        if (!open) return false;  // group full of other keys: miss
-        for (uint32_t j = 0; j < 8; ++j) {
-            const uint32_t s = g + j;
-            const unsigned long long x = atomicCAS(&k0[s], MRG_EMPTY_K0, (unsigned long long)a);
-            if (x != MRG_EMPTY_K0 && x != a) continue;
-            const unsigned long long y = atomicCAS(&k1[s], MRG_EMPTY_K1, (unsigned long long)b);
-            if (y != MRG_EMPTY_K1 && y != b) continue;
-            if (IDX) {
-                const unsigned int z = atomicCAS(&doc[s], MRG_EMPTY_DOC, d);
-                if (z != MRG_EMPTY_DOC && z != d) continue;
+        const uint32_t g = h & (NG - 1);
+        const uint64_t tg = ((h >> 16) & 0xFFu) | 1u;            // nonzero 8-bit tag
+        uint64_t tags = tag[g];
+        uint64_t cand = zero_bytes(tags ^ (tg * 0x0101010101010101ull));
+        while (cand) {
+            const uint32_t s = g * 8u + ((uint32_t)__builtin_ctzll(cand) >> 3);
+            if (matches(s, a, b, d)) {
+                atomicAdd(&cnt[s], 1u);
+                return true;
             }
-            atomicAdd(&cnt[s], 1u);
-            return true;
+            cand &= cand - 1u;
         }
-        return false;
+        uint64_t empty = zero_bytes(tags);
+        while (empty) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(empty) >> 3;
+            const uint64_t want = tags | (tg << (8u * j));
+            const uint64_t old = atomicCAS(&tag[g], tags, want);
+            if (old == tags) {  // slot j claimed
+                const uint32_t s = g * 8u + j;
+                k0[s] = a;
+                k1[s] = b;
+                if (IDX) doc[s] = d;
+                atomicAdd(&cnt[s], 1u);
+                return true;
+            }
+            // the group changed under us: a slot we had not checked may now hold the key
+            const uint64_t newly = zero_bytes(tags) & ~zero_bytes(old);
+            uint64_t nc = zero_bytes(old ^ (tg * 0x0101010101010101ull)) & newly;
+            while (nc) {
+                const uint32_t s = g * 8u + ((uint32_t)__builtin_ctzll(nc) >> 3);
+                if (matches(s, a, b, d)) {
+                    atomicAdd(&cnt[s], 1u);
+                    return true;
+                }
+                nc &= nc - 1u;
+            }
+            tags = old;
+            empty = zero_bytes(tags);
+        }
+        return false;  // group full of other keys: miss
     }
 };
 
@@ -238,6 +261,7 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
     __shared__ __attribute__((aligned(16))) unsigned long long s_k1[CAP];
     __shared__ unsigned int s_cnt[CAP];
     __shared__ __attribute__((aligned(16))) unsigned int s_doc[IDX ? CAP : 1];
+    __shared__ unsigned long long s_tag[CAP / 8];
     __shared__ uint32_t s_wchunk[WG / 64][MRG_NBUCKET];  // per-wave current chunk of each bucket
     __shared__ uint32_t s_wfill[WG / 64][MRG_NBUCKET];   // records in it
     __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
@@ -252,6 +276,7 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
         s_cnt[i] = 0;
         if (IDX) s_doc[i] = MRG_EMPTY_DOC;
     }
+    for (int i = tid; i < CAP / 8; i += WG) s_tag[i] = 0;
     for (int i = tid; i < (WG / 64) * MRG_NBUCKET; i += WG) {
         (&s_wchunk[0][0])[i] = MRG_NO_CHUNK;
         (&s_wfill[0][0])[i] = MRG_CHUNK_RECS;  // "full": the first record opens a chunk
@@ -259,7 +284,7 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
     for (int i = tid; i <= MRG_NBUCKET; i += WG) s_cbase[i] = (uint32_t)A.cbase[i];
     if (tid < 128) s_lut[tid] = (uint8_t)(mrg_uclass((uint32_t)tid) == MRG_CLS_W ? 1u
                                           : (mrg_uclass((uint32_t)tid) == MRG_CLS_S ? 2u : 0u));
-    LdsTable<CAP, IDX> table{s_k0, s_k1, s_cnt, s_doc};
+    LdsTable<CAP, IDX> table{s_k0, s_k1, s_cnt, s_doc, s_tag};
     uint32_t my_tokens = 0, my_tail = 0;
 
     // prefetch of the first tile

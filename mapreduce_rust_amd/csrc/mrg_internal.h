@@ -14,7 +14,7 @@
 // MRG_CHUNK_RECS records; one workgroup per bucket later sums them in LDS (k_keys.hip).
 #define MRG_NBUCKET_LOG2 9
 #define MRG_NBUCKET (1 << MRG_NBUCKET_LOG2)
-#define MRG_CHUNK_RECS 128
+#define MRG_CHUNK_RECS 256
 #define MRG_NO_CHUNK 0xFFFFFFFFu
 #define MRG_BA_CAP 4096          // LDS table slots of the per-bucket aggregation kernel
 
