@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import mapreduce_rust_amd as M  # noqa: E402
+from mapreduce_rust_amd import shuffle as S  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MIB = 1 << 20
@@ -49,27 +50,6 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lds-cap", type=int, default=0)
     return ap.parse_args()
-
-
-def exchange(ctx, n_owners, dev):
-    """Shuffle step: pack per owner, all-to-all of counts, records and heap bytes (RCCL), import."""
-    rec, heap = ctx.export_sizes(n_owners)
-    send_rec = torch.empty(max(sum(rec), 1) * 40, dtype=torch.uint8, device=dev)
-    send_heap = torch.empty(max(sum(heap), 1), dtype=torch.uint8, device=dev)
-    ctx.export(send_rec.data_ptr(), send_heap.data_ptr())
-    counts = torch.tensor(rec + heap, dtype=torch.int64, device=dev)
-    recv_counts = torch.empty_like(counts)
-    dist.all_to_all_single(recv_counts, counts.view(2, n_owners).t().contiguous().view(-1),
-                           [2] * n_owners, [2] * n_owners)
-    rc = recv_counts.view(n_owners, 2).cpu().tolist()
-    r_rec = [a for a, _ in rc]
-    r_heap = [b for _, b in rc]
-    recv_rec = torch.empty(max(sum(r_rec), 1) * 40, dtype=torch.uint8, device=dev)
-    recv_heap = torch.empty(max(sum(r_heap), 1), dtype=torch.uint8, device=dev)
-    dist.all_to_all_single(recv_rec[:sum(r_rec) * 40], send_rec[:sum(rec) * 40],
-                           [x * 40 for x in r_rec], [x * 40 for x in rec])
-    dist.all_to_all_single(recv_heap[:sum(r_heap)], send_heap[:sum(heap)], r_heap, heap)
-    ctx.import_(recv_rec.data_ptr(), sum(r_rec), recv_heap.data_ptr(), sum(r_heap), r_rec, r_heap)
 
 
 def cpu_baseline(sample, n_reduce):
@@ -129,7 +109,7 @@ def main():
         ctx.set_input(buf.data_ptr(), doc_off, doc_ids)
         ctx.map()
         if world > 1:
-            exchange(ctx, world, dev)
+            S.shuffle(ctx, world, dev)  # RCCL all-to-all over xGMI, owner(r) = r % N
         return ctx.reduce()
 
     for w in range(a.warmup):

@@ -1,0 +1,59 @@
+"""Multi-GPU static plan and the shuffle exchange (torch.distributed: RCCL on GPU, gloo on CPU).
+
+The reference coordinator hands out map tasks (input files) and reduce tasks (partitions) on demand
+(src/mr/coordinator.rs:137-215) and the shuffle goes through mr-{m}-{r}.txt files in a shared CWD
+(src/mr/worker.rs:117-140, 79-109).  Here the plan is static: rank g maps its shard of the input
+files, and owns every partition r with r % G == g.  After the map each rank packs its per-key
+records by owner (mrg_job_export), one all-to-all of the per-owner counts tells every rank how much
+it receives, and two all-to-all(v)s move the 40-byte exchange records and the long-key heap bytes.
+The receiving rank re-aggregates (mrg_job_import: the same key can arrive from every rank) and
+reduces its partitions.  There is exactly one data-path collective, the exchange itself.
+"""
+import torch
+import torch.distributed as dist
+
+XREC = 40
+
+
+def owner_of(partition, n_owners):
+    """Static plan: partition r is reduced by rank r % G."""
+    return partition % n_owners
+
+
+def shard_files(n_files, rank, world):
+    """Map shard of a rank: files rank, rank + G, ... (equal bytes for equal-size files)."""
+    return list(range(rank, n_files, world))
+
+
+def alltoall_exchange(send_rec, send_heap, rec_counts, heap_counts, group=None):
+    """Exchange per-owner slices.  send_rec: uint8 tensor of sum(rec_counts) * 40 bytes ordered by
+    owner; send_heap: uint8 tensor of sum(heap_counts) bytes ordered by owner.
+    Returns (recv_rec, recv_heap, recv_rec_counts, recv_heap_counts), ordered by sender."""
+    world = dist.get_world_size(group)
+    dev = send_rec.device
+    counts = torch.tensor(list(rec_counts) + list(heap_counts), dtype=torch.int64, device=dev)
+    # [rec_0..rec_{G-1}, heap_0..heap_{G-1}] -> per destination (rec_o, heap_o) pairs
+    send_c = counts.view(2, world).t().contiguous().view(-1)
+    recv_c = torch.empty_like(send_c)
+    dist.all_to_all_single(recv_c, send_c, [2] * world, [2] * world, group=group)
+    rc = recv_c.view(world, 2).cpu().tolist()
+    r_rec = [int(a) for a, _ in rc]
+    r_heap = [int(b) for _, b in rc]
+    recv_rec = torch.empty(max(sum(r_rec), 1) * XREC, dtype=torch.uint8, device=dev)
+    recv_heap = torch.empty(max(sum(r_heap), 1), dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(recv_rec[:sum(r_rec) * XREC], send_rec[:sum(rec_counts) * XREC],
+                           [x * XREC for x in r_rec], [x * XREC for x in rec_counts], group=group)
+    dist.all_to_all_single(recv_heap[:sum(r_heap)], send_heap[:sum(heap_counts)], r_heap, list(heap_counts),
+                           group=group)
+    return recv_rec, recv_heap, r_rec, r_heap
+
+
+def shuffle(ctx, world, device, group=None):
+    """The exchange step of a device-resident job on every rank (after ctx.map())."""
+    rec, heap = ctx.export_sizes(world)
+    send_rec = torch.empty(max(sum(rec), 1) * XREC, dtype=torch.uint8, device=device)
+    send_heap = torch.empty(max(sum(heap), 1), dtype=torch.uint8, device=device)
+    ctx.export(send_rec.data_ptr(), send_heap.data_ptr())
+    recv_rec, recv_heap, r_rec, r_heap = alltoall_exchange(send_rec, send_heap, rec, heap, group)
+    ctx.import_(recv_rec.data_ptr(), sum(r_rec), recv_heap.data_ptr(), sum(r_heap), r_rec, r_heap)
+    return sum(r_rec), sum(r_heap)

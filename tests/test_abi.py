@@ -1,0 +1,53 @@
+"""CPU tests of the C ABI boundary: libmrgpu.so loads, exports every entry point declared in
+include/mrgpu.h, the Python binding covers them all, and errors come back as status codes (no GPU
+here: mrg_open must fail cleanly, never abort)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "mrgpu.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*(mrg_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_the_boundary():
+    fns = header_functions()
+    for f in ["mrg_open", "mrg_close", "mrg_map", "mrg_reduce", "mrg_run_job", "mrg_free", "mrg_last_error",
+              "mrg_job_begin", "mrg_job_map", "mrg_job_export", "mrg_job_import", "mrg_job_reduce"]:
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    import mapreduce_rust_amd as M
+    lib = ctypes.CDLL(M.lib_path())
+    missing = [f for f in header_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_the_header():
+    from mapreduce_rust_amd import native
+    assert sorted(native.exported_symbols()) == header_functions()
+    native.load()
+
+
+def test_no_gpu_is_a_clean_error():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    import mapreduce_rust_amd as M
+    with pytest.raises(M.MrgError) as ei:
+        M.Context(0)
+    assert ei.value.code == -3
+    assert M.native.load().mrg_version().startswith(b"mrgpu")
+
+
+def test_record_layout_constant():
+    src = open(os.path.join(ROOT, "include", "mrgpu.h")).read()
+    assert "#define MRG_XREC_BYTES 40" in src
+    from mapreduce_rust_amd import native, shuffle
+    assert native.XREC_BYTES == shuffle.XREC == 40
