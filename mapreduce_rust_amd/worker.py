@@ -1,0 +1,84 @@
+"""Host-side mirror of the reference Worker (src/mr/worker.rs) over libmrgpu.so.
+
+Same task structure and file conventions as the reference:
+  Worker(map_n, reduce_n)                     worker.rs:28-37
+  Worker.map(m):    data/gut-{m}.txt  ->  mr-{m}-{r}.rec for r < reduce_n     worker.rs:142-155
+  Worker.reduce(r): mr-{m}-{r}.rec for m < map_n  ->  mr-{r}.txt              worker.rs:157-193
+Map output per partition is the engine's combined form (per-key counts as 40-byte exchange
+records + long-key heap, include/mrgpu.h) instead of one "key 1" text line per token; mr-{r}.txt
+is byte-identical to the reference's.  A map task and a reduce task may run in different
+processes, as in the reference (the files in the working directory are the hand-off).
+
+Record file layout (little-endian): u64 n_records, u64 heap_bytes, records, heap.
+"""
+import os
+import struct
+
+from . import native
+
+APPS = {"wc": native.APP_WC, "indexer": native.APP_INDEXER}
+
+
+def _rec_path(m, r, cwd):
+    return os.path.join(cwd, f"mr-{m}-{r}.rec")
+
+
+class Worker:
+    def __init__(self, map_n, reduce_n, app="wc", device=0, flags=0, cwd="."):
+        if app not in APPS:
+            raise ValueError(f"unknown app {app!r}")
+        self.map_n, self.reduce_n = map_n, reduce_n
+        self.app = APPS[app]
+        self.flags = flags
+        self.cwd = cwd
+        self.ctx = native.Context(device)
+
+    def doc_name(self, m):
+        return f"data/gut-{m}.txt"      # worker.rs:67
+
+    def map(self, m):
+        """Map task m: the input file's bytes -> per-partition records."""
+        with open(os.path.join(self.cwd, self.doc_name(m)), "rb") as f:   # worker.rs:73-75
+            data = f.read()
+        parts = self.ctx.map_task(self.app, data, self.doc_name(m), m, self.reduce_n, self.flags)
+        try:
+            for r in range(self.reduce_n):                                 # worker.rs:120-125
+                rec, heap = parts.get(r)
+                with open(_rec_path(m, r, self.cwd), "wb") as f:
+                    f.write(struct.pack("<QQ", len(rec) // native.XREC_BYTES, len(heap)))
+                    f.write(rec)
+                    f.write(heap)
+        finally:
+            parts.free()
+        return True
+
+    def reduce(self, r):
+        """Reduce task r: every map task's records of partition r -> mr-{r}.txt."""
+        import ctypes
+        recs, heaps, seg_r, seg_h = [], [], [], []
+        for m in range(self.map_n):                                        # worker.rs:84-107
+            with open(_rec_path(m, r, self.cwd), "rb") as f:
+                n, hb = struct.unpack("<QQ", f.read(16))
+                recs.append(f.read(n * native.XREC_BYTES))
+                heaps.append(f.read(hb))
+                seg_r.append(n)
+                seg_h.append(hb)
+        out = self._reduce_records(r, b"".join(recs), b"".join(heaps), seg_r, seg_h)
+        with open(os.path.join(self.cwd, f"mr-{r}.txt"), "wb") as f:       # worker.rs:167-168
+            f.write(out)
+        return True
+
+    def _reduce_records(self, r, rec, heap, seg_r, seg_h):
+        import torch
+        dev = torch.device("cuda", self.ctx.device)
+        d_rec = torch.frombuffer(bytearray(rec) + bytearray(16), dtype=torch.uint8).to(dev)
+        d_heap = torch.frombuffer(bytearray(heap) + bytearray(16), dtype=torch.uint8).to(dev)
+        self.ctx.job_begin(self.app, self.reduce_n, self.flags)
+        if self.app == native.APP_INDEXER:
+            self.ctx.set_doc_names([self.doc_name(m) for m in range(self.map_n)])
+        self.ctx.import_(d_rec.data_ptr(), sum(seg_r), d_heap.data_ptr(), sum(seg_h), seg_r, seg_h)
+        self.ctx.reduce()
+        return self.ctx.outputs()[r]
+
+    def close(self):
+        self.ctx.close()

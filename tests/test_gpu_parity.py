@@ -247,3 +247,34 @@ def test_run_job_cli_files(tmp_path, corpus):
         os.chdir(cwd)
     for r in range(10):
         assert sha((tmp_path / f"mr-{r}.txt").read_bytes()) == GOLDEN["wc"]["10"][f"mr-{r}.txt"]
+
+
+def test_worker_tasks_through_files(tmp_path, corpus):
+    """Reference task structure: 6 map tasks then 10 reduce tasks, hand-off through files."""
+    from mapreduce_rust_amd.worker import Worker
+    (tmp_path / "data").mkdir()
+    for m in range(6):
+        (tmp_path / "data" / f"gut-{m}.txt").write_bytes(corpus[m])
+    w = Worker(6, 10, cwd=str(tmp_path))
+    for m in range(6):
+        assert w.map(m)
+    w2 = Worker(6, 10, cwd=str(tmp_path))   # a second worker process would do the same
+    for r in range(10):
+        assert w2.reduce(r)
+        assert sha((tmp_path / f"mr-{r}.txt").read_bytes()) == GOLDEN["wc"]["10"][f"mr-{r}.txt"], r
+    w.close()
+    w2.close()
+
+
+def test_worker_indexer_tasks(tmp_path, corpus):
+    from mapreduce_rust_amd.worker import Worker
+    (tmp_path / "data").mkdir()
+    for m in range(6):
+        (tmp_path / "data" / f"gut-{m}.txt").write_bytes(corpus[m])
+    w = Worker(6, 10, app="indexer", cwd=str(tmp_path))
+    for m in range(6):
+        w.map(m)
+    for r in range(10):
+        w.reduce(r)
+        assert sha((tmp_path / f"mr-{r}.txt").read_bytes()) == GOLDEN["indexer"]["10"][f"mr-{r}.txt"], r
+    w.close()
