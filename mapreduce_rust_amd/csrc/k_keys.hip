@@ -15,7 +15,7 @@ namespace {
 inline dim3 grid_for(uint64_t n, int b = 256) { return dim3((unsigned)((n + b - 1) / b)); }
 
 // ---------------------------------------------------------------- per-bucket LDS aggregation
-// One workgroup per hash bucket sums every record of its bucket -- the map kernel's tail chunks
+// One workgroup per hash bucket sums every record of its bucket -- the map workgroups' tail regions
 // (count 1 each) and the bucket's slice of every map workgroup's flushed LDS table -- in an LDS
 // table with the monotone claim protocol.  A key that finds no slot (more distinct keys in the
 // bucket than the table holds) is written to the overflow list; since slots only ever fill, a key
@@ -72,40 +72,31 @@ __global__ __launch_bounds__(BA_WG) void k_bucket_agg(BucketArgs A) {
     }
     __syncthreads();
     const uint32_t b = blockIdx.x;
-    constexpr uint32_t CH = MRG_CHUNK_RECS;
     constexpr uint32_t RW = IDX ? 3u : 2u;
-    const uint64_t nch = min((uint64_t)A.bucket_next[b], A.cbase[b + 1] - A.cbase[b]);
-    const uint64_t total = nch * CH;
-    const uint64_t *pool = A.pool + A.cbase[b] * CH * RW;
-    const uint32_t *fill = A.chunk_fill + A.cbase[b];
-    // tail chunks
-    for (uint64_t base = 0; base < total; base += BA_WG) {
-        const uint64_t i = base + tid;
-        bool valid = false;
-        uint64_t a = 0, c = 0;
-        uint32_t d = MRG_EMPTY_DOC;
-        if (i < total) {
-            const uint32_t ch = (uint32_t)(i / CH), off = (uint32_t)(i % CH);
-            if (off < fill[ch]) {
-                valid = true;
-                const uint64_t *r = pool + i * RW;
-                a = r[0];
-                c = r[1];
-                if (IDX) d = (uint32_t)r[2];
+    const uint32_t cap = A.bcap[b];
+    // every map workgroup r left (a) its tail records of this bucket in region (b, r) of the pool
+    // and (b) this bucket's slice of its flushed LDS table; wave wv takes r = wv, wv + 8, ...
+    for (uint32_t r = wv; r < A.nreg; r += BA_WG / 64) {
+        const uint32_t n = min(A.bcount[(uint64_t)r * MRG_NBUCKET + b], cap);
+        const uint64_t *src = A.pool + (A.rbase[b] + (uint64_t)r * cap) * RW;
+        for (uint32_t base = 0; base < n; base += 64) {
+            const uint32_t i = base + lane;
+            bool ovf = false;
+            uint64_t a = 0, c = 0;
+            uint32_t d = MRG_EMPTY_DOC;
+            if (i < n) {
+                const uint64_t *rec = src + (uint64_t)i * RW;
+                a = rec[0];
+                c = rec[1];
+                if (IDX) d = (uint32_t)rec[2];
+                ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
+            }
+            const uint64_t j = mrg_wave_append(&A.counters[CNT_OVF2], ovf);
+            if (ovf && j < A.ocap) {
+                A.ok0[j] = a; A.ok1[j] = c; A.ocnt[j] = 1u;
+                if (IDX) A.odoc[j] = d;
             }
         }
-        bool ovf = false;
-        if (valid) {
-            ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
-        }
-        const uint64_t j = mrg_wave_append(&A.counters[CNT_OVF2], ovf);
-        if (ovf && j < A.ocap) {
-            A.ok0[j] = a; A.ok1[j] = c; A.ocnt[j] = 1u;
-            if (IDX) A.odoc[j] = d;
-        }
-    }
-    // flushed LDS tables of the map workgroups: this bucket's slice of every region
-    for (uint32_t r = wv; r < A.nreg; r += BA_WG / 64) {
         const uint32_t *fo = A.foff + (uint64_t)r * (MRG_NBUCKET + 1);
         const uint32_t lo = fo[b], hi = fo[b + 1];
         const uint64_t reg = (uint64_t)r * A.regcap;
@@ -113,17 +104,17 @@ __global__ __launch_bounds__(BA_WG) void k_bucket_agg(BucketArgs A) {
             const uint32_t k = base + lane;
             bool ovf = false;
             uint64_t a = 0, c = 0;
-            uint32_t d = MRG_EMPTY_DOC, n = 0;
+            uint32_t d = MRG_EMPTY_DOC, n2 = 0;
             if (k < hi) {
                 a = A.fk0[reg + k];
                 c = A.fk1[reg + k];
-                n = A.fcnt[reg + k];
+                n2 = A.fcnt[reg + k];
                 if (IDX) d = A.fdoc[reg + k];
-                ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, n, ba_hash(a, c, d, A.hash_bits));
+                ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, n2, ba_hash(a, c, d, A.hash_bits));
             }
             const uint64_t j = mrg_wave_append(&A.counters[CNT_OVF2], ovf);
             if (ovf && j < A.ocap) {
-                A.ok0[j] = a; A.ok1[j] = c; A.ocnt[j] = n;
+                A.ok0[j] = a; A.ok1[j] = c; A.ocnt[j] = n2;
                 if (IDX) A.odoc[j] = d;
             }
         }

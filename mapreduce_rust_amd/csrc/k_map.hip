@@ -6,42 +6,47 @@
 // SipHash(key) % R is a pure function of the key.  Also validates UTF-8 like read_to_string
 // (worker.rs:75): the first invalid byte offset is reported and the job fails with MRG_EUTF8.
 //
-// Layout: documents back to back in one HBM buffer; each document is cut into 4 KiB
-// tiles on a 16-byte-aligned grid; a persistent grid of 256-thread workgroups walks the tiles, the
-// next tile's 16-byte loads in flight (registers) while the current one is processed from LDS.
+// Layout: documents back to back in one HBM buffer; each document is cut into 1 KiB
+// tiles on a 16-byte-aligned grid.  A persistent grid of 512-thread workgroups (8 waves) walks the
+// tiles, and every WAVE works on a tile of its own -- no workgroup barrier in the main loop: the
+// wave's next tile (64 lanes x 16 B + halo) is in flight in registers while it processes the
+// current one from its private LDS window.  The 8 waves share the workgroup's combine table.
 //
 // ASCII tiles (the common case; wave-uniform test) take the fast path:
 //   1. every lane classifies one 16-byte segment through a 128-entry LDS LUT into an interleaved
 //      32-bit mask (bit 2k = byte k is \w, bit 2k+1 = byte k is White_Space);
-//   2. token starts = non-space bytes after a space: mask arithmetic; each wave compacts its starts
-//      into an LDS queue (wave prefix sum) so that all 64 lanes then work on one token each;
+//   2. token starts = non-space bytes after a space: mask arithmetic, the previous byte's class
+//      from the neighbour lane (shuffle); the wave compacts its starts into an LDS queue (prefix
+//      sum) so that all 64 lanes then work on one token each;
 //   3. per token: end = next space bit, key = the \w bytes -- contiguous unless a deleted byte sits
 //      inside the token ("don't") -- read as 3 x 8 B from LDS and packed big-endian into (k0, k1);
-//      interior deletions, > 31-byte raw tokens and tokens running past the halo take the exact
-//      per-codepoint walker.
+//      > 31-byte raw tokens and tokens running past the halo take the exact per-codepoint walker.
 // Non-ASCII tiles use the per-codepoint walker for every token (UTF-8 decode + class table).
-// Keys of <= 16 bytes go to a workgroup-private LDS hash table (exact: the packed key IS the
-// identity) of 8-slot groups probed with one batched read; misses are appended to one of 512 hash
-// buckets in HBM through per-wave chunk cursors.  Keys > 16 bytes become long-token records
-// (start, raw length, doc) resolved by the collision-safe fingerprint sort (k_keys.hip).  At the end
-// the LDS table is flushed, sorted by bucket, into the workgroup's region.
+// Keys of <= 16 bytes go to the workgroup's LDS hash table (exact: the packed key IS the identity)
+// of 8-slot tagged groups; a miss is appended to one of 512 hash buckets in HBM, into the region
+// this workgroup owns in that bucket (an LDS cursor per bucket: no HBM atomics).  Keys > 16 bytes
+// become long-token records (start, raw length, doc) resolved by the collision-safe fingerprint
+// sort (k_keys.hip).  At the end the LDS table is flushed, sorted by bucket, into the workgroup's
+// flush region.
 #include "mrg_device.h"
 #include "mrg_internal.h"
 
 namespace {
 
 constexpr int WG = MRG_MAP_WG;
+constexpr int NWAVE = WG / 64;
 constexpr int SEG = MRG_MAP_SEG;
 constexpr int TILE = MRG_MAP_TILE;
 constexpr int HALO = MRG_MAP_HALO;
 constexpr int BEHIND = MRG_MAP_BEHIND;
-constexpr int NSEG = (TILE + HALO) / SEG;           // classified segments: tile + halo
-constexpr int LDS_BYTES = BEHIND + TILE + HALO + 32;
-constexpr int NVEC_MAX = (LDS_BYTES + 15) / 16;     // 16-byte vectors per staged window (<= 2 per thread)
-constexpr int QCAP = WG / 4 * SEG / 2;              // tokens per wave per tile <= 512
+constexpr int NSEG = TILE / SEG + 1;                // classified segments: tile + first halo segment
+constexpr int LDS_BYTES = BEHIND + TILE + HALO + 32;  // per wave (+32: 3 x 8 B key reads at the edge)
+constexpr int NVEC_MAX = (BEHIND + TILE + HALO + 15) / 16;  // staged 16-byte vectors per tile
+constexpr int QCAP = TILE / 2;                      // tokens per tile <= 512
 constexpr uint64_t SBITS = 0xAAAAAAAAAAAAAAAAull;    // odd bits: White_Space flags
 constexpr uint64_t WBITS = 0x5555555555555555ull;    // even bits: \w flags
-static_assert(NVEC_MAX <= 2 * WG, "two prefetch vectors per thread");
+static_assert(NVEC_MAX <= 128, "two prefetch vectors per lane");
+static_assert(TILE == 64 * SEG, "one segment per lane");
 
 // LDS-staged window: byte a lives at lds[a - wbase] when lo <= a < hi, else it is read from HBM.
 struct Window {
@@ -189,20 +194,14 @@ __device__ __noinline__ bool walk_token(const RD &rd, uint64_t a, uint64_t doc_h
     return true;
 }
 
-__device__ __forceinline__ uint32_t lds_ld(uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
 // One round of token emission by a whole wave (all 64 lanes must call it): LDS-table insert of short
-// keys; misses are appended to their hash bucket through this wave's private chunk cursors
-// (wchunk/wfill, in LDS): one HBM atomic per MRG_CHUNK_RECS records, never per round.
+// keys; a miss is appended to its hash bucket's region of this workgroup (an LDS counter per
+// bucket, no HBM atomics).  Long keys become long-token records.
 template <int CAP, bool IDX>
-__device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> &table, uint32_t *wchunk,
-                                           uint32_t *wfill, const uint32_t *cbase, bool have, uint64_t tk0, uint64_t tk1, uint32_t tlen,
-                                           uint64_t tstart, uint32_t traw, uint32_t docid, uint32_t &my_tail) {
+__device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> &table, uint32_t *bcount,
+                                           const uint32_t *bcap, const unsigned long long *bbase, bool have,
+                                           uint64_t tk0, uint64_t tk1, uint32_t tlen, uint64_t tstart, uint32_t traw,
+                                           uint32_t docid) {
     const bool is_long = have && tlen > 16u;
     bool tail = false;
     uint32_t h = 0;
@@ -211,36 +210,16 @@ __device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> 
         h = key_hash(tk0, tk1, dkey, A.hash_bits);
         tail = !table.insert(tk0, tk1, dkey, h);
     }
-    if (__any(tail)) {
-        constexpr uint32_t CH = MRG_CHUNK_RECS;
+    if (tail) {
         const uint32_t b = bucket_of(h);
-        uint32_t slot = 0, c_old = MRG_NO_CHUNK;
-        if (tail) {
-            c_old = lds_ld(&wchunk[b]);
-            slot = atomicAdd(&wfill[b], 1u);
-        }
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (tail && slot == CH) {  // this lane found the chunk full: it opens the next one
-            const uint32_t fin = lds_ld(&wfill[b]);
-            const uint32_t cap = cbase[b + 1] - cbase[b];
-            if (c_old != MRG_NO_CHUNK && c_old < cap) A.chunk_fill[(uint64_t)cbase[b] + c_old] = CH;
-            const uint32_t nc = atomicAdd(&A.bucket_next[b], 1u);
-            lds_st(&wchunk[b], nc);
-            lds_st(&wfill[b], fin - CH);
-        }
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (tail) {
-            const uint32_t c = slot < CH ? c_old : lds_ld(&wchunk[b]);
-            const uint32_t off = slot < CH ? slot : slot - CH;
-            if (c < cbase[b + 1] - cbase[b]) {
-                uint64_t *dst = A.pool + (((uint64_t)cbase[b] + c) * CH + off) * (IDX ? 3u : 2u);
-                dst[0] = tk0;
-                dst[1] = tk1;
-                if (IDX) dst[2] = docid;
-            } else {
-                atomicAdd(&A.counters[CNT_OVF], 1ull);
-            }
-            ++my_tail;
+        const uint32_t slot = atomicAdd(&bcount[b], 1u);
+        if (slot < bcap[b]) {
+            uint64_t *dst = A.pool + (bbase[b] + slot) * (IDX ? 3u : 2u);
+            dst[0] = tk0;
+            dst[1] = tk1;
+            if (IDX) dst[2] = docid;
+        } else {
+            atomicAdd(&A.counters[CNT_OVF], 1ull);
         }
     }
     const uint64_t li = mrg_wave_append(&A.counters[CNT_LONG], is_long);
@@ -251,22 +230,30 @@ __device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> 
     }
 }
 
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int CAP, bool IDX>
-__global__ __launch_bounds__(WG) void k_map(MapArgs A) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_tile[LDS_BYTES];
-    __shared__ uint32_t s_mask[NSEG + 2];
-    __shared__ uint16_t s_queue[WG / 64][QCAP];
+__global__ __launch_bounds__(WG, CAP >= 4096 ? 2 : 4) void k_map(MapArgs A) {
+    // per wave: staged window, segment masks, token queue (waves work on their own tiles)
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[NWAVE][LDS_BYTES];
+    __shared__ uint32_t s_mask[NWAVE][NSEG];
+    __shared__ uint16_t s_queue[NWAVE][QCAP];
     __shared__ uint8_t s_lut[128];
+    // workgroup: combine table + tail-region cursors
     __shared__ __attribute__((aligned(16))) unsigned long long s_k0[CAP];
     __shared__ __attribute__((aligned(16))) unsigned long long s_k1[CAP];
     __shared__ unsigned int s_cnt[CAP];
     __shared__ __attribute__((aligned(16))) unsigned int s_doc[IDX ? CAP : 1];
     __shared__ unsigned long long s_tag[CAP / 8];
-    __shared__ uint32_t s_wchunk[WG / 64][MRG_NBUCKET];  // per-wave current chunk of each bucket
-    __shared__ uint32_t s_wfill[WG / 64][MRG_NBUCKET];   // records in it
+    __shared__ uint32_t s_bcount[MRG_NBUCKET];           // records appended to (bucket, this WG)
+    __shared__ uint32_t s_bcap[MRG_NBUCKET];
+    __shared__ unsigned long long s_bbase[MRG_NBUCKET];  // first pool record of (bucket, this WG)
     __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
-    __shared__ uint32_t s_cbase[MRG_NBUCKET + 1];       // first pool chunk of each bucket
-    __shared__ uint16_t s_rank[CAP];
+    static_assert(sizeof(s_queue) >= CAP * sizeof(uint16_t), "flush ranks reuse the queues");
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
@@ -277,60 +264,67 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
         if (IDX) s_doc[i] = MRG_EMPTY_DOC;
     }
     for (int i = tid; i < CAP / 8; i += WG) s_tag[i] = 0;
-    for (int i = tid; i < (WG / 64) * MRG_NBUCKET; i += WG) {
-        (&s_wchunk[0][0])[i] = MRG_NO_CHUNK;
-        (&s_wfill[0][0])[i] = MRG_CHUNK_RECS;  // "full": the first record opens a chunk
+    for (int b = tid; b < MRG_NBUCKET; b += WG) {
+        s_bcount[b] = 0;
+        const uint32_t cap = A.bcap[b];
+        s_bcap[b] = cap;
+        s_bbase[b] = A.rbase[b] + (uint64_t)blockIdx.x * cap;
     }
-    for (int i = tid; i <= MRG_NBUCKET; i += WG) s_cbase[i] = (uint32_t)A.cbase[i];
     if (tid < 128) s_lut[tid] = (uint8_t)(mrg_uclass((uint32_t)tid) == MRG_CLS_W ? 1u
                                           : (mrg_uclass((uint32_t)tid) == MRG_CLS_S ? 2u : 0u));
     LdsTable<CAP, IDX> table{s_k0, s_k1, s_cnt, s_doc, s_tag};
-    uint32_t my_tokens = 0, my_tail = 0;
+    uint32_t my_tokens = 0;
+    uint8_t *tile = s_tile[wv];
+    uint32_t *mask = s_mask[wv];
+    uint16_t *queue = s_queue[wv];
+    __syncthreads();
 
     // prefetch of the first tile
-    uint64_t c = blockIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
+    uint64_t c = (uint64_t)blockIdx.x * NWAVE + wv;
     TileInfo nx{};
     uint4 pf0 = {0, 0, 0, 0}, pf1 = {0, 0, 0, 0};
     if (c < A.n_chunks) {
         nx = locate(A, c);
         const uint4 *src = reinterpret_cast<const uint4 *>(A.in + (nx.At - (uint64_t)BEHIND));
-        if (nx.v0 + tid < nx.v1) pf0 = src[nx.v0 + tid];
-        if (nx.v0 + tid + WG < nx.v1) pf1 = src[nx.v0 + tid + WG];
+        if (nx.v0 + lane < nx.v1) pf0 = src[nx.v0 + lane];
+        if (nx.v0 + lane + 64 < nx.v1) pf1 = src[nx.v0 + lane + 64];
     }
 
-    for (; c < A.n_chunks; c += gridDim.x) {
+    for (; c < A.n_chunks; c += stride) {
         const TileInfo T = nx;
         Window W;
-        W.lds = s_tile;
+        W.lds = tile;
         W.g = A.in;
         W.wbase = T.At - (uint64_t)BEHIND;
         W.lo = T.wlo;
         W.hi = T.whi;
 
-        __syncthreads();  // previous tile fully consumed
+        // this wave finished its previous tile (program order): the buffers are free
         bool nonascii = false;
-        if (T.v0 + tid < T.v1) {
-            reinterpret_cast<uint4 *>(s_tile)[T.v0 + tid] = pf0;
+        if (T.v0 + lane < T.v1) {
+            reinterpret_cast<uint4 *>(tile)[T.v0 + lane] = pf0;
             nonascii |= ((pf0.x | pf0.y | pf0.z | pf0.w) & 0x80808080u) != 0u;
         }
-        if (T.v0 + tid + WG < T.v1) {
-            reinterpret_cast<uint4 *>(s_tile)[T.v0 + tid + WG] = pf1;
+        if (T.v0 + lane + 64 < T.v1) {
+            reinterpret_cast<uint4 *>(tile)[T.v0 + lane + 64] = pf1;
             nonascii |= ((pf1.x | pf1.y | pf1.z | pf1.w) & 0x80808080u) != 0u;
         }
-        const bool generic = __syncthreads_or(nonascii);
+        const bool generic = __any(nonascii);
         // next tile's loads fly while this one is processed
-        if (c + gridDim.x < A.n_chunks) {
-            nx = locate(A, c + gridDim.x);
+        if (c + stride < A.n_chunks) {
+            nx = locate(A, c + stride);
             const uint4 *src = reinterpret_cast<const uint4 *>(A.in + (nx.At - (uint64_t)BEHIND));
-            if (nx.v0 + tid < nx.v1) pf0 = src[nx.v0 + tid];
-            if (nx.v0 + tid + WG < nx.v1) pf1 = src[nx.v0 + tid + WG];
+            if (nx.v0 + lane < nx.v1) pf0 = src[nx.v0 + lane];
+            if (nx.v0 + lane + 64 < nx.v1) pf1 = src[nx.v0 + lane + 64];
         }
+        wave_sync_lds();
         const uint64_t At = T.At, t0 = T.t0, t1 = T.t1, doc_lo = T.doc_lo, doc_hi = T.doc_hi;
         const uint32_t docid = T.docid;
 
         if (generic) {
             // ================= generic path: per-lane codepoint walker =================
-            const uint64_t sg0 = At + (uint64_t)tid * SEG;
+            const uint64_t sg0 = At + (uint64_t)lane * SEG;
             const uint64_t s0 = max(sg0, t0);
             const uint64_t s1 = min(sg0 + (uint64_t)SEG, t1);
             bool done = s0 >= s1;
@@ -383,46 +377,44 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
                 }
                 if (!__any(have)) break;
                 my_tokens += have ? 1u : 0u;
-                emit_round(A, table, s_wchunk[wv], s_wfill[wv], s_cbase, have, tk0, tk1, tlen, tstart, traw, docid, my_tail);
+                emit_round(A, table, s_bcount, s_bcap, s_bbase, have, tk0, tk1, tlen, tstart, traw, docid);
             }
             continue;
         }
 
         // ================= ASCII fast path =================
-        // 1. classify: segment g covers [At + 16 g, +16); bytes outside [doc_lo, W.hi) count as space
-        for (int g = tid; g < NSEG + 2; g += WG) {
+        // 1. classify: segment g covers [At + 16 g, +16); bytes outside [doc_lo, W.hi) count as space.
+        //    Segments 0..63 are the tile (one per lane), segment 64 the first halo segment.
+        auto classify = [&](uint32_t g) -> uint32_t {
             const uint64_t B = At + (uint64_t)g * SEG;
-            uint32_t m = 0xAAAAAAAAu;
-            if (g < NSEG && B < W.hi) {
-                const uint4 x = reinterpret_cast<const uint4 *>(s_tile)[1 + g];
-                m = 0;
+            if (B >= W.hi) return 0xAAAAAAAAu;
+            const uint4 x = reinterpret_cast<const uint4 *>(tile)[1 + g];
+            uint32_t m = 0;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t w = k == 0 ? x.x : (k == 1 ? x.y : (k == 2 ? x.z : x.w));
-                    m |= (uint32_t)s_lut[w & 0x7Fu] << (8 * k);
-                    m |= (uint32_t)s_lut[(w >> 8) & 0x7Fu] << (8 * k + 2);
-                    m |= (uint32_t)s_lut[(w >> 16) & 0x7Fu] << (8 * k + 4);
-                    m |= (uint32_t)s_lut[w >> 24] << (8 * k + 6);
-                }
-                const uint32_t lo_inv = doc_lo > B ? (uint32_t)min<uint64_t>(doc_lo - B, 16) : 0u;
-                const uint32_t hi_ok = (uint32_t)min<uint64_t>(W.hi - B, 16);
-                const uint32_t vhi = hi_ok >= 16u ? 0xFFFFFFFFu : ((1u << (2u * hi_ok)) - 1u);
-                const uint32_t vlo = lo_inv >= 16u ? 0xFFFFFFFFu : ((1u << (2u * lo_inv)) - 1u);
-                const uint32_t valid = vhi & ~vlo;
-                m = (m & valid) | (0xAAAAAAAAu & ~valid);
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t w = k == 0 ? x.x : (k == 1 ? x.y : (k == 2 ? x.z : x.w));
+                m |= (uint32_t)s_lut[w & 0x7Fu] << (8 * k);
+                m |= (uint32_t)s_lut[(w >> 8) & 0x7Fu] << (8 * k + 2);
+                m |= (uint32_t)s_lut[(w >> 16) & 0x7Fu] << (8 * k + 4);
+                m |= (uint32_t)s_lut[w >> 24] << (8 * k + 6);
             }
-            s_mask[g] = m;
-        }
-        uint32_t prevS_tile = 1u;  // class of the byte before the tile
-        if (At > doc_lo) prevS_tile = (s_lut[s_tile[BEHIND - 1] & 0x7Fu] >> 1) & 1u;
-        __syncthreads();
-
-        // 2. token starts of this lane's tile segment -> per-wave queue
-        const uint32_t m = s_mask[tid];
-        const uint32_t prev = tid ? (s_mask[tid - 1] >> 31) : prevS_tile;
+            const uint32_t lo_inv = doc_lo > B ? (uint32_t)min<uint64_t>(doc_lo - B, 16) : 0u;
+            const uint32_t hi_ok = (uint32_t)min<uint64_t>(W.hi - B, 16);
+            const uint32_t vhi = hi_ok >= 16u ? 0xFFFFFFFFu : ((1u << (2u * hi_ok)) - 1u);
+            const uint32_t vlo = lo_inv >= 16u ? 0xFFFFFFFFu : ((1u << (2u * lo_inv)) - 1u);
+            const uint32_t valid = vhi & ~vlo;
+            return (m & valid) | (0xAAAAAAAAu & ~valid);
+        };
+        const uint32_t m = classify((uint32_t)lane);
+        mask[lane] = m;
+        if (lane == 0) mask[64] = classify(64u);
+        // 2. token starts of this lane's segment (the previous byte's class: the neighbour lane's
+        //    mask, or the staged byte before the tile) -> the wave's queue (prefix sum)
+        uint32_t prev = __shfl_up(m >> 31, 1);
+        if (lane == 0) prev = At > doc_lo ? (s_lut[tile[BEHIND - 1] & 0x7Fu] >> 1) & 1u : 1u;
         const uint32_t IS = m & 0xAAAAAAAAu;
         uint32_t st = ~IS & ((IS << 2) | (prev << 1)) & 0xAAAAAAAAu;
-        if (At + (uint64_t)tid * SEG >= t1) st = 0;
+        if (At + (uint64_t)lane * SEG >= t1) st = 0;
         const uint32_t cnt = __popc(st);
         uint32_t incl = cnt;
         for (int o = 1; o < 64; o <<= 1) {
@@ -432,13 +424,11 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
         uint32_t pos = incl - cnt;
         while (st) {
             const uint32_t k = (uint32_t)__builtin_ctz(st) >> 1;
-            s_queue[wv][pos++] = (uint16_t)(tid * SEG + k);
+            queue[pos++] = (uint16_t)(lane * SEG + k);
             st &= st - 1u;
         }
         const uint32_t total = __shfl(incl, 63);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_sync_lds();
 
         // 3. tokens of the queue, one per lane per round (the queue and masks are read-only now)
         for (uint32_t base = 0; base < total; base += 64) {
@@ -447,9 +437,9 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
             uint64_t tk0 = 0, tk1 = 0, tstart = 0;
             uint32_t tlen = 0, traw = 0;
             if (q < total) {
-                const uint32_t s = s_queue[wv][q];
+                const uint32_t s = queue[q];
                 const uint32_t g = s >> 4, i = s & 15u;
-                const uint64_t win = (uint64_t)s_mask[g] | ((uint64_t)s_mask[g + 1] << 32);
+                const uint64_t win = (uint64_t)mask[g] | ((uint64_t)mask[g + 1] << 32);
                 const uint64_t sr = (win & SBITS) >> (2u * i + 2u);
                 bool slow = true;
                 uint32_t n = 0;
@@ -470,7 +460,7 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
                             uint32_t LL = 0;
                             for (uint32_t j = first; j <= last; ++j) {
                                 if ((w >> (2u * j)) & 1u) {
-                                    mrg_key_append(a0, a1, LL, s_tile[BEHIND + s + j]);
+                                    mrg_key_append(a0, a1, LL, tile[BEHIND + s + j]);
                                     ++LL;
                                 }
                             }
@@ -487,7 +477,7 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
                             traw = n;
                             if (L <= 16u) {
                                 const uint32_t off = BEHIND + s + first;
-                                const uint64_t *q64 = reinterpret_cast<const uint64_t *>(s_tile + (off & ~7u));
+                                const uint64_t *q64 = reinterpret_cast<const uint64_t *>(tile + (off & ~7u));
                                 const uint64_t x0 = q64[0], x1 = q64[1], x2 = q64[2];
                                 const uint32_t sh = (off & 7u) * 8u;
                                 uint64_t lo = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
@@ -510,17 +500,19 @@ __global__ __launch_bounds__(WG) void k_map(MapArgs A) {
                 }
             }
             my_tokens += have ? 1u : 0u;
-            emit_round(A, table, s_wchunk[wv], s_wfill[wv], s_cbase, have, tk0, tk1, tlen, tstart, traw, docid, my_tail);
+            emit_round(A, table, s_bcount, s_bcap, s_bbase, have, tk0, tk1, tlen, tstart, traw, docid);
         }
     }
 
-    // ---- close this wave's open chunks
-    for (int b = lane; b < MRG_NBUCKET; b += 64) {
-        const uint32_t cch = s_wchunk[wv][b];
-        if (cch != MRG_NO_CHUNK && cch < s_cbase[b + 1] - s_cbase[b]) A.chunk_fill[(uint64_t)s_cbase[b] + cch] = s_wfill[wv][b];
-    }
     // ---- flush the LDS table into this workgroup's region, sorted by bucket
     __syncthreads();
+    uint16_t *s_rank = &s_queue[0][0];
+    uint32_t *bcount = A.bcount + (uint64_t)blockIdx.x * MRG_NBUCKET;
+    uint32_t my_tail = 0;
+    for (int b = tid; b < MRG_NBUCKET; b += WG) {
+        my_tail += s_bcount[b];
+        bcount[b] = s_bcount[b];
+    }
     for (int b = tid; b <= MRG_NBUCKET; b += WG) s_hist[b] = 0;
     __syncthreads();
     for (int i = tid; i < CAP; i += WG) {

@@ -4,18 +4,17 @@
 #include <stddef.h>
 #include <stdint.h>
 
-#define MRG_MAP_WG 256          // threads per map workgroup (4 waves)
+#define MRG_MAP_WG 512          // threads per map workgroup (8 waves sharing one LDS table)
 #define MRG_MAP_SEG 16          // input bytes per lane per tile
-#define MRG_MAP_TILE (MRG_MAP_WG * MRG_MAP_SEG)  // 4 KiB tile per workgroup iteration
-#define MRG_MAP_HALO 256        // bytes after the tile staged in LDS (tokens crossing the tile end)
+#define MRG_MAP_TILE (64 * MRG_MAP_SEG)  // 1 KiB tile per WAVE iteration (waves never synchronise)
+#define MRG_MAP_HALO 64         // bytes after the tile staged in LDS (tokens crossing the tile end)
 #define MRG_MAP_BEHIND 16       // bytes before the tile staged in LDS (previous codepoint)
 
-// Tail records (LDS-table misses) are bucketed by key hash into MRG_NBUCKET buckets of chunks of
-// MRG_CHUNK_RECS records; one workgroup per bucket later sums them in LDS (k_keys.hip).
+// Tail records (LDS-table misses) are bucketed by key hash into MRG_NBUCKET buckets; every
+// (bucket, map workgroup) pair owns a private region of the pool, so appending is an LDS atomic.
+// One workgroup per bucket later sums them in LDS (k_keys.hip).
 #define MRG_NBUCKET_LOG2 9
 #define MRG_NBUCKET (1 << MRG_NBUCKET_LOG2)
-#define MRG_CHUNK_RECS 256
-#define MRG_NO_CHUNK 0xFFFFFFFFu
 #define MRG_BA_CAP 4096          // LDS table slots of the per-bucket aggregation kernel
 
 // counters[] slots written by the kernels
@@ -25,7 +24,7 @@ enum {
     CNT_TOKENS = 2,   // tokens
     CNT_ERRPOS = 3,   // first invalid UTF-8 byte (atomicMin), ~0 if none
     CNT_KEYS = 4,     // distinct keys appended to the KeySet
-    CNT_OVF = 5,      // tail records that found no chunk (pool too small: rerun)
+    CNT_OVF = 5,      // tail records beyond their region's capacity (pool too small: rerun)
     CNT_OVF2 = 6,     // keys that did not fit their bucket's LDS table (exact overflow path)
     CNT_N = 8
 };
@@ -45,12 +44,12 @@ struct MapArgs {
     const uint32_t *doc_id;      // [n_docs] global document id
     uint32_t n_docs;
     uint64_t n_chunks;
-    // tail records (LDS-table misses, count 1): bucket b owns chunks [cbase[b], cbase[b+1]) of the
-    // pool; record = pool[((cbase[b] + chunk) * CHUNK + off) * RECW + w]
+    // tail records (LDS-table misses, count 1): map workgroup w appends the records of bucket b to
+    // pool records [rbase[b] + w * bcap[b], + bcap[b]); record i = pool[i * RECW .. + RECW)
     uint64_t *pool;
-    const uint64_t *cbase;       // [NBUCKET + 1] first chunk of each bucket
-    uint32_t *bucket_next;       // [NBUCKET] chunks handed out per bucket (may exceed capacity)
-    uint32_t *chunk_fill;        // [cbase[NBUCKET]] records in each chunk
+    const uint64_t *rbase;       // [NBUCKET] first record of bucket b's regions
+    const uint32_t *bcap;        // [NBUCKET] records per (bucket, workgroup) region
+    uint32_t *bcount;            // [grid * NBUCKET] records appended (may exceed bcap: rerun)
     // LDS-table flush: workgroup g writes its entries to [g * CAP, ...) sorted by bucket;
     // foff[g * (NBUCKET + 1) + b] = start of bucket b in that region
     uint64_t *fk0, *fk1;
@@ -95,7 +94,7 @@ struct LongItems {
 
 // ---- k_map.hip
 void mrg_launch_map(const MapArgs &a, int app, int grid, int lds_cap, hipStream_t s);
-uint64_t mrg_map_tiles(uint64_t doc_lo, uint64_t doc_hi);  // 4 KiB tiles of a document (16-B grid)
+uint64_t mrg_map_tiles(uint64_t doc_lo, uint64_t doc_hi);  // 1 KiB wave tiles of a document (16-B grid)
 int mrg_map_cap(int lds_cap);  // LDS-table entries per map workgroup actually used for lds_cap
 int mrg_map_max_grid(int app, int lds_cap, int device);
 void mrg_launch_long_prep(const uint8_t *base, const uint64_t *start, const uint32_t *rawlen, uint64_t n,
@@ -107,8 +106,8 @@ void mrg_launch_long_gather(const uint8_t *base, const uint64_t *start, const ui
 // ---- k_keys.hip
 struct BucketArgs {
     const uint64_t *pool;
-    const uint64_t *cbase;
-    const uint32_t *bucket_next, *chunk_fill;
+    const uint64_t *rbase;
+    const uint32_t *bcap, *bcount;
     const uint64_t *fk0, *fk1;
     const uint32_t *fcnt, *fdoc, *foff;
     uint32_t nreg, regcap;       // map workgroups (flush regions) and entries per region

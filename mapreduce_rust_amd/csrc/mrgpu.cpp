@@ -141,7 +141,7 @@ struct mrg_ctx {
     int lds_cap = 2048;
     int map_grid = 0;
     uint64_t long_hint = 0, ovf_hint = 0;
-    std::vector<uint64_t> bcap_hint;  // chunks per tail bucket
+    std::vector<double> bcap_rate;  // tail records per (bucket, map workgroup) per input byte of the workgroup
     // job
     bool job = false;
     int app = 0;
@@ -305,14 +305,14 @@ void aggregate(mrg_ctx *c, const ShortSrc &src, LongItems li) {
 }
 
 struct MapBufs {
-    uint64_t *pool = nullptr, *cbase = nullptr;
-    uint32_t *bucket_next = nullptr, *chunk_fill = nullptr;
+    uint64_t *pool = nullptr, *rbase = nullptr;
+    uint32_t *bcap = nullptr, *bcount = nullptr;
     uint64_t *fk0 = nullptr, *fk1 = nullptr;
     uint32_t *fcnt = nullptr, *fdoc = nullptr, *foff = nullptr;
     uint64_t *lstart = nullptr;
     uint32_t *llen = nullptr, *ldoc = nullptr;
     void release(Pool &p) {
-        p.put(pool); p.put(cbase); p.put(bucket_next); p.put(chunk_fill);
+        p.put(pool); p.put(rbase); p.put(bcap); p.put(bcount);
         p.put(fk0); p.put(fk1); p.put(fcnt); p.put(fdoc); p.put(foff);
         p.put(lstart); p.put(llen); p.put(ldoc);
         *this = MapBufs{};
@@ -329,7 +329,7 @@ void bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
     for (;;) {
         keys_reserve(c, (uint64_t)MRG_NBUCKET * MRG_BA_CAP + ocap + li.n + 1);
         BucketArgs B{};
-        B.pool = A.pool; B.cbase = A.cbase; B.bucket_next = A.bucket_next; B.chunk_fill = A.chunk_fill;
+        B.pool = A.pool; B.rbase = A.rbase; B.bcap = A.bcap; B.bcount = A.bcount;
         B.fk0 = A.fk0; B.fk1 = A.fk1; B.fcnt = A.fcnt; B.fdoc = A.fdoc; B.foff = A.foff;
         B.nreg = nreg; B.regcap = regcap;
         B.ok0 = pget<uint64_t>(p, ocap); B.ok1 = pget<uint64_t>(p, ocap);
@@ -412,35 +412,41 @@ void job_map(mrg_ctx *c) {
     const uint32_t cap = (uint32_t)mrg_map_cap(c->lds_cap);
     const bool idx = is_idx(c);
     const uint32_t RW = idx ? 3u : 2u;
-    const uint64_t tail_est = total / 20 + 4096;
     uint64_t lcap = std::max<uint64_t>(c->long_hint, total / 1024 + 1024);
-    // chunks per bucket: the expected tail + one open chunk per map wave (grown per bucket on demand)
-    const uint64_t waves = (uint64_t)grid * (MRG_MAP_WG / 64);
-    std::vector<uint64_t> bcap(MRG_NBUCKET, tail_est / ((uint64_t)MRG_NBUCKET * MRG_CHUNK_RECS) + waves + 4);
-    if (c->bcap_hint.size() == MRG_NBUCKET)
-        for (int b = 0; b < MRG_NBUCKET; ++b) bcap[b] = std::max(bcap[b], c->bcap_hint[b]);
+    // records per (bucket, workgroup) tail region: ~1 in 20 input bytes is a tail record (combine
+    // misses), spread evenly over the buckets; grown per bucket to the measured demand on a rerun
+    const double per_wg = (double)std::max<uint64_t>(total, 1) / grid;
+    std::vector<uint64_t> bcap(MRG_NBUCKET);
+    for (int b = 0; b < MRG_NBUCKET; ++b) {
+        double est = per_wg / 20.0 / MRG_NBUCKET;
+        if (c->bcap_rate.size() == MRG_NBUCKET) est = std::max(est, c->bcap_rate[b] * per_wg);
+        bcap[b] = (uint64_t)(est * 1.25) + 32;
+    }
     MapArgs A{};
     MapBufs M;
     uint32_t launches = 0;
     for (;;) {
-        std::vector<uint64_t> cbase(MRG_NBUCKET + 1, 0);
+        std::vector<uint64_t> rbase(MRG_NBUCKET, 0);
+        std::vector<uint32_t> bcap32(MRG_NBUCKET);
+        uint64_t rtot = 0;
         for (int b = 0; b < MRG_NBUCKET; ++b) {
             if (bcap[b] > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
-            cbase[b + 1] = cbase[b] + bcap[b];
+            bcap32[b] = (uint32_t)bcap[b];
+            rbase[b] = rtot;
+            rtot += (uint64_t)grid * bcap[b];
         }
-        const uint64_t cbk = cbase[MRG_NBUCKET];
-        if (cbk > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
-        M.cbase = pget<uint64_t>(p, MRG_NBUCKET + 1);
-        HIPCHK(hipMemcpyAsync(M.cbase, cbase.data(), 8ull * (MRG_NBUCKET + 1), hipMemcpyHostToDevice, s));
+        M.rbase = pget<uint64_t>(p, MRG_NBUCKET);
+        M.bcap = pget<uint32_t>(p, MRG_NBUCKET);
+        M.bcount = pget<uint32_t>(p, (uint64_t)grid * MRG_NBUCKET);
+        HIPCHK(hipMemcpyAsync(M.rbase, rbase.data(), 8ull * MRG_NBUCKET, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(M.bcap, bcap32.data(), 4ull * MRG_NBUCKET, hipMemcpyHostToDevice, s));
         A.in = c->d_in;
         A.doc_off = d_doc_off;
         A.chunk_base = d_cb;
         A.doc_id = d_ids;
         A.n_docs = nd;
         A.n_chunks = n_chunks;
-        M.pool = pget<uint64_t>(p, cbk * MRG_CHUNK_RECS * RW);
-        M.bucket_next = pget<uint32_t>(p, MRG_NBUCKET);
-        M.chunk_fill = pget<uint32_t>(p, cbk);
+        M.pool = pget<uint64_t>(p, rtot * RW);
         M.fk0 = pget<uint64_t>(p, (uint64_t)grid * cap);
         M.fk1 = pget<uint64_t>(p, (uint64_t)grid * cap);
         M.fcnt = pget<uint32_t>(p, (uint64_t)grid * cap);
@@ -449,14 +455,13 @@ void job_map(mrg_ctx *c) {
         M.lstart = pget<uint64_t>(p, lcap);
         M.llen = pget<uint32_t>(p, lcap);
         M.ldoc = pget<uint32_t>(p, lcap);
-        A.pool = M.pool; A.cbase = M.cbase; A.bucket_next = M.bucket_next; A.chunk_fill = M.chunk_fill;
+        A.pool = M.pool; A.rbase = M.rbase; A.bcap = M.bcap; A.bcount = M.bcount;
         A.fk0 = M.fk0; A.fk1 = M.fk1; A.fcnt = M.fcnt; A.fdoc = M.fdoc; A.foff = M.foff;
         A.lstart = M.lstart; A.llen = M.llen; A.ldoc = M.ldoc; A.lcap = lcap;
         A.counters = c->d_cnt;
         A.hash_bits = hash_bits(c);
         HIPCHK(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long) * CNT_N, s));
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_ERRPOS], 0xFF, sizeof(unsigned long long), s));
-        HIPCHK(hipMemsetAsync(M.bucket_next, 0, 4ull * MRG_NBUCKET, s));
         ev_rec(c, 0);
         mrg_launch_map(A, c->app, grid, c->lds_cap, s);  // also with no tiles: writes empty flush regions
         ev_rec(c, 1);
@@ -465,13 +470,18 @@ void job_map(mrg_ctx *c) {
         read_counters(c);
         const uint64_t nl = c->h_cnt[CNT_LONG];
         if (c->h_cnt[CNT_OVF] == 0 && nl <= lcap) break;
-        // capacity exceeded: grow each bucket to its demand (remembered for later jobs), run again
+        // capacity exceeded: grow each bucket's regions to its demand (remembered), run again
         if (c->h_cnt[CNT_OVF]) {
-            std::vector<uint32_t> next(MRG_NBUCKET);
-            HIPCHK(hipMemcpyAsync(next.data(), M.bucket_next, 4ull * MRG_NBUCKET, hipMemcpyDeviceToHost, s));
+            std::vector<uint32_t> cnt((uint64_t)grid * MRG_NBUCKET);
+            HIPCHK(hipMemcpyAsync(cnt.data(), M.bcount, 4ull * cnt.size(), hipMemcpyDeviceToHost, s));
             sync(c);
-            for (int b = 0; b < MRG_NBUCKET; ++b) bcap[b] = std::max<uint64_t>(bcap[b], next[b] + next[b] / 8 + 4);
-            c->bcap_hint = bcap;
+            c->bcap_rate.assign(MRG_NBUCKET, 0.0);
+            for (int b = 0; b < MRG_NBUCKET; ++b) {
+                uint64_t mx = 0;
+                for (int g = 0; g < grid; ++g) mx = std::max<uint64_t>(mx, cnt[(uint64_t)g * MRG_NBUCKET + b]);
+                bcap[b] = std::max<uint64_t>(bcap[b], mx + mx / 8 + 32);
+                c->bcap_rate[b] = (double)mx / per_wg;
+            }
         }
         if (nl > lcap) lcap = c->long_hint = nl + nl / 8 + 1024;
         if (getenv("MRG_DEBUG"))
