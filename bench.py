@@ -132,8 +132,8 @@ def main():
         for k in stage:
             stage[k] += s[k] / a.steps
         if rank == 0:
-            log(f"step: map {s['ms_map']:.2f} ms, agg {s['ms_aggregate']:.2f}, sort {s['ms_sort']:.2f}, "
-                f"format {s['ms_format']:.2f}")
+            log(f"step: map {s['ms_map']:.2f} ms ({s['map_launches']} launch), agg {s['ms_aggregate']:.2f}, "
+                f"sort {s['ms_sort']:.2f}, format {s['ms_format']:.2f}")
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

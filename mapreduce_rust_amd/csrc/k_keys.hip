@@ -119,6 +119,29 @@ __global__ __launch_bounds__(BA_WG) void k_bucket_agg(BucketArgs A) {
             }
         }
     }
+    // records that did not fit their map workgroup's region: this bucket's overflow list
+    {
+        const uint32_t n = min(A.monext[b], A.mocap);
+        const uint64_t *src = A.movf + (uint64_t)b * A.mocap * RW;
+        for (uint32_t base = wv * 64u; base < n; base += BA_WG) {
+            const uint32_t i = base + lane;
+            bool ovf = false;
+            uint64_t a = 0, c = 0;
+            uint32_t d = MRG_EMPTY_DOC;
+            if (i < n) {
+                const uint64_t *rec = src + (uint64_t)i * RW;
+                a = rec[0];
+                c = rec[1];
+                if (IDX) d = (uint32_t)rec[2];
+                ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
+            }
+            const uint64_t j = mrg_wave_append(&A.counters[CNT_OVF2], ovf);
+            if (ovf && j < A.ocap) {
+                A.ok0[j] = a; A.ok1[j] = c; A.ocnt[j] = 1u;
+                if (IDX) A.odoc[j] = d;
+            }
+        }
+    }
     __syncthreads();
     for (int i0 = 0; i0 < BA_CAP; i0 += BA_WG) {
         const int i = i0 + tid;

@@ -43,6 +43,11 @@ constexpr int NSEG = TILE / SEG + 1;                // classified segments: tile
 constexpr int LDS_BYTES = BEHIND + TILE + HALO + 32;  // per wave (+32: 3 x 8 B key reads at the edge)
 constexpr int NVEC_MAX = (BEHIND + TILE + HALO + 15) / 16;  // staged 16-byte vectors per tile
 constexpr int QCAP = TILE / 2;                      // tokens per tile <= 512
+// queue entry (u32): start (10 bits) | raw length n << 10 | key span first << 16 | L << 21 | kind << 27
+constexpr uint32_t QK_PLAIN = 0;  // \w bytes contiguous: key = bytes [first, first + L) of the token
+constexpr uint32_t QK_INNER = 1;  // deleted bytes inside the token ("don't")
+constexpr uint32_t QK_SLOW = 2;   // longer than the 2-segment window or cut by the staged edge: walker
+constexpr uint32_t QK_EMPTY = 3;  // no \w byte: not a token
 constexpr uint64_t SBITS = 0xAAAAAAAAAAAAAAAAull;    // odd bits: White_Space flags
 constexpr uint64_t WBITS = 0x5555555555555555ull;    // even bits: \w flags
 static_assert(NVEC_MAX <= 128, "two prefetch vectors per lane");
@@ -63,12 +68,11 @@ struct TileInfo {
     uint32_t docid, v0, v1;
 };
 
-__device__ __forceinline__ TileInfo locate(const MapArgs &A, uint64_t c) {
-    uint32_t lo_d = 0, hi_d = A.n_docs;  // chunk_base[d] <= c < chunk_base[d+1]
-    while (hi_d - lo_d > 1) {
-        const uint32_t mid = (lo_d + hi_d) >> 1;
-        if (A.chunk_base[mid] <= c) lo_d = mid; else hi_d = mid;
-    }
+// Tile c of the job.  A wave visits its tiles in increasing order, so the document index only moves
+// forward from the previous tile's (usually not at all).
+__device__ __forceinline__ TileInfo locate(const MapArgs &A, uint64_t c, uint32_t &d) {
+    while (A.chunk_base[d + 1] <= c) ++d;  // chunk_base[d] <= c < chunk_base[d+1]
+    const uint32_t lo_d = d;
     TileInfo t;
     t.doc_lo = A.doc_off[lo_d];
     t.doc_hi = A.doc_off[lo_d + 1];
@@ -115,7 +119,9 @@ struct LdsTable {
     unsigned long long *tag;  // [NG]: the 8 tags of group g in bytes of tag[g]
 
     __device__ __forceinline__ bool matches(uint32_t s, uint64_t a, uint64_t b, uint32_t d) const {
-        return k0[s] == a && k1[s] == b && (!IDX || doc[s] == d);
+        // both key words are read before either is compared: one LDS round trip, not two
+        const uint64_t x = (k0[s] ^ a) | (k1[s] ^ b);
+        return x == 0 && (!IDX || doc[s] == d);
     }
 
     __device__ __forceinline__ bool insert(uint64_t a, uint64_t b, uint32_t d, uint32_t h) {
@@ -208,18 +214,23 @@ __device__ __forceinline__ void emit_round(const MapArgs &A, LdsTable<CAP, IDX> 
     const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
     if (have && !is_long) {
         h = key_hash(tk0, tk1, dkey, A.hash_bits);
-        tail = !table.insert(tk0, tk1, dkey, h);
+        tail = (A.ablate & 2u) ? true : !table.insert(tk0, tk1, dkey, h);
     }
-    if (tail) {
+    if (tail && !(A.ablate & 1u)) {
         const uint32_t b = bucket_of(h);
         const uint32_t slot = atomicAdd(&bcount[b], 1u);
+        uint64_t *dst = nullptr;
         if (slot < bcap[b]) {
-            uint64_t *dst = A.pool + (bbase[b] + slot) * (IDX ? 3u : 2u);
+            dst = A.pool + (bbase[b] + slot) * (IDX ? 3u : 2u);
+        } else {  // region full (rare): the bucket's shared overflow list
+            const uint32_t j = atomicAdd(&A.onext[b], 1u);
+            if (j < A.ocap) dst = A.ovf + ((uint64_t)b * A.ocap + j) * (IDX ? 3u : 2u);
+            else atomicAdd(&A.counters[CNT_OVF], 1ull);
+        }
+        if (dst) {
             dst[0] = tk0;
             dst[1] = tk1;
             if (IDX) dst[2] = docid;
-        } else {
-            atomicAdd(&A.counters[CNT_OVF], 1ull);
         }
     }
     const uint64_t li = mrg_wave_append(&A.counters[CNT_LONG], is_long);
@@ -237,11 +248,14 @@ __device__ __forceinline__ void wave_sync_lds() {
 }
 
 template <int CAP, bool IDX>
-__global__ __launch_bounds__(WG, CAP >= 4096 ? 2 : 4) void k_map(MapArgs A) {
+__global__ __launch_bounds__(WG, (CAP >= 4096 || (IDX && CAP >= 2048)) ? 2 : 4) void k_map(const MapArgs *__restrict__ Ap) {
+    // the arguments live in device memory (not the kernarg segment): fields are loaded where they
+    // are used instead of being held in SGPRs for the whole kernel
+    const MapArgs &A = *Ap;
     // per wave: staged window, segment masks, token queue (waves work on their own tiles)
     __shared__ __attribute__((aligned(16))) uint8_t s_tile[NWAVE][LDS_BYTES];
     __shared__ uint32_t s_mask[NWAVE][NSEG];
-    __shared__ uint16_t s_queue[NWAVE][QCAP];
+    __shared__ uint32_t s_queue[NWAVE][QCAP];
     __shared__ uint8_t s_lut[128];
     // workgroup: combine table + tail-region cursors
     __shared__ __attribute__((aligned(16))) unsigned long long s_k0[CAP];
@@ -276,23 +290,36 @@ __global__ __launch_bounds__(WG, CAP >= 4096 ? 2 : 4) void k_map(MapArgs A) {
     uint32_t my_tokens = 0;
     uint8_t *tile = s_tile[wv];
     uint32_t *mask = s_mask[wv];
-    uint16_t *queue = s_queue[wv];
+    uint32_t *queue = s_queue[wv];
     __syncthreads();
 
-    // prefetch of the first tile
+    // Staged window of a tile, as 16-byte vectors j relative to At - 16: j = 0 the byte block before
+    // the tile, j = 1..64 the tile's segments 0..63, j = 65..68 the halo.  Lane l holds vector 1 + l
+    // (its own segment: classified straight from registers) in p0; lanes 0..4 hold vectors 0 and
+    // 65..68 in p1.  Only vectors inside [v0, v1) are loaded (they never leave the allocation).
     const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
     uint64_t c = (uint64_t)blockIdx.x * NWAVE + wv;
+    uint32_t dcur = 0;
+    const uint32_t j0 = 1u + (uint32_t)lane;
+    const uint32_t j1 = lane == 0 ? 0u : 64u + (uint32_t)lane;
+    const bool has1 = lane < 5;
     TileInfo nx{};
     uint4 pf0 = {0, 0, 0, 0}, pf1 = {0, 0, 0, 0};
+    auto prefetch = [&](const TileInfo &t) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(A.in + (t.At - (uint64_t)BEHIND));
+        pf0 = uint4{0, 0, 0, 0};
+        pf1 = uint4{0, 0, 0, 0};
+        if (j0 >= t.v0 && j0 < t.v1) pf0 = src[j0];
+        if (has1 && j1 >= t.v0 && j1 < t.v1) pf1 = src[j1];
+    };
     if (c < A.n_chunks) {
-        nx = locate(A, c);
-        const uint4 *src = reinterpret_cast<const uint4 *>(A.in + (nx.At - (uint64_t)BEHIND));
-        if (nx.v0 + lane < nx.v1) pf0 = src[nx.v0 + lane];
-        if (nx.v0 + lane + 64 < nx.v1) pf1 = src[nx.v0 + lane + 64];
+        nx = locate(A, c, dcur);
+        prefetch(nx);
     }
 
     for (; c < A.n_chunks; c += stride) {
         const TileInfo T = nx;
+        const uint4 x0 = pf0, x1 = pf1;
         Window W;
         W.lds = tile;
         W.g = A.in;
@@ -301,28 +328,21 @@ __global__ __launch_bounds__(WG, CAP >= 4096 ? 2 : 4) void k_map(MapArgs A) {
         W.hi = T.whi;
 
         // this wave finished its previous tile (program order): the buffers are free
-        bool nonascii = false;
-        if (T.v0 + lane < T.v1) {
-            reinterpret_cast<uint4 *>(tile)[T.v0 + lane] = pf0;
-            nonascii |= ((pf0.x | pf0.y | pf0.z | pf0.w) & 0x80808080u) != 0u;
-        }
-        if (T.v0 + lane + 64 < T.v1) {
-            reinterpret_cast<uint4 *>(tile)[T.v0 + lane + 64] = pf1;
-            nonascii |= ((pf1.x | pf1.y | pf1.z | pf1.w) & 0x80808080u) != 0u;
-        }
+        const bool in0 = j0 >= T.v0 && j0 < T.v1, in1 = has1 && j1 >= T.v0 && j1 < T.v1;
+        if (in0) reinterpret_cast<uint4 *>(tile)[j0] = x0;
+        if (in1) reinterpret_cast<uint4 *>(tile)[j1] = x1;
+        const bool nonascii = (((x0.x | x0.y | x0.z | x0.w) | (x1.x | x1.y | x1.z | x1.w)) & 0x80808080u) != 0u;
         const bool generic = __any(nonascii);
         // next tile's loads fly while this one is processed
         if (c + stride < A.n_chunks) {
-            nx = locate(A, c + stride);
-            const uint4 *src = reinterpret_cast<const uint4 *>(A.in + (nx.At - (uint64_t)BEHIND));
-            if (nx.v0 + lane < nx.v1) pf0 = src[nx.v0 + lane];
-            if (nx.v0 + lane + 64 < nx.v1) pf1 = src[nx.v0 + lane + 64];
+            nx = locate(A, c + stride, dcur);
+            prefetch(nx);
         }
-        wave_sync_lds();
         const uint64_t At = T.At, t0 = T.t0, t1 = T.t1, doc_lo = T.doc_lo, doc_hi = T.doc_hi;
         const uint32_t docid = T.docid;
 
         if (generic) {
+            wave_sync_lds();
             // ================= generic path: per-lane codepoint walker =================
             const uint64_t sg0 = At + (uint64_t)lane * SEG;
             const uint64_t s0 = max(sg0, t0);
@@ -383,12 +403,15 @@ __global__ __launch_bounds__(WG, CAP >= 4096 ? 2 : 4) void k_map(MapArgs A) {
         }
 
         // ================= ASCII fast path =================
+        // positions relative to At fit 32 bits: the tile is 1 KiB, the staged window ends at hi_rel
+        const uint32_t hi_rel = (uint32_t)(W.hi - At);          // <= 1024 + HALO
+        const bool cut = W.hi < doc_hi;                          // staged window ends inside the document
+        const uint32_t t1_rel = (uint32_t)(t1 - At);
+        const uint32_t lo_rel = doc_lo > At ? (uint32_t)(doc_lo - At) : 0u;
         // 1. classify: segment g covers [At + 16 g, +16); bytes outside [doc_lo, W.hi) count as space.
-        //    Segments 0..63 are the tile (one per lane), segment 64 the first halo segment.
-        auto classify = [&](uint32_t g) -> uint32_t {
-            const uint64_t B = At + (uint64_t)g * SEG;
-            if (B >= W.hi) return 0xAAAAAAAAu;
-            const uint4 x = reinterpret_cast<const uint4 *>(tile)[1 + g];
+        auto classify = [&](const uint4 &x, uint32_t g) -> uint32_t {
+            const uint32_t B = g * SEG;
+            if (B >= hi_rel) return 0xAAAAAAAAu;
             uint32_t m = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -398,23 +421,28 @@ __global__ __launch_bounds__(WG, CAP >= 4096 ? 2 : 4) void k_map(MapArgs A) {
                 m |= (uint32_t)s_lut[(w >> 16) & 0x7Fu] << (8 * k + 4);
                 m |= (uint32_t)s_lut[w >> 24] << (8 * k + 6);
             }
-            const uint32_t lo_inv = doc_lo > B ? (uint32_t)min<uint64_t>(doc_lo - B, 16) : 0u;
-            const uint32_t hi_ok = (uint32_t)min<uint64_t>(W.hi - B, 16);
+            const uint32_t lo_inv = lo_rel > B ? min(lo_rel - B, 16u) : 0u;
+            const uint32_t hi_ok = min(hi_rel - B, 16u);
             const uint32_t vhi = hi_ok >= 16u ? 0xFFFFFFFFu : ((1u << (2u * hi_ok)) - 1u);
             const uint32_t vlo = lo_inv >= 16u ? 0xFFFFFFFFu : ((1u << (2u * lo_inv)) - 1u);
             const uint32_t valid = vhi & ~vlo;
             return (m & valid) | (0xAAAAAAAAu & ~valid);
         };
-        const uint32_t m = classify((uint32_t)lane);
+        const uint32_t m = classify(x0, (uint32_t)lane);
+        uint32_t m64 = lane == 1 ? classify(x1, 64u) : 0u;   // the first halo segment is lane 1's p1
+        m64 = __builtin_amdgcn_readlane(m64, 1);
         mask[lane] = m;
-        if (lane == 0) mask[64] = classify(64u);
-        // 2. token starts of this lane's segment (the previous byte's class: the neighbour lane's
-        //    mask, or the staged byte before the tile) -> the wave's queue (prefix sum)
+        if (lane == 0) mask[64] = m64;
+        uint32_t mn = __shfl_down(m, 1);
+        if (lane == 63) mn = m64;
+        // 2. token starts of this lane's segment: the previous byte's class from lane l-1's mask (or
+        //    the staged byte before the tile); each start becomes one queue entry that already knows
+        //    its raw length, key span and kind, so a consumer lane reads the key bytes directly
         uint32_t prev = __shfl_up(m >> 31, 1);
-        if (lane == 0) prev = At > doc_lo ? (s_lut[tile[BEHIND - 1] & 0x7Fu] >> 1) & 1u : 1u;
+        if (lane == 0) prev = At > doc_lo ? (s_lut[(x1.w >> 24) & 0x7Fu] >> 1) & 1u : 1u;
         const uint32_t IS = m & 0xAAAAAAAAu;
         uint32_t st = ~IS & ((IS << 2) | (prev << 1)) & 0xAAAAAAAAu;
-        if (At + (uint64_t)lane * SEG >= t1) st = 0;
+        if ((uint32_t)lane * SEG >= t1_rel) st = 0;
         const uint32_t cnt = __popc(st);
         uint32_t incl = cnt;
         for (int o = 1; o < 64; o <<= 1) {
@@ -422,91 +450,95 @@ __global__ __launch_bounds__(WG, CAP >= 4096 ? 2 : 4) void k_map(MapArgs A) {
             if (lane >= o) incl += u;
         }
         uint32_t pos = incl - cnt;
+        const uint64_t win = (uint64_t)m | ((uint64_t)mn << 32);
         while (st) {
             const uint32_t k = (uint32_t)__builtin_ctz(st) >> 1;
-            queue[pos++] = (uint16_t)(lane * SEG + k);
             st &= st - 1u;
+            const uint32_t s = (uint32_t)lane * SEG + k;
+            const uint64_t sr = (win & SBITS) >> (2u * k + 2u);
+            uint32_t n = 0, first = 0, L = 0, kind = QK_SLOW;
+            if (sr) {
+                n = ((uint32_t)__builtin_ctzll(sr) >> 1) + 1u;  // raw length
+                if (!(cut && s + n >= hi_rel)) {                // not ended by the staged edge
+                    const uint64_t w = (win >> (2u * k)) & WBITS & ((1ull << (2u * n)) - 1u);
+                    if (!w) {
+                        kind = QK_EMPTY;                        // no \w byte: no token
+                    } else {
+                        first = (uint32_t)__builtin_ctzll(w) >> 1;
+                        const uint32_t last = (63u - (uint32_t)__builtin_clzll(w)) >> 1;
+                        L = last - first + 1u;
+                        const uint64_t pat = (WBITS >> (64u - 2u * L)) << (2u * first);
+                        kind = w == pat ? QK_PLAIN : QK_INNER;
+                    }
+                }
+            }
+            queue[pos++] = s | (n << 10) | (first << 16) | (L << 21) | (kind << 27);
         }
-        const uint32_t total = __shfl(incl, 63);
+        const uint32_t total = (A.ablate & 4u) ? 0u : __shfl(incl, 63);
+        my_tokens += (A.ablate & 4u) ? cnt : 0u;
         wave_sync_lds();
 
-        // 3. tokens of the queue, one per lane per round (the queue and masks are read-only now)
+        // 3. tokens of the queue, one per lane per round (queue, masks and tile are read-only now)
         for (uint32_t base = 0; base < total; base += 64) {
             const uint32_t q = base + lane;
             bool have = false;
-            uint64_t tk0 = 0, tk1 = 0, tstart = 0;
-            uint32_t tlen = 0, traw = 0;
+            uint64_t tk0 = 0, tk1 = 0;
+            uint32_t tlen = 0, traw = 0, s = 0;
             if (q < total) {
-                const uint32_t s = queue[q];
-                const uint32_t g = s >> 4, i = s & 15u;
-                const uint64_t win = (uint64_t)mask[g] | ((uint64_t)mask[g + 1] << 32);
-                const uint64_t sr = (win & SBITS) >> (2u * i + 2u);
-                bool slow = true;
-                uint32_t n = 0;
-                if (sr) {
-                    n = ((uint32_t)__builtin_ctzll(sr) >> 1) + 1u;  // raw length
-                    slow = (At + s + n >= W.hi) && (W.hi < doc_hi);  // ended at the staged edge
-                }
-                if (!slow) {
-                    const uint64_t w = (win >> (2u * i)) & WBITS & ((1ull << (2u * n)) - 1u);
-                    if (w) {
-                        const uint32_t first = (uint32_t)__builtin_ctzll(w) >> 1;
-                        const uint32_t last = (63u - (uint32_t)__builtin_clzll(w)) >> 1;
-                        const uint32_t L = last - first + 1u;
-                        const uint64_t pat = (WBITS >> (64u - 2u * L)) << (2u * first);
-                        if (w != pat) {
-                            // deleted (X) bytes inside an ASCII token ("don't"): keep the \w bytes
-                            uint64_t a0 = 0, a1 = 0;
-                            uint32_t LL = 0;
-                            for (uint32_t j = first; j <= last; ++j) {
-                                if ((w >> (2u * j)) & 1u) {
-                                    mrg_key_append(a0, a1, LL, tile[BEHIND + s + j]);
-                                    ++LL;
-                                }
-                            }
-                            have = true;
-                            tlen = LL;
-                            tstart = At + s;
-                            traw = n;
-                            tk0 = a0;
-                            tk1 = a1;
-                        } else {
-                            have = true;
-                            tlen = L;
-                            tstart = At + s;
-                            traw = n;
-                            if (L <= 16u) {
-                                const uint32_t off = BEHIND + s + first;
-                                const uint64_t *q64 = reinterpret_cast<const uint64_t *>(tile + (off & ~7u));
-                                const uint64_t x0 = q64[0], x1 = q64[1], x2 = q64[2];
-                                const uint32_t sh = (off & 7u) * 8u;
-                                uint64_t lo = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
-                                uint64_t hi = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
-                                if (L < 8u) { lo &= (1ull << (8u * L)) - 1u; hi = 0; }
-                                else if (L < 16u) hi &= (1ull << (8u * (L - 8u))) - 1u;
-                                tk0 = __builtin_bswap64(lo);
-                                tk1 = __builtin_bswap64(hi);
-                            }
+                const uint32_t e = queue[q];
+                s = e & 1023u;
+                const uint32_t n = (e >> 10) & 63u, first = (e >> 16) & 31u, L = (e >> 21) & 63u, kind = e >> 27;
+                if (kind == QK_PLAIN) {
+                    have = true;
+                    tlen = L;
+                    traw = n;
+                    if (L <= 16u) {
+                        const uint32_t off = BEHIND + s + first;
+                        const uint64_t *q64 = reinterpret_cast<const uint64_t *>(tile + (off & ~7u));
+                        const uint64_t y0 = q64[0], y1 = q64[1], y2 = q64[2];
+                        const uint32_t sh = (off & 7u) * 8u;
+                        uint64_t lo = sh ? (y0 >> sh) | (y1 << (64u - sh)) : y0;
+                        uint64_t hi = sh ? (y1 >> sh) | (y2 << (64u - sh)) : y1;
+                        if (L < 8u) { lo &= (1ull << (8u * L)) - 1u; hi = 0; }
+                        else if (L < 16u) hi &= (1ull << (8u * (L - 8u))) - 1u;
+                        tk0 = __builtin_bswap64(lo);
+                        tk1 = __builtin_bswap64(hi);
+                    }
+                } else if (kind == QK_INNER) {
+                    // deleted (X) bytes inside an ASCII token ("don't"): keep the \w bytes
+                    const uint32_t g = s >> 4, i = s & 15u;
+                    const uint64_t wn = (uint64_t)mask[g] | ((uint64_t)mask[g + 1] << 32);
+                    const uint64_t w = (wn >> (2u * i)) & WBITS & ((1ull << (2u * n)) - 1u);
+                    uint64_t a0 = 0, a1 = 0;
+                    uint32_t LL = 0;
+                    for (uint32_t j = first; j < first + L; ++j) {
+                        if ((w >> (2u * j)) & 1u) {
+                            mrg_key_append(a0, a1, LL, tile[BEHIND + s + j]);
+                            ++LL;
                         }
                     }
-                }
-                if (slow) {
-                    uint64_t a0, a1, e;
-                    uint32_t L;
-                    if (walk_token(W, At + s, doc_hi, A.counters, a0, a1, L, e) && L > 0) {
+                    have = true;
+                    tlen = LL;
+                    traw = n;
+                    tk0 = a0;
+                    tk1 = a1;
+                } else if (kind == QK_SLOW) {
+                    uint64_t a0, a1, e2;
+                    uint32_t L2;
+                    if (walk_token(W, At + s, doc_hi, A.counters, a0, a1, L2, e2) && L2 > 0) {
                         have = true;
-                        tk0 = a0; tk1 = a1; tlen = L; tstart = At + s; traw = (uint32_t)(e - (At + s));
+                        tk0 = a0; tk1 = a1; tlen = L2; traw = (uint32_t)(e2 - (At + s));
                     }
                 }
             }
             my_tokens += have ? 1u : 0u;
-            emit_round(A, table, s_bcount, s_bcap, s_bbase, have, tk0, tk1, tlen, tstart, traw, docid);
+            emit_round(A, table, s_bcount, s_bcap, s_bbase, have, tk0, tk1, tlen, At + s, traw, docid);
         }
     }
 
     // ---- flush the LDS table into this workgroup's region, sorted by bucket
     __syncthreads();
-    uint16_t *s_rank = &s_queue[0][0];
+    uint16_t *s_rank = reinterpret_cast<uint16_t *>(&s_queue[0][0]);
     uint32_t *bcount = A.bcount + (uint64_t)blockIdx.x * MRG_NBUCKET;
     uint32_t my_tail = 0;
     for (int b = tid; b < MRG_NBUCKET; b += WG) {
@@ -610,12 +642,13 @@ __global__ void k_long_gather(const uint8_t *in, const uint64_t *lstart, const u
 }  // namespace
 
 template <int CAP, bool IDX>
-static void launch_map_t(const MapArgs &a, int grid, hipStream_t s) {
+static void launch_map_t(const MapArgs *a, int grid, hipStream_t s) {
     hipLaunchKernelGGL((k_map<CAP, IDX>), dim3(grid), dim3(WG), 0, s, a);
 }
 
-void mrg_launch_map(const MapArgs &a, int app, int grid, int lds_cap, hipStream_t s) {
+void mrg_launch_map(const MapArgs &h, MapArgs *a, int app, int grid, int lds_cap, hipStream_t s) {
     const bool idx = app == 1;
+    (void)hipMemcpyAsync(a, &h, sizeof(MapArgs), hipMemcpyHostToDevice, s);
     if (lds_cap >= 4096) { if (idx) launch_map_t<4096, true>(a, grid, s); else launch_map_t<4096, false>(a, grid, s); }
     else if (lds_cap >= 2048) { if (idx) launch_map_t<2048, true>(a, grid, s); else launch_map_t<2048, false>(a, grid, s); }
     else { if (idx) launch_map_t<1024, true>(a, grid, s); else launch_map_t<1024, false>(a, grid, s); }

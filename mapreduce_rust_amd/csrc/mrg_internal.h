@@ -24,7 +24,7 @@ enum {
     CNT_TOKENS = 2,   // tokens
     CNT_ERRPOS = 3,   // first invalid UTF-8 byte (atomicMin), ~0 if none
     CNT_KEYS = 4,     // distinct keys appended to the KeySet
-    CNT_OVF = 5,      // tail records beyond their region's capacity (pool too small: rerun)
+    CNT_OVF = 5,      // tail records that found neither region nor overflow-list room (rerun)
     CNT_OVF2 = 6,     // keys that did not fit their bucket's LDS table (exact overflow path)
     CNT_N = 8
 };
@@ -49,7 +49,12 @@ struct MapArgs {
     uint64_t *pool;
     const uint64_t *rbase;       // [NBUCKET] first record of bucket b's regions
     const uint32_t *bcap;        // [NBUCKET] records per (bucket, workgroup) region
-    uint32_t *bcount;            // [grid * NBUCKET] records appended (may exceed bcap: rerun)
+    uint32_t *bcount;            // [grid * NBUCKET] records appended (may exceed bcap)
+    // records beyond their region's capacity: bucket b's overflow list, records
+    // [b * ocap, b * ocap + min(onext[b], ocap)) of `ovf` (a full list forces a rerun)
+    uint64_t *ovf;
+    uint32_t *onext;             // [NBUCKET]
+    uint32_t ocap;
     // LDS-table flush: workgroup g writes its entries to [g * CAP, ...) sorted by bucket;
     // foff[g * (NBUCKET + 1) + b] = start of bucket b in that region
     uint64_t *fk0, *fk1;
@@ -60,6 +65,9 @@ struct MapArgs {
     uint64_t lcap;
     unsigned long long *counters;
     uint32_t hash_bits;          // 0 = full; else truncate internal hashes (collision test knob)
+    uint32_t ablate;             // perf diagnostics only (env MRG_ABLATE; results are WRONG when set):
+                                 // 1 = no tail-record stores, 2 = no LDS-table probe (all tokens
+                                 // become tail records), 4 = no per-token work after the queue
 };
 
 // A set of keys with counts (SoA).  len > 16 keys have their bytes at heap[hoff .. hoff+len).
@@ -93,7 +101,8 @@ struct LongItems {
 };
 
 // ---- k_map.hip
-void mrg_launch_map(const MapArgs &a, int app, int grid, int lds_cap, hipStream_t s);
+// `dev_args` is device memory for one MapArgs (the kernel reads its arguments from there)
+void mrg_launch_map(const MapArgs &a, MapArgs *dev_args, int app, int grid, int lds_cap, hipStream_t s);
 uint64_t mrg_map_tiles(uint64_t doc_lo, uint64_t doc_hi);  // 1 KiB wave tiles of a document (16-B grid)
 int mrg_map_cap(int lds_cap);  // LDS-table entries per map workgroup actually used for lds_cap
 int mrg_map_max_grid(int app, int lds_cap, int device);
@@ -108,6 +117,9 @@ struct BucketArgs {
     const uint64_t *pool;
     const uint64_t *rbase;
     const uint32_t *bcap, *bcount;
+    const uint64_t *movf;        // map-side overflow lists (MapArgs::ovf / onext / ocap)
+    const uint32_t *monext;
+    uint32_t mocap;
     const uint64_t *fk0, *fk1;
     const uint32_t *fcnt, *fdoc, *foff;
     uint32_t nreg, regcap;       // map workgroups (flush regions) and entries per region

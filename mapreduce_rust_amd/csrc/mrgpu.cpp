@@ -142,6 +142,7 @@ struct mrg_ctx {
     int map_grid = 0;
     uint64_t long_hint = 0, ovf_hint = 0;
     std::vector<double> bcap_rate;  // tail records per (bucket, map workgroup) per input byte of the workgroup
+    uint64_t ocap_hint = 0;         // records per bucket overflow list
     // job
     bool job = false;
     int app = 0;
@@ -307,12 +308,15 @@ void aggregate(mrg_ctx *c, const ShortSrc &src, LongItems li) {
 struct MapBufs {
     uint64_t *pool = nullptr, *rbase = nullptr;
     uint32_t *bcap = nullptr, *bcount = nullptr;
+    MapArgs *dargs = nullptr;
+    uint64_t *ovf = nullptr;
+    uint32_t *onext = nullptr;
     uint64_t *fk0 = nullptr, *fk1 = nullptr;
     uint32_t *fcnt = nullptr, *fdoc = nullptr, *foff = nullptr;
     uint64_t *lstart = nullptr;
     uint32_t *llen = nullptr, *ldoc = nullptr;
     void release(Pool &p) {
-        p.put(pool); p.put(rbase); p.put(bcap); p.put(bcount);
+        p.put(pool); p.put(rbase); p.put(bcap); p.put(bcount); p.put(dargs); p.put(ovf); p.put(onext);
         p.put(fk0); p.put(fk1); p.put(fcnt); p.put(fdoc); p.put(foff);
         p.put(lstart); p.put(llen); p.put(ldoc);
         *this = MapBufs{};
@@ -330,6 +334,7 @@ void bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         keys_reserve(c, (uint64_t)MRG_NBUCKET * MRG_BA_CAP + ocap + li.n + 1);
         BucketArgs B{};
         B.pool = A.pool; B.rbase = A.rbase; B.bcap = A.bcap; B.bcount = A.bcount;
+        B.movf = A.ovf; B.monext = A.onext; B.mocap = A.ocap;
         B.fk0 = A.fk0; B.fk1 = A.fk1; B.fcnt = A.fcnt; B.fdoc = A.fdoc; B.foff = A.foff;
         B.nreg = nreg; B.regcap = regcap;
         B.ok0 = pget<uint64_t>(p, ocap); B.ok1 = pget<uint64_t>(p, ocap);
@@ -422,6 +427,9 @@ void job_map(mrg_ctx *c) {
         if (c->bcap_rate.size() == MRG_NBUCKET) est = std::max(est, c->bcap_rate[b] * per_wg);
         bcap[b] = (uint64_t)(est * 1.25) + 32;
     }
+    // per-bucket overflow lists absorb the run-to-run variation of the regions' demand (the LDS
+    // table's contents depend on wave timing), so a launch is repeated only when one fills up
+    uint64_t ocap = std::max<uint64_t>(c->ocap_hint, std::max<uint64_t>(1024, total / 20 / MRG_NBUCKET / 16));
     MapArgs A{};
     MapBufs M;
     uint32_t launches = 0;
@@ -438,6 +446,11 @@ void job_map(mrg_ctx *c) {
         M.rbase = pget<uint64_t>(p, MRG_NBUCKET);
         M.bcap = pget<uint32_t>(p, MRG_NBUCKET);
         M.bcount = pget<uint32_t>(p, (uint64_t)grid * MRG_NBUCKET);
+        M.dargs = pget<MapArgs>(p, 1);
+        if (ocap > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
+        M.ovf = pget<uint64_t>(p, (uint64_t)MRG_NBUCKET * ocap * RW);
+        M.onext = pget<uint32_t>(p, MRG_NBUCKET);
+        HIPCHK(hipMemsetAsync(M.onext, 0, 4ull * MRG_NBUCKET, s));
         HIPCHK(hipMemcpyAsync(M.rbase, rbase.data(), 8ull * MRG_NBUCKET, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(M.bcap, bcap32.data(), 4ull * MRG_NBUCKET, hipMemcpyHostToDevice, s));
         A.in = c->d_in;
@@ -456,14 +469,16 @@ void job_map(mrg_ctx *c) {
         M.llen = pget<uint32_t>(p, lcap);
         M.ldoc = pget<uint32_t>(p, lcap);
         A.pool = M.pool; A.rbase = M.rbase; A.bcap = M.bcap; A.bcount = M.bcount;
+        A.ovf = M.ovf; A.onext = M.onext; A.ocap = (uint32_t)ocap;
         A.fk0 = M.fk0; A.fk1 = M.fk1; A.fcnt = M.fcnt; A.fdoc = M.fdoc; A.foff = M.foff;
         A.lstart = M.lstart; A.llen = M.llen; A.ldoc = M.ldoc; A.lcap = lcap;
         A.counters = c->d_cnt;
         A.hash_bits = hash_bits(c);
+        A.ablate = getenv("MRG_ABLATE") ? (uint32_t)atoi(getenv("MRG_ABLATE")) : 0u;
         HIPCHK(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long) * CNT_N, s));
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_ERRPOS], 0xFF, sizeof(unsigned long long), s));
         ev_rec(c, 0);
-        mrg_launch_map(A, c->app, grid, c->lds_cap, s);  // also with no tiles: writes empty flush regions
+        mrg_launch_map(A, M.dargs, c->app, grid, c->lds_cap, s);  // also with no tiles: writes empty flush regions
         ev_rec(c, 1);
         HIPCHK(hipGetLastError());
         ++launches;
@@ -479,9 +494,10 @@ void job_map(mrg_ctx *c) {
             for (int b = 0; b < MRG_NBUCKET; ++b) {
                 uint64_t mx = 0;
                 for (int g = 0; g < grid; ++g) mx = std::max<uint64_t>(mx, cnt[(uint64_t)g * MRG_NBUCKET + b]);
-                bcap[b] = std::max<uint64_t>(bcap[b], mx + mx / 8 + 32);
+                bcap[b] = std::max<uint64_t>(bcap[b], mx + mx / 4 + 64);
                 c->bcap_rate[b] = (double)mx / per_wg;
             }
+            ocap = c->ocap_hint = 2 * ocap;
         }
         if (nl > lcap) lcap = c->long_hint = nl + nl / 8 + 1024;
         if (getenv("MRG_DEBUG"))
