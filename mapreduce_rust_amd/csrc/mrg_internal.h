@@ -4,7 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
-#define MRG_MAP_WG 512          // threads per map workgroup (8 waves sharing one LDS table)
+#define MRG_MAP_WAVES 16        // waves per map workgroup (one workgroup per CU, one shared LDS table)
+#define MRG_MAP_WG (64 * MRG_MAP_WAVES)
 #define MRG_MAP_SEG 16          // input bytes per lane per tile
 #define MRG_MAP_TILE (64 * MRG_MAP_SEG)  // 1 KiB tile per WAVE iteration (waves never synchronise)
 #define MRG_MAP_HALO 64         // bytes after the tile staged in LDS (tokens crossing the tile end)
@@ -63,6 +64,10 @@ struct MapArgs {
     uint64_t *lstart;
     uint32_t *llen, *ldoc;
     uint64_t lcap;
+    // non-ASCII tiles, recorded by the main loop and processed after it: wave w's k-th tile is bit
+    // k % 64 of gbits[w * kwords + k / 64]
+    uint64_t *gbits;
+    uint32_t kwords;
     unsigned long long *counters;
     uint32_t hash_bits;          // 0 = full; else truncate internal hashes (collision test knob)
     uint32_t ablate;             // perf diagnostics only (env MRG_ABLATE; results are WRONG when set):

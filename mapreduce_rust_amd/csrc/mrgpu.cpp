@@ -138,7 +138,7 @@ struct mrg_ctx {
     unsigned long long *h_cnt = nullptr;  // pinned mirror
     bool timing = false;
     hipEvent_t ev[8] = {};
-    int lds_cap = 2048;
+    int lds_cap = 4096;
     int map_grid = 0;
     uint64_t long_hint = 0, ovf_hint = 0;
     std::vector<double> bcap_rate;  // tail records per (bucket, map workgroup) per input byte of the workgroup
@@ -315,10 +315,11 @@ struct MapBufs {
     uint32_t *fcnt = nullptr, *fdoc = nullptr, *foff = nullptr;
     uint64_t *lstart = nullptr;
     uint32_t *llen = nullptr, *ldoc = nullptr;
+    uint64_t *gbits = nullptr;
     void release(Pool &p) {
         p.put(pool); p.put(rbase); p.put(bcap); p.put(bcount); p.put(dargs); p.put(ovf); p.put(onext);
         p.put(fk0); p.put(fk1); p.put(fcnt); p.put(fdoc); p.put(foff);
-        p.put(lstart); p.put(llen); p.put(ldoc);
+        p.put(lstart); p.put(llen); p.put(ldoc); p.put(gbits);
         *this = MapBufs{};
     }
 };
@@ -472,6 +473,13 @@ void job_map(mrg_ctx *c) {
         A.ovf = M.ovf; A.onext = M.onext; A.ocap = (uint32_t)ocap;
         A.fk0 = M.fk0; A.fk1 = M.fk1; A.fcnt = M.fcnt; A.fdoc = M.fdoc; A.foff = M.foff;
         A.lstart = M.lstart; A.llen = M.llen; A.ldoc = M.ldoc; A.lcap = lcap;
+        {  // one bit per tile of each wave (written whole by the kernel: no clearing needed)
+            const uint64_t waves = (uint64_t)grid * MRG_MAP_WAVES;
+            const uint64_t per_wave = (n_chunks + waves - 1) / waves;
+            A.kwords = (uint32_t)std::max<uint64_t>(1, (per_wave + 63) / 64);
+            M.gbits = pget<uint64_t>(p, waves * A.kwords);
+            A.gbits = M.gbits;
+        }
         A.counters = c->d_cnt;
         A.hash_bits = hash_bits(c);
         A.ablate = getenv("MRG_ABLATE") ? (uint32_t)atoi(getenv("MRG_ABLATE")) : 0u;
