@@ -42,6 +42,8 @@ constexpr int HALO = MRG_MAP_HALO;
 constexpr int BEHIND = MRG_MAP_BEHIND;
 constexpr int WIN = BEHIND + TILE + HALO + 48;  // staged window + slack for 5-dword key reads
 constexpr int QCAP = TILE / 2;                   // a start needs a space before it: <= 512 per tile
+constexpr int NSUB = MRG_MAP_NSUB;               // 1 KiB tiles per block
+constexpr int BLK = NSUB * TILE;                 // bytes per wave iteration
 static_assert(TILE == 64 * SEG, "one segment per lane");
 static_assert(WIN % 16 == 0, "16-byte window rows");
 
@@ -52,6 +54,9 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {  // lane l <- l
 __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {  // lane l <- lane l-1 (lane 0 <- 0)
     return __builtin_amdgcn_update_dpp(0u, v, 0x138, 0xF, 0xF, false);  // wave_shr:1
 }
+// readlane / readfirstlane return int: wrap them so shifts and widening stay unsigned
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ uint32_t first_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);  // row_shr:1
     v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);  // row_shr:2
@@ -67,23 +72,78 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Global memory through address-space-1 pointers.  The kernel reads its pointers from a MapArgs in
+// device memory, so without the cast every access would be a FLAT instruction -- and a pending FLAT
+// op makes each LDS wait (lgkmcnt) also wait for every outstanding global load and store.
+#define GAS __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ GAS T *gp(T *p) {
+    return (GAS T *)p;
+}
+// Read-only job tables (document offsets, tile bases) through the constant address space: uniform
+// loads become scalar loads (lgkmcnt), so the tile lookup never waits on the vector-memory counter
+// -- which would also wait for the input prefetch issued just before it.
+#define CAS __attribute__((address_space(4)))
+template <class T>
+__device__ __forceinline__ const CAS T *cp(const T *p) {
+    return (const CAS T *)p;
+}
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+template <class T>
+__device__ __forceinline__ T g_add(T *p, T v) {
+    return __hip_atomic_fetch_add(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// wave-aggregated append on a global counter (one atomic per wave): this lane's slot if pred
+__device__ __forceinline__ uint64_t g_wave_append(unsigned long long *counter, bool pred) {
+    const uint64_t mask = __ballot(pred);
+    if (!mask) return 0;
+    const int leader = __ffsll((long long)mask) - 1;
+    unsigned long long base = 0;
+    if ((int)__lane_id() == leader) base = g_add(counter, (unsigned long long)__popcll(mask));
+    base = __shfl(base, leader);
+    return base + (uint64_t)__popcll(mask & mrg_lanemask_lt());
+}
+
 struct TileInfo {
     uint64_t At, t0, t1, doc_lo, doc_hi, wlo, whi;
     uint32_t docid, v0, v1;
 };
 
-// Tile c of the job.  A wave visits its tiles in increasing order, so the document index only moves
-// forward from the previous tile's (usually not at all).
-__device__ __forceinline__ TileInfo locate(const MapArgs &A, uint64_t c, uint32_t &d) {
-    while (A.chunk_base[d + 1] <= c) ++d;  // chunk_base[d] <= c < chunk_base[d+1]
+struct BlkInfo {
+    uint64_t Ab, doc_lo, doc_hi;
+    uint32_t docid, v0, v1;
+};
+
+// Block c of the job (BLK bytes on the document's 16-byte grid).  A wave visits its blocks in increasing
+// order, so the document index only moves forward (usually not at all).  v0/v1: the loadable
+// 16-byte vectors relative to Ab - 16 (the byte block before, the block, its 64-byte halo).
+__device__ __forceinline__ BlkInfo locate_blk(const MapArgs &A, uint64_t c, uint32_t &d) {
+    const CAS uint64_t *cb = cp(A.chunk_base), *doff = cp(A.doc_off);
+    while (cb[d + 1] <= c) ++d;  // chunk_base[d] <= c < chunk_base[d+1]
+    BlkInfo b;
+    b.doc_lo = doff[d];
+    b.doc_hi = doff[d + 1];
+    b.Ab = (b.doc_lo & ~15ull) + (c - cb[d]) * (uint64_t)BLK;
+    b.docid = A.doc_id ? cp(A.doc_id)[d] : d;
+    const uint64_t vbase = b.Ab - (uint64_t)BEHIND;  // may wrap below 0: only differences are used
+    const uint64_t wlo = max(b.doc_lo, b.Ab >= (uint64_t)BEHIND ? b.Ab - BEHIND : 0ull);
+    const uint64_t whi = min(b.Ab + (uint64_t)(BLK + HALO), b.doc_hi);
+    b.v0 = (uint32_t)(((wlo & ~15ull) - vbase) >> 4);
+    b.v1 = (uint32_t)((((whi + 15u) & ~15ull) - vbase) >> 4);
+    return b;
+}
+
+// 1 KiB tile j of a block, with its staged window [At - 16, At + 1024 + 64) clipped to the document.
+__device__ __forceinline__ TileInfo sub_tile(const BlkInfo &b, uint32_t j) {
     TileInfo t;
-    t.doc_lo = A.doc_off[d];
-    t.doc_hi = A.doc_off[d + 1];
-    t.At = (t.doc_lo & ~15ull) + (c - A.chunk_base[d]) * (uint64_t)TILE;  // aligned tile base
+    t.At = b.Ab + (uint64_t)j * TILE;
+    t.doc_lo = b.doc_lo;
+    t.doc_hi = b.doc_hi;
+    t.docid = b.docid;
     t.t0 = max(t.At, t.doc_lo);
     t.t1 = min(t.At + (uint64_t)TILE, t.doc_hi);
-    t.docid = A.doc_id ? A.doc_id[d] : d;
-    const uint64_t wbase = t.At - (uint64_t)BEHIND;  // may wrap below 0: only differences are used
+    const uint64_t wbase = t.At - (uint64_t)BEHIND;
     t.wlo = max(t.doc_lo, t.At >= (uint64_t)BEHIND ? t.At - BEHIND : 0ull);
     t.whi = min(t.t1 + (uint64_t)HALO, t.doc_hi);
     t.v0 = (uint32_t)(((t.wlo & ~15ull) - wbase) >> 4);
@@ -92,7 +152,8 @@ __device__ __forceinline__ TileInfo locate(const MapArgs &A, uint64_t c, uint32_
 }
 
 __device__ __forceinline__ void report_error(unsigned long long *counters, uint64_t pos) {
-    atomicMin(&counters[CNT_ERRPOS], (unsigned long long)pos);
+    __hip_atomic_fetch_min(gp(&counters[CNT_ERRPOS]), (unsigned long long)pos, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ uint32_t key_hash(uint64_t k0, uint64_t k1, uint32_t d, uint32_t hash_bits) {
@@ -226,13 +287,13 @@ __device__ __forceinline__ void emit(const MapArgs &A, LdsTable<CAP, IDX> &table
     if (tail && !(A.ablate & 1u)) {
         const uint32_t b = bucket_of(h);
         const uint32_t slot = atomicAdd(&bcount[b], 1u);
-        uint64_t *dst = nullptr;
+        GAS uint64_t *dst = nullptr;
         if (slot < bcap[b]) {
-            dst = A.pool + (bbase[b] + slot) * (IDX ? 3u : 2u);
+            dst = gp(A.pool) + (bbase[b] + slot) * (IDX ? 3u : 2u);
         } else {  // region full (rare): the bucket's shared overflow list
-            const uint32_t j = atomicAdd(&A.onext[b], 1u);
-            if (j < A.ocap) dst = A.ovf + ((uint64_t)b * A.ocap + j) * (IDX ? 3u : 2u);
-            else atomicAdd(&A.counters[CNT_OVF], 1ull);
+            const uint32_t j = g_add(&A.onext[b], 1u);
+            if (j < A.ocap) dst = gp(A.ovf) + ((uint64_t)b * A.ocap + j) * (IDX ? 3u : 2u);
+            else g_add(&A.counters[CNT_OVF], 1ull);
         }
         if (dst) {
             if (IDX) {
@@ -240,16 +301,16 @@ __device__ __forceinline__ void emit(const MapArgs &A, LdsTable<CAP, IDX> &table
                 dst[1] = tk1;
                 dst[2] = docid;
             } else {
-                *reinterpret_cast<KeyPair *>(dst) = KeyPair{tk0, tk1};  // one 16-byte store
+                *reinterpret_cast<GAS u64x2 *>(dst) = u64x2{tk0, tk1};  // one 16-byte store
             }
         }
     }
     if (__any(is_long)) {
-        const uint64_t li = mrg_wave_append(&A.counters[CNT_LONG], is_long);
+        const uint64_t li = g_wave_append(&A.counters[CNT_LONG], is_long);
         if (is_long && li < A.lcap) {
-            A.lstart[li] = tstart;
-            A.llen[li] = traw;
-            A.ldoc[li] = docid;
+            gp(A.lstart)[li] = tstart;
+            gp(A.llen)[li] = traw;
+            gp(A.ldoc)[li] = docid;
         }
     }
 }
@@ -267,7 +328,8 @@ __device__ __forceinline__ uint32_t generic_tile(const MapArgs &A, LdsTable<CAP,
     const int lane = (int)__lane_id();
     const uint64_t wbase = At - (uint64_t)BEHIND;
     auto rd = [&](uint64_t a) -> uint32_t {
-        return (a >= wlo && a < whi) ? (uint32_t)win[a - wbase] : (uint32_t)A.in[a];
+        if (a >= wlo && a < whi) return (uint32_t)win[a - wbase];
+        return (uint32_t)gp(A.in)[a];
     };
     uint32_t my_tokens = 0;
         // ================= generic path: per-lane codepoint walker =================
@@ -363,9 +425,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     for (int i = tid; i < CAP / 8; i += WG) s_tag[i] = 0;
     for (int b = tid; b < MRG_NBUCKET; b += WG) {
         s_bcount[b] = 0;
-        const uint32_t cap = A.bcap[b];
+        const uint32_t cap = gp(A.bcap)[b];
         s_bcap[b] = cap;
-        s_bbase[b] = A.rbase[b] + (uint64_t)blockIdx.x * cap;
+        s_bbase[b] = gp(A.rbase)[b] + (uint64_t)blockIdx.x * cap;
     }
     if (tid < 128) {
         const uint32_t c = mrg_uclass((uint32_t)tid);
@@ -386,79 +448,57 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     uint16_t *queue = s_q[wv];
     __syncthreads();
 
-    // Staged window of a tile, as 16-byte vectors j relative to At - 16: j = 0 the byte block before
-    // the tile, j = 1..64 the tile's segments 0..63, j = 65..68 the halo.  Lane l holds vector 1 + l
-    // (its own segment: classified straight from registers) in p0; lanes 0..4 hold vectors 0 and
-    // 65..68 in p1.  Only vectors inside [v0, v1) are loaded (they never leave the allocation).
-    const uint64_t stride = (uint64_t)gridDim.x * NW;
-    const uint64_t n_chunks = A.n_chunks;
-    uint64_t c = (uint64_t)blockIdx.x * NW + wv;
-    uint32_t dcur = 0;
+    // Tile staging for the walkers (deferred non-ASCII tiles): 16-byte vectors j relative to At - 16:
+    // j = 0 the bytes before the tile, j = 1..64 the tile's segments, j = 65..68 the halo.  Lane l
+    // loads vector 1 + l; lanes 0..4 also vectors 0 and 65..68.  Only vectors in [v0, v1) are read.
     const uint32_t j0 = 1u + (uint32_t)lane;
     const uint32_t j1 = lane == 0 ? 0u : 64u + (uint32_t)lane;
     const bool has1 = lane < 5;
     auto load = [&](const TileInfo &t, uint4 &p0, uint4 &p1) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(A.in + (t.At - (uint64_t)BEHIND));
-        p0 = uint4{0, 0, 0, 0};
-        p1 = uint4{0, 0, 0, 0};
-        if (j0 >= t.v0 && j0 < t.v1) p0 = src[j0];
-        if (has1 && j1 >= t.v0 && j1 < t.v1) p1 = src[j1];
+        const GAS u32x4 *src = reinterpret_cast<const GAS u32x4 *>(gp(A.in) + (t.At - (uint64_t)BEHIND));
+        u32x4 v0 = {0, 0, 0, 0}, v1 = {0, 0, 0, 0};
+        if (j0 >= t.v0 && j0 < t.v1) v0 = src[j0];
+        if (has1 && j1 >= t.v0 && j1 < t.v1) v1 = src[j1];
+        p0 = uint4{v0.x, v0.y, v0.z, v0.w};
+        p1 = uint4{v1.x, v1.y, v1.z, v1.w};
     };
-    // two tiles in flight while one is processed
-    TileInfo n1{}, n2{};
-    uint4 a0{0, 0, 0, 0}, a1{0, 0, 0, 0}, b0{0, 0, 0, 0}, b1{0, 0, 0, 0};
-    if (c < n_chunks) {
-        n1 = locate(A, c, dcur);
-        load(n1, a0, a1);
-    }
-    if (c + stride < n_chunks) {
-        n2 = locate(A, c + stride, dcur);
-        load(n2, b0, b1);
-    }
+    // A 2 KiB block in registers: lane l holds bytes [Ab + 1024 j + 16 l, +16) in v[j]; e = the 16
+    // bytes before the block on lane 0, the 64-byte halo after it on lanes 1..4.  The three loads are
+    // unconditional (no branch for the scheduler to wait inside): an out-of-range lane reads a
+    // clamped in-range vector instead.  Its bytes are never used as text: classify() turns every
+    // byte outside the document into White_Space, and keys only come from bytes inside it.
+    struct Blk {
+        uint4 v0, v1, e;
+    };
+    auto load_blk = [&](const BlkInfo &b, Blk &X) {
+        const GAS uint8_t *src = gp(A.in) + (b.Ab - (uint64_t)BEHIND);
+        auto ld = [&](uint32_t idx) -> uint4 {
+            const u32x4 t = *reinterpret_cast<const GAS u32x4 *>(src + 16u * min(max(idx, b.v0), b.v1 - 1u));
+            return uint4{t.x, t.y, t.z, t.w};
+        };
+        X.v0 = ld(1u + (uint32_t)lane);
+        X.v1 = ld(65u + (uint32_t)lane);
+        X.e = ld(lane == 0 ? 0u : 128u + (uint32_t)lane);
+    };
 
-    // non-ASCII tiles: bit k of this wave's bitmap = its k-th tile (one 64-bit word per 64 tiles)
-    uint64_t *gbits = A.gbits + (uint64_t)(blockIdx.x * NW + wv) * A.kwords;
+    // non-ASCII tiles: bit k of this wave's bitmap = its k-th 1 KiB tile (one 64-bit word per 64)
+    GAS uint64_t *gbits = gp(A.gbits) + (uint64_t)(blockIdx.x * NW + wv) * A.kwords;
     uint64_t gword = 0;
-    uint32_t kt = 0;  // this wave's tile counter
-    for (; c < n_chunks; c += stride, ++kt) {
+    uint32_t kt = 0;  // this wave's tile counter (NSUB per block)
+
+    // one block: masks of its 1 KiB tiles up front, then tile by tile through the
+    // wave's LDS window
+    auto process_blk = [&](const BlkInfo &I, const Blk &X) {
         if (kt && (kt & 63u) == 0) {
             if (lane == 0) gbits[(kt >> 6) - 1] = gword;
             gword = 0;
         }
-        const TileInfo T = n1;
-        const uint4 x0 = a0, x1 = a1;
-        n1 = n2;
-        a0 = b0;
-        a1 = b1;
-        if (c + 2 * stride < n_chunks) {
-            n2 = locate(A, c + 2 * stride, dcur);
-            load(n2, b0, b1);
-        }
-        const uint64_t At = T.At, t1 = T.t1, doc_lo = T.doc_lo, doc_hi = T.doc_hi;
-        const uint64_t wlo = T.wlo, whi = T.whi, wbase = At - (uint64_t)BEHIND;
-        const uint32_t docid = T.docid;
-
-        // this wave finished its previous tile (program order): the buffers are free
-        wave_sync_lds();
-        const bool in0 = j0 >= T.v0 && j0 < T.v1, in1 = has1 && j1 >= T.v0 && j1 < T.v1;
-        if (in0) reinterpret_cast<uint4 *>(win)[j0] = x0;
-        if (in1) reinterpret_cast<uint4 *>(win)[j1] = x1;
-        const bool nonascii = (((x0.x | x0.y | x0.z | x0.w) | (x1.x | x1.y | x1.z | x1.w)) & 0x80808080u) != 0u;
-        const bool generic = __any(nonascii);
-        wave_sync_lds();
-
-        if (generic) {  // recorded; processed after the main loop
-            gword |= 1ull << (kt & 63u);
-        } else {
-
-        // ================= ASCII fast path =================
-        // positions relative to At fit 32 bits: the tile is 1 KiB, the staged window ends at hi_rel
-        const uint32_t hi_rel = (uint32_t)(whi - At);            // <= 1024 + HALO
-        const bool cut = whi < doc_hi;                           // staged window ends inside the document
-        const uint32_t t1_rel = (uint32_t)(t1 - At);
-        const uint32_t lo_rel = doc_lo > At ? (uint32_t)(doc_lo - At) : 0u;
-        // 1. classify segment [B, B + 16) (relative to At) into W16 | S16 << 16; bytes outside
-        //    [doc_lo, whi) count as White_Space
+        const uint64_t Ab = I.Ab, doc_lo = I.doc_lo, doc_hi = I.doc_hi;
+        const uint32_t docid = I.docid;
+        // classify segment [B, B + 16) (relative to Ab) into W16 | S16 << 16; bytes outside the
+        // document count as White_Space (exact for every staged byte: no window cut)
+        const uint32_t lo_rel = doc_lo > Ab ? (uint32_t)(doc_lo - Ab) : 0u;
+        const uint32_t hi_rel = (uint32_t)min(doc_hi - Ab, (uint64_t)(BLK + HALO));
         auto classify = [&](const uint4 &x, uint32_t B) -> uint32_t {
             if (B >= hi_rel) return 0xFFFF0000u;
             uint32_t mA = 0, mB = 0;  // bytes 0..7 and 8..15: W bits 0..7, S bits 8..15
@@ -481,122 +521,197 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const uint32_t valid = ((1u << hi_ok) - 1u) & ~((1u << lo_inv) - 1u);
             return (m & (valid | (valid << 16))) | ((~valid & 0xFFFFu) << 16);
         };
-        const uint32_t m = classify(x0, (uint32_t)lane * SEG);
-        uint32_t m64 = lane == 1 ? classify(x1, (uint32_t)TILE) : 0u;  // the first halo segment is lane 1's p1
-        m64 = __builtin_amdgcn_readlane(m64, 1);
-        uint32_t mn = from_next_lane(m);
-        if (lane == 63) mn = m64;
-        const uint32_t Wpair = (m & 0xFFFFu) | (mn << 16);
-        const uint32_t Spair = (m >> 16) | (mn & 0xFFFF0000u);
-        mp[lane] = (uint64_t)Wpair | ((uint64_t)Spair << 32);
-        // 2. token starts of this lane's segment: the previous byte's class from lane l-1 (or the
-        //    staged byte before the tile); each start gets a queue slot by a wave prefix sum
-        uint32_t prev = from_prev_lane(m) >> 31;
-        if (lane == 0) prev = At > doc_lo ? (uint32_t)(s_lut[(x1.w >> 24) & 0x7Fu] >> 8) : 1u;
-        const uint32_t S = m >> 16;
-        uint32_t st = ~S & ((S << 1) | prev) & 0xFFFFu;
-        if ((uint32_t)lane * SEG >= t1_rel) st = 0;
-        const uint32_t cnt = __builtin_popcount(st);
-        const uint32_t incl = wave_incl_scan(cnt);
-        uint32_t pos = incl - cnt;
-        while (st) {
-            const uint32_t k = (uint32_t)__builtin_ctz(st);
-            st &= st - 1u;
-            queue[pos++] = (uint16_t)((uint32_t)lane * SEG + k);
-        }
-        const uint32_t total = (A.ablate & 4u) ? 0u : __builtin_amdgcn_readlane(incl, 63);
-        uint32_t nslow = 0;
-        my_tokens += (A.ablate & 4u) ? cnt : 0u;
-        wave_sync_lds();
+        auto na = [](const uint4 &x) { return ((x.x | x.y | x.z | x.w) & 0x80808080u) != 0u; };
+        const uint32_t l16 = (uint32_t)lane * SEG;
+        const uint32_t m0 = classify(X.v0, l16), m1 = classify(X.v1, 1024u + l16);
+        const uint32_t mh = lane_u32(lane == 1 ? classify(X.e, (uint32_t)BLK) : 0u, 1);
+        const bool n0 = na(X.v0), n1 = na(X.v1), ne = na(X.e);
+        // class of the byte before the block (lane 0's e, byte 15)
+        const uint32_t prev_blk =
+            Ab > doc_lo ? (uint32_t)(s_lut[(lane_u32(X.e.w, 0) >> 24) & 0x7Fu] >> 8) : 1u;
 
-        // 3. tokens of the queue, one per lane per round (queue, masks and window are read-only now)
-        for (uint32_t base = 0; base < total; base += 64) {
-            const uint32_t q = base + (uint32_t)lane;
-            const bool act = q < total;
-            const uint32_t s = act ? (uint32_t)queue[q] : 0u;
-            const uint64_t mw = mp[s >> 4];
-            const uint32_t Wp = (uint32_t)mw, Sp = (uint32_t)(mw >> 32);
-            const uint32_t i = s & 15u;
-            const uint32_t Sr = Sp >> i;
-            const uint32_t n = (uint32_t)__builtin_ctz(Sr | 0x80000000u);  // raw length (if Sr != 0)
-            const bool ended = Sr != 0u && !(cut && s + n >= hi_rel);  // end seen inside the staged bytes
-            const uint32_t w = __builtin_amdgcn_ubfe(Wp, i, n);          // \w bits of the raw token
-            const uint32_t first = (uint32_t)__builtin_ctz(w | 0x80000000u);
-            const uint32_t last = 31u - (uint32_t)__builtin_clz(w | 1u);
-            const uint32_t span = last - first + 1u;
-            const bool fast = act && ended && w != 0u && span <= 16u;
-            const bool slow = act && (!ended || (w != 0u && span > 16u));
-            // key bytes [s + first, + span) of the window, big-endian packed, zero padded
-            const uint32_t off = (uint32_t)BEHIND + s + first;
-            const uint32_t dw = off >> 2, r = off & 3u;
-            const uint32_t d0 = win32[dw], d1 = win32[dw + 1], d2 = win32[dw + 2], d3 = win32[dw + 3],
-                           d4 = win32[dw + 4];
-            const uint32_t *zm = s_zm[fast ? span : 0u];
-            const uint32_t bsel = 0x00010203u + r * 0x01010101u;
-            const uint32_t o0 = __builtin_amdgcn_perm(d1, d0, (bsel & ~zm[0]) | (0x0C0C0C0Cu & zm[0]));
-            const uint32_t o1 = __builtin_amdgcn_perm(d2, d1, (bsel & ~zm[1]) | (0x0C0C0C0Cu & zm[1]));
-            const uint32_t o2 = __builtin_amdgcn_perm(d3, d2, (bsel & ~zm[2]) | (0x0C0C0C0Cu & zm[2]));
-            const uint32_t o3 = __builtin_amdgcn_perm(d4, d3, (bsel & ~zm[3]) | (0x0C0C0C0Cu & zm[3]));
-            uint64_t tk0 = ((uint64_t)o0 << 32) | o1, tk1 = ((uint64_t)o2 << 32) | o3;
-            uint32_t tlen = span;
-            // deleted bytes inside the token ("don't"): squeeze out each gap of the \w mask
-            uint32_t gaps = fast ? (~(w >> first) & ((1u << span) - 1u)) : 0u;
-            if (__any(gaps != 0u)) {
-                while (gaps) {
-                    const uint32_t ga = (uint32_t)__builtin_ctz(gaps);                // gap start (key byte)
-                    const uint32_t gl = (uint32_t)__builtin_ctz(~(gaps >> ga));       // gap length
-                    const uint32_t sh = 8u * gl;                                      // 8..120 bits
-                    // shifted = (tk0:tk1) << sh; keep the top ga bytes, take the rest from shifted
-                    uint64_t s0v, s1v;
-                    if (sh >= 64u) { s0v = tk1 << (sh - 64u); s1v = 0; }
-                    else { s0v = (tk0 << sh) | (tk1 >> (64u - sh)); s1v = tk1 << sh; }
-                    const uint32_t kb = 8u * ga;                                      // kept bits
-                    const uint64_t m0 = kb >= 64u ? ~0ull : (kb ? ~0ull << (64u - kb) : 0ull);
-                    const uint64_t m1 = kb <= 64u ? 0ull : ~0ull << (128u - kb);
-                    tk0 = (tk0 & m0) | (s0v & ~m0);
-                    tk1 = (tk1 & m1) | (s1v & ~m1);
-                    gaps = (gaps >> (ga + gl)) << ga;
-                    tlen -= gl;
-                }
+#pragma unroll 1
+        for (uint32_t j = 0; j < NSUB; ++j) {
+            const uint64_t At = Ab + (uint64_t)j * TILE;
+            if (At >= doc_hi) break;
+            const uint32_t tj = kt + j;
+            const bool last = j == NSUB - 1;
+            const uint4 x = j == 0 ? X.v0 : X.v1;
+            const uint4 xh = j == 0 ? X.v1 : X.e;  // halo source
+            const uint32_t m = j == 0 ? m0 : m1;
+            const uint32_t mprev = m0;
+            // non-ASCII anywhere the fast path reads: the tile, the first halo segment, the byte before
+            const bool nx = j == 0 ? n0 : n1;
+            const bool nh = j == 0 ? n1 : ne;
+            const bool np = j == 0 ? ne : n0;
+            const uint32_t hl = last ? 1u : 0u;  // lane holding the first halo segment
+            const bool nonascii = nx || ((uint32_t)lane == hl && nh) || ((uint32_t)lane == (j ? 63u : 0u) && np);
+            if (__any(nonascii)) {  // recorded; processed after the main loop
+                gword |= 1ull << (tj & 63u);
+                continue;
             }
-            // slow tokens (past the 2-segment window or the staged halo, or > 16 raw key bytes) are
-            // deferred: their starts go to the consumed front of the queue (every lane has read its
-            // own entry, and nslow + rank <= base + lane)
-            const uint64_t sm = __ballot(slow);
-            if (sm) {
-                if (slow) queue[nslow + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u))] =
-                    (uint16_t)s;
-                nslow += (uint32_t)__builtin_popcountll(sm);
-            }
-            my_tokens += fast ? 1u : 0u;
-            emit(A, table, s_bcount, s_bcap, s_bbase, fast, tk0, tk1, tlen, At + s, n, docid);
-        }
-        // deferred slow tokens: the exact per-codepoint walker, one token per lane
-        if (nslow) {
+            const uint64_t t1 = min(At + (uint64_t)TILE, doc_hi);
+            const uint64_t whi = min(t1 + (uint64_t)HALO, doc_hi);
+            const uint64_t wbase = At - (uint64_t)BEHIND;
+
+            // stage the tile and its 64-byte halo (the previous tile's readers are done: program order)
             wave_sync_lds();
-            const uint64_t wbase_ = wbase;
-            auto rd = [&](uint64_t a) -> uint32_t {
-                return (a >= wlo && a < whi) ? (uint32_t)win[a - wbase_] : (uint32_t)A.in[a];
-            };
-            for (uint32_t base = 0; base < nslow; base += 64) {
+            reinterpret_cast<uint4 *>(win)[1 + lane] = x;
+            if (!last ? lane < 4 : (lane >= 1 && lane < 5))
+                reinterpret_cast<uint4 *>(win)[65 + (!last ? lane : lane - 1)] = xh;
+            // masks: this lane's segment and the next one (lane 63: the first halo segment)
+            uint32_t mn = from_next_lane(m);
+            if (lane == 63) mn = !last ? lane_u32(m1, 0) : mh;
+            const uint32_t Wpair = (m & 0xFFFFu) | (mn << 16);
+            const uint32_t Spair = (m >> 16) | (mn & 0xFFFF0000u);
+            mp[lane] = (uint64_t)Wpair | ((uint64_t)Spair << 32);
+            // token starts of this lane's segment: the previous byte's class from lane l-1 (lane 0:
+            // the previous tile's last byte); each start gets a queue slot by a wave prefix sum
+            uint32_t prev = from_prev_lane(m) >> 31;
+            if (lane == 0) prev = j == 0 ? prev_blk : (lane_u32(mprev, 63) >> 31);
+            const uint32_t S = m >> 16;
+            uint32_t st = ~S & ((S << 1) | prev) & 0xFFFFu;
+            if (l16 >= (uint32_t)(t1 - At)) st = 0;
+            const uint32_t cnt = __builtin_popcount(st);
+            const uint32_t incl = wave_incl_scan(cnt);
+            uint32_t pos = incl - cnt;
+            while (st) {
+                const uint32_t kb = (uint32_t)__builtin_ctz(st);
+                st &= st - 1u;
+                queue[pos++] = (uint16_t)(l16 + kb);
+            }
+            const uint32_t total = (A.ablate & 4u) ? 0u : lane_u32(incl, 63);
+            uint32_t nslow = 0;
+            my_tokens += (A.ablate & 4u) ? cnt : 0u;
+            wave_sync_lds();
+
+            // tokens of the queue, one per lane per round (queue, masks and window are read-only now)
+            for (uint32_t base = 0; base < total; base += 64) {
                 const uint32_t q = base + (uint32_t)lane;
-                bool have = false;
-                uint64_t tk0 = 0, tk1 = 0, a = 0;
-                uint32_t tlen = 0, traw = 0;
-                if (q < nslow) {
-                    a = At + queue[q];
-                    uint64_t e2;
-                    if (walk_token(rd, a, doc_hi, A.counters, tk0, tk1, tlen, e2) && tlen > 0) {
-                        have = true;
-                        traw = (uint32_t)(e2 - a);
+                const bool act = q < total;
+                const uint32_t s = act ? (uint32_t)queue[q] : 0u;
+                const uint64_t mw = mp[s >> 4];
+                const uint32_t Wp = (uint32_t)mw, Sp = (uint32_t)(mw >> 32);
+                const uint32_t i = s & 15u;
+                const uint32_t Sr = Sp >> i;
+                const uint32_t n = (uint32_t)__builtin_ctz(Sr | 0x80000000u);  // raw length (if Sr != 0)
+                const bool ended = Sr != 0u;                                     // end inside the 2 segments
+                const uint32_t w = __builtin_amdgcn_ubfe(Wp, i, n);              // \w bits of the raw token
+                const uint32_t first = (uint32_t)__builtin_ctz(w | 0x80000000u);
+                const uint32_t last = 31u - (uint32_t)__builtin_clz(w | 1u);
+                const uint32_t span = last - first + 1u;
+                const bool fast = act && ended && w != 0u && span <= 16u;
+                const bool slow = act && (!ended || (w != 0u && span > 16u));
+                // key bytes [s + first, + span) of the window, big-endian packed, zero padded
+                const uint32_t off = (uint32_t)BEHIND + s + first;
+                const uint32_t dw = off >> 2, r = off & 3u;
+                const uint32_t d0 = win32[dw], d1 = win32[dw + 1], d2 = win32[dw + 2], d3 = win32[dw + 3],
+                               d4 = win32[dw + 4];
+                const uint32_t *zm = s_zm[fast ? span : 0u];
+                const uint32_t bsel = 0x00010203u + r * 0x01010101u;
+                const uint32_t o0 = __builtin_amdgcn_perm(d1, d0, (bsel & ~zm[0]) | (0x0C0C0C0Cu & zm[0]));
+                const uint32_t o1 = __builtin_amdgcn_perm(d2, d1, (bsel & ~zm[1]) | (0x0C0C0C0Cu & zm[1]));
+                const uint32_t o2 = __builtin_amdgcn_perm(d3, d2, (bsel & ~zm[2]) | (0x0C0C0C0Cu & zm[2]));
+                const uint32_t o3 = __builtin_amdgcn_perm(d4, d3, (bsel & ~zm[3]) | (0x0C0C0C0Cu & zm[3]));
+                uint64_t tk0 = ((uint64_t)o0 << 32) | o1, tk1 = ((uint64_t)o2 << 32) | o3;
+                uint32_t tlen = span;
+                // deleted bytes inside the token ("don't"): squeeze out each gap of the \w mask
+                uint32_t gaps = fast ? (~(w >> first) & ((1u << span) - 1u)) : 0u;
+                if (__any(gaps != 0u)) {
+                    while (gaps) {
+                        const uint32_t ga = (uint32_t)__builtin_ctz(gaps);           // gap start (key byte)
+                        const uint32_t gl = (uint32_t)__builtin_ctz(~(gaps >> ga));  // gap length
+                        const uint32_t sh = 8u * gl;                                 // 8..120 bits
+                        // shifted = (tk0:tk1) << sh; keep the top ga bytes, take the rest from shifted
+                        uint64_t s0v, s1v;
+                        if (sh >= 64u) { s0v = tk1 << (sh - 64u); s1v = 0; }
+                        else { s0v = (tk0 << sh) | (tk1 >> (64u - sh)); s1v = tk1 << sh; }
+                        const uint32_t kb = 8u * ga;                                 // kept bits
+                        const uint64_t k0m = kb >= 64u ? ~0ull : (kb ? ~0ull << (64u - kb) : 0ull);
+                        const uint64_t k1m = kb <= 64u ? 0ull : ~0ull << (128u - kb);
+                        tk0 = (tk0 & k0m) | (s0v & ~k0m);
+                        tk1 = (tk1 & k1m) | (s1v & ~k1m);
+                        gaps = (gaps >> (ga + gl)) << ga;
+                        tlen -= gl;
                     }
                 }
-                my_tokens += have ? 1u : 0u;
-                emit(A, table, s_bcount, s_bcap, s_bbase, have, tk0, tk1, tlen, a, traw, docid);
+                // slow tokens (past the 2-segment window, or > 16 raw key bytes) are deferred: their
+                // starts go to the consumed front of the queue (every lane has read its own entry,
+                // and nslow + rank <= base + lane)
+                const uint64_t sm = __ballot(slow);
+                if (sm) {
+                    if (slow)
+                        queue[nslow + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u))] =
+                            (uint16_t)s;
+                    nslow += (uint32_t)__builtin_popcountll(sm);
+                }
+                my_tokens += fast ? 1u : 0u;
+                emit(A, table, s_bcount, s_bcap, s_bbase, fast, tk0, tk1, tlen, At + s, n, docid);
+            }
+            // deferred slow tokens: the exact per-codepoint walker, one token per lane (forward
+            // reads only: the staged bytes are [At, whi))
+            if (nslow) {
+                wave_sync_lds();
+                auto rd = [&](uint64_t a) -> uint32_t {
+                    if (a >= At && a < whi) return (uint32_t)win[a - wbase];
+                    return (uint32_t)gp(A.in)[a];
+                };
+                for (uint32_t base = 0; base < nslow; base += 64) {
+                    const uint32_t q = base + (uint32_t)lane;
+                    bool have = false;
+                    uint64_t tk0 = 0, tk1 = 0, a = 0;
+                    uint32_t tlen = 0, traw = 0;
+                    if (q < nslow) {
+                        a = At + queue[q];
+                        uint64_t e2;
+                        if (walk_token(rd, a, doc_hi, A.counters, tk0, tk1, tlen, e2) && tlen > 0) {
+                            have = true;
+                            traw = (uint32_t)(e2 - a);
+                        }
+                    }
+                    my_tokens += have ? 1u : 0u;
+                    emit(A, table, s_bcount, s_bcap, s_bbase, have, tk0, tk1, tlen, a, traw, docid);
+                }
             }
         }
-        }  // ASCII tile
+        kt += NSUB;
+    };
+
+    // Main loop: two register sets, A and B.  Block c's loads were issued one block earlier; the
+    // next block's loads go out before c is processed, so exactly five loads are younger than c's
+    // when its data is first used.  Past the end, the "next" block is a reload of the current one.
+    const uint64_t stride = (uint64_t)gridDim.x * NW;
+    const uint64_t nb = A.n_chunks;  // blocks of the job
+    uint64_t c = (uint64_t)blockIdx.x * NW + wv;
+    uint32_t dcur = 0;
+    Blk XA, XB;
+    BlkInfo IA{}, IB{};
+    // Make a block's registers available HERE (the compiler waits for its loads at this point, when
+    // only older loads and stores are outstanding), before the next block's loads are issued --
+    // otherwise the scheduler sinks the first use below them and the wait covers the new loads too.
+    auto settle = [](Blk &X) {
+        asm volatile("" : "+v"(X.v0.x), "+v"(X.v0.y), "+v"(X.v0.z), "+v"(X.v0.w), "+v"(X.v1.x), "+v"(X.v1.y),
+                     "+v"(X.v1.z), "+v"(X.v1.w), "+v"(X.e.x), "+v"(X.e.y), "+v"(X.e.z), "+v"(X.e.w));
+    };
+    if (c < nb) {
+        IA = locate_blk(A, c, dcur);
+        load_blk(IA, XA);
+    }
+    while (c < nb) {
+        const uint64_t cB = c + stride;
+        IB = cB < nb ? locate_blk(A, cB, dcur) : IA;
+        settle(XA);
+        load_blk(IB, XB);
+        process_blk(IA, XA);
+        c = cB;
+        if (c >= nb) break;
+        const uint64_t cA = c + stride;
+        IA = cA < nb ? locate_blk(A, cA, dcur) : IB;
+        settle(XB);
+        load_blk(IA, XA);
+        process_blk(IB, XB);
+        c = cA;
     }
     if (lane == 0 && kt) gbits[(kt - 1) >> 6] = gword;  // the last (partial) word
 
@@ -606,12 +721,13 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         uint32_t dgen = 0;
         const uint64_t c0 = (uint64_t)blockIdx.x * NW + wv;
         for (uint32_t wi = 0; wi * 64u < nk; ++wi) {
-            uint64_t bits = __builtin_amdgcn_readfirstlane((uint32_t)gbits[wi]) |
-                            ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(gbits[wi] >> 32)) << 32);
+            const uint64_t gw = gbits[wi];
+            uint64_t bits = (uint64_t)first_u32((uint32_t)gw) | ((uint64_t)first_u32((uint32_t)(gw >> 32)) << 32);
             while (bits) {
                 const uint32_t kk = wi * 64u + (uint32_t)__builtin_ctzll(bits);
                 bits &= bits - 1u;
-                const TileInfo T = locate(A, c0 + (uint64_t)kk * stride, dgen);
+                const BlkInfo b = locate_blk(A, c0 + (uint64_t)(kk / NSUB) * stride, dgen);
+                const TileInfo T = sub_tile(b, kk % NSUB);
                 uint4 x0, x1;
                 load(T, x0, x1);
                 wave_sync_lds();
@@ -627,7 +743,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // ---- flush the LDS table into this workgroup's region, sorted by bucket
     __syncthreads();
     uint16_t *s_rank = &s_q[0][0];
-    uint32_t *bcount = A.bcount + (uint64_t)blockIdx.x * MRG_NBUCKET;
+    GAS uint32_t *bcount = gp(A.bcount) + (uint64_t)blockIdx.x * MRG_NBUCKET;
     uint32_t my_tail = 0;
     for (int b = tid; b < MRG_NBUCKET; b += WG) {
         my_tail += s_bcount[b];
@@ -648,12 +764,12 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const uint32_t v = s_hist[b0 + lane];
             const uint32_t inc = wave_incl_scan(v);
             s_hist[b0 + lane] = run + inc - v;
-            run += __builtin_amdgcn_readlane(inc, 63);
+            run += lane_u32(inc, 63);
         }
         if (lane == 0) s_hist[MRG_NBUCKET] = run;
     }
     __syncthreads();
-    uint32_t *foff = A.foff + (uint64_t)blockIdx.x * (MRG_NBUCKET + 1);
+    GAS uint32_t *foff = gp(A.foff) + (uint64_t)blockIdx.x * (MRG_NBUCKET + 1);
     for (int b = tid; b <= MRG_NBUCKET; b += WG) foff[b] = s_hist[b];
     const uint64_t reg = (uint64_t)blockIdx.x * CAP;
     for (int i = tid; i < CAP; i += WG) {
@@ -662,10 +778,10 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const uint32_t d = IDX ? s_doc[i] : MRG_EMPTY_DOC;
         const uint32_t b = bucket_of(key_hash(k.a, k.b, d, A.hash_bits));
         const uint64_t pos2 = reg + s_hist[b] + s_rank[i];
-        A.fk0[pos2] = k.a;
-        A.fk1[pos2] = k.b;
-        A.fcnt[pos2] = s_cnt[i];
-        if (IDX) A.fdoc[pos2] = d;
+        gp(A.fk0)[pos2] = k.a;
+        gp(A.fk1)[pos2] = k.b;
+        gp(A.fcnt)[pos2] = s_cnt[i];
+        if (IDX) gp(A.fdoc)[pos2] = d;
     }
     uint32_t t = my_tokens, tl = my_tail;
     for (int off = 32; off > 0; off >>= 1) {
@@ -673,8 +789,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         tl += __shfl_down(tl, off);
     }
     if (lane == 0) {
-        atomicAdd(&A.counters[CNT_TOKENS], (unsigned long long)t);
-        atomicAdd(&A.counters[CNT_REC], (unsigned long long)tl);
+        g_add(&A.counters[CNT_TOKENS], (unsigned long long)t);
+        g_add(&A.counters[CNT_REC], (unsigned long long)tl);
     }
 }
 
@@ -741,10 +857,10 @@ void mrg_launch_map(const MapArgs &h, MapArgs *a, int app, int grid, int lds_cap
 
 int mrg_map_cap(int lds_cap) { return lds_cap >= 4096 ? 4096 : 2048; }
 
-// tiles of a document [lo, hi): on the 16-byte grid starting at lo & ~15
+// BLK-byte blocks of a document [lo, hi): on the 16-byte grid starting at lo & ~15
 uint64_t mrg_map_tiles(uint64_t lo, uint64_t hi) {
     if (hi <= lo) return 0;
-    return (hi - (lo & ~15ull) + TILE - 1) / TILE;
+    return (hi - (lo & ~15ull) + BLK - 1) / BLK;
 }
 
 int mrg_map_max_grid(int app, int lds_cap, int device) {

@@ -10,6 +10,7 @@
 #define MRG_MAP_TILE (64 * MRG_MAP_SEG)  // 1 KiB tile per WAVE iteration (waves never synchronise)
 #define MRG_MAP_HALO 64         // bytes after the tile staged in LDS (tokens crossing the tile end)
 #define MRG_MAP_BEHIND 16       // bytes before the tile staged in LDS (previous codepoint)
+#define MRG_MAP_NSUB 2          // 1 KiB tiles per wave iteration (one block, prefetched one block ahead)
 
 // Tail records (LDS-table misses) are bucketed by key hash into MRG_NBUCKET buckets; every
 // (bucket, map workgroup) pair owns a private region of the pool, so appending is an LDS atomic.
@@ -108,7 +109,7 @@ struct LongItems {
 // ---- k_map.hip
 // `dev_args` is device memory for one MapArgs (the kernel reads its arguments from there)
 void mrg_launch_map(const MapArgs &a, MapArgs *dev_args, int app, int grid, int lds_cap, hipStream_t s);
-uint64_t mrg_map_tiles(uint64_t doc_lo, uint64_t doc_hi);  // 1 KiB wave tiles of a document (16-B grid)
+uint64_t mrg_map_tiles(uint64_t doc_lo, uint64_t doc_hi);  // wave blocks (NSUB KiB) of a document (16-B grid)
 int mrg_map_cap(int lds_cap);  // LDS-table entries per map workgroup actually used for lds_cap
 int mrg_map_max_grid(int app, int lds_cap, int device);
 void mrg_launch_long_prep(const uint8_t *base, const uint64_t *start, const uint32_t *rawlen, uint64_t n,

@@ -475,7 +475,7 @@ void job_map(mrg_ctx *c) {
         A.lstart = M.lstart; A.llen = M.llen; A.ldoc = M.ldoc; A.lcap = lcap;
         {  // one bit per tile of each wave (written whole by the kernel: no clearing needed)
             const uint64_t waves = (uint64_t)grid * MRG_MAP_WAVES;
-            const uint64_t per_wave = (n_chunks + waves - 1) / waves;
+            const uint64_t per_wave = MRG_MAP_NSUB * ((n_chunks + waves - 1) / waves);  // 1 KiB tiles per wave
             A.kwords = (uint32_t)std::max<uint64_t>(1, (per_wave + 63) / 64);
             M.gbits = pget<uint64_t>(p, waves * A.kwords);
             A.gbits = M.gbits;

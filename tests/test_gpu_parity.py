@@ -127,6 +127,19 @@ def test_tile_boundaries_and_long_tokens(ctx):
         assert run_wc(ctx, [data], R) == O.wc([data], R, O.FAST)
 
 
+def test_document_offsets_and_tile_edges(ctx):
+    """Documents starting at every offset mod 16, with words ending exactly on 1 KiB tile and 2 KiB
+    block edges (a start at a tile's first byte takes the previous tile's last class)."""
+    import oracle_lib as O
+    from gpu_util import run_wc
+    unit = b"five six seven "  # 15 bytes: word/space phases cycle through every tile alignment
+    for lead in range(16):
+        d0 = (b"ab " * 800)[:lead + 16 * 37]
+        docs = [d0, unit * 150, b"".join(b"w%03da w%03db " % (i, i) for i in range(200)), unit * 3]
+        exp = O.wc(docs, 3, O.FAST)
+        assert run_wc(ctx, docs, 3) == exp, lead
+
+
 @pytest.mark.parametrize("bits", [1, 4, 12, 20])
 def test_forced_hash_collisions(ctx, corpus, bits):
     """Truncated internal hashes: output must be identical (collision-safe tie-breaks)."""
