@@ -16,13 +16,27 @@ inline dim3 grid_for(uint64_t n, int b = 256) { return dim3((unsigned)((n + b - 
 
 // ---------------------------------------------------------------- per-bucket LDS aggregation
 // One workgroup per hash bucket sums every record of its bucket -- the map workgroups' tail regions
-// (count 1 each) and the bucket's slice of every map workgroup's flushed LDS table -- in an LDS
-// table with the monotone claim protocol.  A key that finds no slot (more distinct keys in the
-// bucket than the table holds) is written to the overflow list; since slots only ever fill, a key
-// that failed once fails always, so the LDS table and the overflow path never share a key.
-constexpr int BA_WG = 512;
+// (count 1 each), the bucket's slice of every map workgroup's flushed LDS table and the bucket's
+// overflow list -- in an LDS table.  A key that finds no slot within the probe limit (more distinct
+// keys in the bucket than the table holds) goes to the overflow list; since slots only ever fill, a
+// key that failed once fails always, so the LDS table and the overflow path never share a key.
+//
+// Throughput: the tail regions are the bulk (hundreds of MB); every wave streams them in chunks of
+// 4 records per lane (1 KiB per load instruction), with the next chunk's loads in flight while the
+// current one is summed, and a record that finds its key costs one 16-byte LDS read + one LDS add.
+constexpr int BA_WG = 1024;
+constexpr int BA_NW = BA_WG / 64;
 constexpr int BA_CAP = MRG_BA_CAP;
 constexpr int BA_PROBE = 64;
+constexpr int BA_U = 4;            // records per lane per chunk
+constexpr int BA_MAXREG = 2048;    // map workgroups (regions) the per-region size table holds
+
+#define GASK __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ GASK T *gk(T *p) {
+    return (GASK T *)p;
+}
+typedef uint64_t u64x2k __attribute__((ext_vector_type(2)));
 
 // the map kernel's key hash (k_map.hip key_hash): bucket = top 9 bits
 __device__ __forceinline__ uint32_t ba_hash(uint64_t a, uint64_t b, uint32_t d, uint32_t hash_bits) {
@@ -31,24 +45,38 @@ __device__ __forceinline__ uint32_t ba_hash(uint64_t a, uint64_t b, uint32_t d, 
     return h;
 }
 
+struct alignas(16) BaKey {
+    unsigned long long a, b;
+};
+
+// Add c to key (a, b[, d]).  Slots fill monotonically (k0, then k1, then doc, each by CAS from its
+// empty value), so a slot whose fields all equal the key is the key's slot for good: the common case
+// is one 16-byte read and one add.  A partly claimed slot is resolved by the CAS protocol.
 template <bool IDX>
-__device__ __forceinline__ bool ba_insert(unsigned long long *k0, unsigned long long *k1, unsigned long long *cnt,
-                                          unsigned int *doc, uint64_t a, uint64_t b, uint32_t d, uint64_t c,
-                                          uint32_t h) {
-    uint32_t slot = (h >> 11) & (BA_CAP - 1);  // bits disjoint from the bucket (top 9) and map-group bits
+__device__ __forceinline__ bool ba_add(BaKey *key, unsigned long long *cnt, unsigned int *doc, uint64_t a,
+                                       uint64_t b, uint32_t d, uint64_t c, uint32_t h) {
+    uint32_t slot = (h >> 11) & (BA_CAP - 1);  // bits disjoint from the bucket (top 9)
     for (int p = 0; p < BA_PROBE; ++p) {
-        const unsigned long long x = atomicCAS(&k0[slot], MRG_EMPTY_K0, (unsigned long long)a);
-        if (x == MRG_EMPTY_K0 || x == a) {
-            const unsigned long long y = atomicCAS(&k1[slot], MRG_EMPTY_K1, (unsigned long long)b);
-            if (y == MRG_EMPTY_K1 || y == b) {
-                bool ok = true;
-                if (IDX) {
-                    const unsigned int z = atomicCAS(&doc[slot], MRG_EMPTY_DOC, d);
-                    ok = (z == MRG_EMPTY_DOC || z == d);
-                }
-                if (ok) {
-                    atomicAdd(&cnt[slot], (unsigned long long)c);
-                    return true;
+        const BaKey k = key[slot];
+        const bool dk = !IDX || doc[slot] == d;
+        if (k.a == a && k.b == b && dk) {
+            atomicAdd(&cnt[slot], (unsigned long long)c);
+            return true;
+        }
+        if (k.a == MRG_EMPTY_K0 || (k.a == a && (k.b == MRG_EMPTY_K1 || (IDX && k.b == b)))) {
+            const unsigned long long x = atomicCAS(&key[slot].a, MRG_EMPTY_K0, (unsigned long long)a);
+            if (x == MRG_EMPTY_K0 || x == a) {
+                const unsigned long long y = atomicCAS(&key[slot].b, MRG_EMPTY_K1, (unsigned long long)b);
+                if (y == MRG_EMPTY_K1 || y == b) {
+                    bool ok = true;
+                    if (IDX) {
+                        const unsigned int z = atomicCAS(&doc[slot], MRG_EMPTY_DOC, d);
+                        ok = (z == MRG_EMPTY_DOC || z == d);
+                    }
+                    if (ok) {
+                        atomicAdd(&cnt[slot], (unsigned long long)c);
+                        return true;
+                    }
                 }
             }
         }
@@ -58,46 +86,110 @@ __device__ __forceinline__ bool ba_insert(unsigned long long *k0, unsigned long 
 }
 
 template <bool IDX>
-__global__ __launch_bounds__(BA_WG) void k_bucket_agg(BucketArgs A) {
-    __shared__ unsigned long long s_k0[BA_CAP];
-    __shared__ unsigned long long s_k1[BA_CAP];
+__global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
+    __shared__ BaKey s_key[BA_CAP];
     __shared__ unsigned long long s_cnt[BA_CAP];
     __shared__ unsigned int s_doc[IDX ? BA_CAP : 1];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    __shared__ uint32_t s_rn[BA_MAXREG];  // tail records of region r in this bucket
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int i = tid; i < BA_CAP; i += BA_WG) {
-        s_k0[i] = MRG_EMPTY_K0;
-        s_k1[i] = MRG_EMPTY_K1;
+        s_key[i] = BaKey{MRG_EMPTY_K0, MRG_EMPTY_K1};
         s_cnt[i] = 0;
         if (IDX) s_doc[i] = MRG_EMPTY_DOC;
     }
-    __syncthreads();
     const uint32_t b = blockIdx.x;
     constexpr uint32_t RW = IDX ? 3u : 2u;
-    const uint32_t cap = A.bcap[b];
-    // every map workgroup r left (a) its tail records of this bucket in region (b, r) of the pool
-    // and (b) this bucket's slice of its flushed LDS table; wave wv takes r = wv, wv + 8, ...
-    for (uint32_t r = wv; r < A.nreg; r += BA_WG / 64) {
-        const uint32_t n = min(A.bcount[(uint64_t)r * MRG_NBUCKET + b], cap);
-        const uint64_t *src = A.pool + (A.rbase[b] + (uint64_t)r * cap) * RW;
-        for (uint32_t base = 0; base < n; base += 64) {
-            const uint32_t i = base + lane;
-            bool ovf = false;
-            uint64_t a = 0, c = 0;
-            uint32_t d = MRG_EMPTY_DOC;
-            if (i < n) {
-                const uint64_t *rec = src + (uint64_t)i * RW;
-                a = rec[0];
-                c = rec[1];
-                if (IDX) d = (uint32_t)rec[2];
-                ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
-            }
-            const uint64_t j = mrg_wave_append(&A.counters[CNT_OVF2], ovf);
-            if (ovf && j < A.ocap) {
-                A.ok0[j] = a; A.ok1[j] = c; A.ocnt[j] = 1u;
-                if (IDX) A.odoc[j] = d;
+    const uint32_t cap = gk(A.bcap)[b];
+    const uint32_t nreg = A.nreg;
+    for (uint32_t r = tid; r < nreg; r += BA_WG) s_rn[r] = min(gk(A.bcount)[(uint64_t)r * MRG_NBUCKET + b], cap);
+    __syncthreads();
+
+    auto overflow = [&](bool ovf, uint64_t a, uint64_t c, uint32_t d, uint64_t n2) {
+        const uint64_t j = mrg_wave_append(&A.counters[CNT_OVF2], ovf);
+        if (ovf && j < A.ocap) {
+            gk(A.ok0)[j] = a; gk(A.ok1)[j] = c; gk(A.ocnt)[j] = (uint32_t)n2;
+            if (IDX) gk(A.odoc)[j] = d;
+        }
+    };
+
+    // ---- 1. tail regions: wave wv takes regions wv, wv + 16, ...; chunks of 64 * BA_U records
+    const GASK uint64_t *pool = gk(A.pool) + A.rbase[b] * RW;
+    struct Chunk {
+        u64x2k k[BA_U];
+        uint32_t d[IDX ? BA_U : 1];
+    };
+    auto first_chunk = [&](uint32_t &r, uint32_t &off) {
+        r = (uint32_t)wv;
+        off = 0;
+        while (r < nreg && s_rn[r] == 0) r += BA_NW;
+    };
+    auto next_chunk = [&](uint32_t &r, uint32_t &off) {
+        off += 64u * BA_U;
+        while (r < nreg && off >= s_rn[r]) {
+            r += BA_NW;
+            off = 0;
+        }
+    };
+    // unconditional loads: an index past the region's end reads its last record (masked later)
+    auto load_chunk = [&](uint32_t r, uint32_t off, Chunk &X) {
+        const uint32_t n = s_rn[r];
+        const GASK uint64_t *src = pool + (uint64_t)r * cap * RW;
+#pragma unroll
+        for (int k = 0; k < BA_U; ++k) {
+            const uint32_t i = min(off + 64u * k + (uint32_t)lane, n - 1u);
+            if (IDX) {
+                X.k[k] = u64x2k{src[(uint64_t)i * 3], src[(uint64_t)i * 3 + 1]};
+                X.d[k] = (uint32_t)src[(uint64_t)i * 3 + 2];
+            } else {
+                X.k[k] = *reinterpret_cast<const GASK u64x2k *>(src + (uint64_t)i * 2);
             }
         }
-        const uint32_t *fo = A.foff + (uint64_t)r * (MRG_NBUCKET + 1);
+    };
+    auto settle = [](Chunk &X) {
+#pragma unroll
+        for (int k = 0; k < BA_U; ++k) asm volatile("" : "+v"(X.k[k]));
+        if (IDX)
+            for (int k = 0; k < BA_U; ++k) asm volatile("" : "+v"(X.d[k]));
+    };
+    auto sum_chunk = [&](uint32_t r, uint32_t off, const Chunk &X) {
+        const uint32_t n = s_rn[r];
+#pragma unroll
+        for (int k = 0; k < BA_U; ++k) {
+            const bool ok = off + 64u * k + (uint32_t)lane < n;
+            const uint64_t a = X.k[k].x, c = X.k[k].y;
+            const uint32_t d = IDX ? X.d[k] : MRG_EMPTY_DOC;
+            bool ovf = false;
+            if (ok) ovf = !ba_add<IDX>(s_key, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
+            if (__any(ovf)) overflow(ovf, a, c, d, 1);
+        }
+    };
+    {
+        Chunk XA, XB;
+        uint32_t rA, oA;
+        first_chunk(rA, oA);
+        if (rA < nreg) load_chunk(rA, oA, XA);
+        while (rA < nreg) {
+            uint32_t rB = rA, oB = oA;
+            next_chunk(rB, oB);
+            settle(XA);
+            if (rB < nreg) load_chunk(rB, oB, XB);
+            else load_chunk(rA, oA, XB);  // keep the load count fixed
+            sum_chunk(rA, oA, XA);
+            if (rB >= nreg) break;
+            rA = rB;
+            oA = oB;
+            next_chunk(rA, oA);
+            settle(XB);
+            if (rA < nreg) load_chunk(rA, oA, XA);
+            else load_chunk(rB, oB, XA);
+            sum_chunk(rB, oB, XB);
+        }
+    }
+
+    // ---- 2. this bucket's slice of every map workgroup's flushed table (a few entries each)
+    for (uint32_t r = wv; r < nreg; r += BA_NW) {
+        const GASK uint32_t *fo = gk(A.foff) + (uint64_t)r * (MRG_NBUCKET + 1);
         const uint32_t lo = fo[b], hi = fo[b + 1];
         const uint64_t reg = (uint64_t)r * A.regcap;
         for (uint32_t base = lo; base < hi; base += 64) {
@@ -106,55 +198,46 @@ __global__ __launch_bounds__(BA_WG) void k_bucket_agg(BucketArgs A) {
             uint64_t a = 0, c = 0;
             uint32_t d = MRG_EMPTY_DOC, n2 = 0;
             if (k < hi) {
-                a = A.fk0[reg + k];
-                c = A.fk1[reg + k];
-                n2 = A.fcnt[reg + k];
-                if (IDX) d = A.fdoc[reg + k];
-                ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, n2, ba_hash(a, c, d, A.hash_bits));
+                a = gk(A.fk0)[reg + k];
+                c = gk(A.fk1)[reg + k];
+                n2 = gk(A.fcnt)[reg + k];
+                if (IDX) d = gk(A.fdoc)[reg + k];
+                ovf = !ba_add<IDX>(s_key, s_cnt, s_doc, a, c, d, n2, ba_hash(a, c, d, A.hash_bits));
             }
-            const uint64_t j = mrg_wave_append(&A.counters[CNT_OVF2], ovf);
-            if (ovf && j < A.ocap) {
-                A.ok0[j] = a; A.ok1[j] = c; A.ocnt[j] = n2;
-                if (IDX) A.odoc[j] = d;
-            }
+            if (__any(ovf)) overflow(ovf, a, c, d, n2);
         }
     }
-    // records that did not fit their map workgroup's region: this bucket's overflow list
+    // ---- 3. records that did not fit their map workgroup's region: this bucket's overflow list
     {
-        const uint32_t n = min(A.monext[b], A.mocap);
-        const uint64_t *src = A.movf + (uint64_t)b * A.mocap * RW;
+        const uint32_t n = min(gk(A.monext)[b], A.mocap);
+        const GASK uint64_t *src = gk(A.movf) + (uint64_t)b * A.mocap * RW;
         for (uint32_t base = wv * 64u; base < n; base += BA_WG) {
             const uint32_t i = base + lane;
             bool ovf = false;
             uint64_t a = 0, c = 0;
             uint32_t d = MRG_EMPTY_DOC;
             if (i < n) {
-                const uint64_t *rec = src + (uint64_t)i * RW;
-                a = rec[0];
-                c = rec[1];
-                if (IDX) d = (uint32_t)rec[2];
-                ovf = !ba_insert<IDX>(s_k0, s_k1, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
+                a = src[(uint64_t)i * RW];
+                c = src[(uint64_t)i * RW + 1];
+                if (IDX) d = (uint32_t)src[(uint64_t)i * RW + 2];
+                ovf = !ba_add<IDX>(s_key, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
             }
-            const uint64_t j = mrg_wave_append(&A.counters[CNT_OVF2], ovf);
-            if (ovf && j < A.ocap) {
-                A.ok0[j] = a; A.ok1[j] = c; A.ocnt[j] = 1u;
-                if (IDX) A.odoc[j] = d;
-            }
+            if (__any(ovf)) overflow(ovf, a, c, d, 1);
         }
     }
     __syncthreads();
     for (int i0 = 0; i0 < BA_CAP; i0 += BA_WG) {
         const int i = i0 + tid;
-        const bool full = s_k0[i] != MRG_EMPTY_K0;
+        const BaKey k = s_key[i];
+        const bool full = k.a != MRG_EMPTY_K0;
         const uint64_t j = mrg_wave_append(&A.counters[CNT_KEYS], full);
         if (full) {
-            const uint64_t a = s_k0[i], c = s_k1[i];
-            A.out.k0[j] = a;
-            A.out.k1[j] = c;
-            A.out.cnt[j] = s_cnt[i];
-            A.out.doc[j] = IDX ? s_doc[i] : MRG_EMPTY_DOC;
-            A.out.len[j] = mrg_short_len(a, c);
-            A.out.hoff[j] = MRG_NO_HEAP;
+            gk(A.out.k0)[j] = k.a;
+            gk(A.out.k1)[j] = k.b;
+            gk(A.out.cnt)[j] = s_cnt[i];
+            gk(A.out.doc)[j] = IDX ? s_doc[i] : MRG_EMPTY_DOC;
+            gk(A.out.len)[j] = mrg_short_len(k.a, k.b);
+            gk(A.out.hoff)[j] = MRG_NO_HEAP;
         }
     }
 }

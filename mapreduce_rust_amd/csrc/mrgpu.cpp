@@ -327,6 +327,7 @@ struct MapBufs {
 // Map-side records: per-bucket LDS aggregation of tail chunks + flushed map tables, exact overflow
 // through the HBM table, then the long keys.
 void bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap, LongItems li) {
+    if (nreg > 2048) raise(MRG_EINVAL, "internal: %u map workgroups exceed the aggregation's region table", nreg);
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     const bool idx = is_idx(c);
