@@ -193,21 +193,11 @@ struct LdsTable {
         return ((k.a ^ a) | (k.b ^ b)) == 0 && (!IDX || doc[s] == d);
     }
 
-    __device__ __forceinline__ bool insert(uint64_t a, uint64_t b, uint32_t d, uint32_t h) {
-        const uint32_t g = h & (NG - 1);
-        const uint32_t tg = ((h >> 16) & 0x7Fu) | 0x80u;
+    // Claim an empty slot of group g for the key, or find it in a slot filled meanwhile (per lane;
+    // only lanes whose key missed a group with empty slots get here -- rare once the table is full).
+    __device__ __forceinline__ bool claim(uint64_t a, uint64_t b, uint32_t d, uint32_t g, uint32_t tg, uint64_t tags) {
         const uint32_t rep32 = tg * 0x01010101u;
         const uint64_t rep = (uint64_t)rep32 | ((uint64_t)rep32 << 32);
-        uint64_t tags = tag[g];
-        uint64_t cand = zero_bytes(tags ^ rep);
-        while (cand) {
-            const uint32_t s = g * 8u + ((uint32_t)__builtin_ctzll(cand) >> 3);
-            if (matches(s, a, b, d)) {
-                atomicAdd(&cnt[s], 1u);
-                return true;
-            }
-            cand &= cand - 1u;
-        }
         uint64_t empty = zero_bytes(tags);
         while (empty) {
             const uint32_t j = (uint32_t)__builtin_ctzll(empty) >> 3;
@@ -234,6 +224,37 @@ struct LdsTable {
             empty = zero_bytes(tags);
         }
         return false;  // group full of other keys: miss
+    }
+
+    // One probe per lane of the wave, written without per-lane loops: the group's tag word, then the
+    // key of the FIRST tag-matching slot (a second candidate only where one exists: tags are 7 bits,
+    // so about 6% of probes see one).  A key seen only in a third candidate slot, or not at all, is
+    // a miss -- harmless: misses go to the tail and are summed exactly later.
+    __device__ __forceinline__ bool insert_wave(bool act, uint64_t a, uint64_t b, uint32_t d, uint32_t h) {
+        const uint32_t g = act ? (h & (NG - 1)) : 0u;
+        const uint32_t tg = ((h >> 16) & 0x7Fu) | 0x80u;
+        const uint32_t rep32 = tg * 0x01010101u;
+        const uint64_t rep = (uint64_t)rep32 | ((uint64_t)rep32 << 32);
+        const uint64_t tags = tag[g];
+        uint64_t cand = act ? zero_bytes(tags ^ rep) : 0ull;
+        const uint32_t s1 = g * 8u + min((uint32_t)__builtin_ctzll(cand | (1ull << 63)) >> 3, 7u);
+        bool hit = cand != 0 && matches(s1, a, b, d);
+        uint32_t s = s1;
+        cand &= cand - 1u;
+        const bool try2 = !hit && cand != 0;
+        if (__any(try2)) {
+            const uint32_t s2 = g * 8u + min((uint32_t)__builtin_ctzll(cand | (1ull << 63)) >> 3, 7u);
+            if (try2 && matches(s2, a, b, d)) {
+                hit = true;
+                s = s2;
+            }
+        }
+        atomicAdd(&cnt[s], hit ? 1u : 0u);  // every lane: no branch (s is a valid slot)
+        const bool need = act && !hit && zero_bytes(tags) != 0;
+        if (__any(need)) {
+            if (need) hit = claim(a, b, d, g, tg, tags);
+        }
+        return hit;
     }
 };
 
@@ -269,6 +290,46 @@ __device__ __forceinline__ bool walk_token(const RD &rd, uint64_t a, uint64_t do
     return true;
 }
 
+// Emission of the fast path's tokens (keys <= 16 bytes, never long), written to keep the wave on
+// one path: the hash for every lane, LDS adds of 0 or 1, branches only around the store and the
+// rare paths (region overflow).
+template <int CAP, bool IDX>
+__device__ __forceinline__ void emit_fast(const MapArgs &A, uint32_t abl, LdsTable<CAP, IDX> &table,
+                                          uint32_t *bcount, const uint32_t *bcap, const unsigned long long *bbase,
+                                          GAS uint64_t *pool, bool have, uint64_t tk0, uint64_t tk1, uint32_t docid) {
+    const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
+    const uint32_t h = key_hash(tk0, tk1, dkey, A.hash_bits);
+    const bool hit = table.insert_wave(have && !(abl & 2u), tk0, tk1, dkey, h);
+    const bool tail = have && !hit && !(abl & 1u);
+    const uint32_t b = bucket_of(h);
+    const uint32_t slot = atomicAdd(&bcount[b], tail ? 1u : 0u);
+    const bool ok = tail && slot < bcap[b];
+    if (ok) {
+        GAS uint64_t *dst = pool + (bbase[b] + slot) * (IDX ? 3u : 2u);
+        if (IDX) {
+            dst[0] = tk0;
+            dst[1] = tk1;
+            dst[2] = docid;
+        } else {
+            *reinterpret_cast<GAS u64x2 *>(dst) = u64x2{tk0, tk1};  // one 16-byte store
+        }
+    }
+    const bool ovf = tail && !ok;
+    if (__any(ovf)) {  // region full (rare): the bucket's shared overflow list
+        if (ovf) {
+            const uint32_t j = g_add(&A.onext[b], 1u);
+            if (j < A.ocap) {
+                GAS uint64_t *dst = gp(A.ovf) + ((uint64_t)b * A.ocap + j) * (IDX ? 3u : 2u);
+                dst[0] = tk0;
+                dst[1] = tk1;
+                if (IDX) dst[2] = docid;
+            } else {
+                g_add(&A.counters[CNT_OVF], 1ull);
+            }
+        }
+    }
+}
+
 // One round of token emission by a whole wave (all 64 lanes call it): LDS-table insert of short
 // keys; a miss is appended to its hash bucket's region of this workgroup (an LDS counter per
 // bucket, no HBM atomics).  Long keys become long-token records.
@@ -282,7 +343,10 @@ __device__ __forceinline__ void emit(const MapArgs &A, LdsTable<CAP, IDX> &table
     const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
     if (have && !is_long) {
         h = key_hash(tk0, tk1, dkey, A.hash_bits);
-        tail = (A.ablate & 2u) ? true : !table.insert(tk0, tk1, dkey, h);
+    }
+    {
+        const bool act = have && !is_long && !(A.ablate & 2u);
+        tail = (have && !is_long) && !table.insert_wave(act, tk0, tk1, dkey, h);
     }
     if (tail && !(A.ablate & 1u)) {
         const uint32_t b = bucket_of(h);
@@ -442,6 +506,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     }
     LdsTable<CAP, IDX> table{s_key, s_cnt, s_doc, s_tag};
     uint32_t my_tokens = 0;
+    // uniform job parameters used in the hot loop, read once
+    const uint32_t abl = A.ablate;
+    GAS uint64_t *const pool = gp(A.pool);
     uint8_t *win = s_win[wv];
     const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
     uint64_t *mp = s_mp[wv];
@@ -470,7 +537,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     struct Blk {
         uint4 v0, v1, e;
     };
-    auto load_blk = [&](const BlkInfo &b, Blk &X) {
+    BlkInfo first_blk{};  // ablate & 8 (timing only): every block re-reads the wave's first block
+    auto load_blk = [&](const BlkInfo &b0, Blk &X) {
+        const BlkInfo &b = (A.ablate & 8u) ? first_blk : b0;  // a real block: its own base and bounds
         const GAS uint8_t *src = gp(A.in) + (b.Ab - (uint64_t)BEHIND);
         auto ld = [&](uint32_t idx) -> uint4 {
             const u32x4 t = *reinterpret_cast<const GAS u32x4 *>(src + 16u * min(max(idx, b.v0), b.v1 - 1u));
@@ -580,9 +649,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 st &= st - 1u;
                 queue[pos++] = (uint16_t)(l16 + kb);
             }
-            const uint32_t total = (A.ablate & 4u) ? 0u : lane_u32(incl, 63);
+            const uint32_t total = (abl & 4u) ? 0u : lane_u32(incl, 63);
             uint32_t nslow = 0;
-            my_tokens += (A.ablate & 4u) ? cnt : 0u;
+            my_tokens += (abl & 4u) ? cnt : 0u;
             wave_sync_lds();
 
             // tokens of the queue, one per lane per round (queue, masks and window are read-only now)
@@ -602,36 +671,46 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 const uint32_t span = last - first + 1u;
                 const bool fast = act && ended && w != 0u && span <= 16u;
                 const bool slow = act && (!ended || (w != 0u && span > 16u));
-                // key bytes [s + first, + span) of the window, big-endian packed, zero padded
+                // deleted bytes inside the token ("don't"): one 1-byte gap is folded into the selectors
+                // below (key bytes from the gap on come from one window byte later); tokens with more
+                // gaps squeeze them out afterwards
+                const uint32_t gaps = fast ? (~(w >> first) & ((1u << span) - 1u)) : 0u;
+                const bool one_gap = gaps != 0u && (gaps & (gaps - 1u)) == 0u;
+                const uint32_t ga = one_gap ? (uint32_t)__builtin_ctz(gaps) : 16u;
+                uint32_t tlen = one_gap ? span - 1u : span;
+                // key bytes of the window from s + first, big-endian packed, zero padded: output byte p
+                // of word j is key byte 4j + 3 - p (selector r + 3 - p [+ 1 past the gap], 0x0C = zero)
                 const uint32_t off = (uint32_t)BEHIND + s + first;
                 const uint32_t dw = off >> 2, r = off & 3u;
                 const uint32_t d0 = win32[dw], d1 = win32[dw + 1], d2 = win32[dw + 2], d3 = win32[dw + 3],
                                d4 = win32[dw + 4];
-                const uint32_t *zm = s_zm[fast ? span : 0u];
+                const uint32_t *zm = s_zm[fast ? tlen : 0u];
+                const uint32_t *gm = s_zm[ga];
                 const uint32_t bsel = 0x00010203u + r * 0x01010101u;
-                const uint32_t o0 = __builtin_amdgcn_perm(d1, d0, (bsel & ~zm[0]) | (0x0C0C0C0Cu & zm[0]));
-                const uint32_t o1 = __builtin_amdgcn_perm(d2, d1, (bsel & ~zm[1]) | (0x0C0C0C0Cu & zm[1]));
-                const uint32_t o2 = __builtin_amdgcn_perm(d3, d2, (bsel & ~zm[2]) | (0x0C0C0C0Cu & zm[2]));
-                const uint32_t o3 = __builtin_amdgcn_perm(d4, d3, (bsel & ~zm[3]) | (0x0C0C0C0Cu & zm[3]));
+                auto sel = [&](int j) {
+                    return ((bsel + (gm[j] & 0x01010101u)) & ~zm[j]) | (0x0C0C0C0Cu & zm[j]);
+                };
+                const uint32_t o0 = __builtin_amdgcn_perm(d1, d0, sel(0));
+                const uint32_t o1 = __builtin_amdgcn_perm(d2, d1, sel(1));
+                const uint32_t o2 = __builtin_amdgcn_perm(d3, d2, sel(2));
+                const uint32_t o3 = __builtin_amdgcn_perm(d4, d3, sel(3));
                 uint64_t tk0 = ((uint64_t)o0 << 32) | o1, tk1 = ((uint64_t)o2 << 32) | o3;
-                uint32_t tlen = span;
-                // deleted bytes inside the token ("don't"): squeeze out each gap of the \w mask
-                uint32_t gaps = fast ? (~(w >> first) & ((1u << span) - 1u)) : 0u;
-                if (__any(gaps != 0u)) {
-                    while (gaps) {
-                        const uint32_t ga = (uint32_t)__builtin_ctz(gaps);           // gap start (key byte)
-                        const uint32_t gl = (uint32_t)__builtin_ctz(~(gaps >> ga));  // gap length
-                        const uint32_t sh = 8u * gl;                                 // 8..120 bits
-                        // shifted = (tk0:tk1) << sh; keep the top ga bytes, take the rest from shifted
+                uint32_t mgaps = one_gap ? 0u : gaps;
+                if (__any(mgaps != 0u)) {
+                    while (mgaps) {
+                        const uint32_t ga2 = (uint32_t)__builtin_ctz(mgaps);          // gap start (key byte)
+                        const uint32_t gl = (uint32_t)__builtin_ctz(~(mgaps >> ga2)); // gap length
+                        const uint32_t sh = 8u * gl;                                  // 8..120 bits
+                        // shifted = (tk0:tk1) << sh; keep the top ga2 bytes, take the rest from shifted
                         uint64_t s0v, s1v;
                         if (sh >= 64u) { s0v = tk1 << (sh - 64u); s1v = 0; }
                         else { s0v = (tk0 << sh) | (tk1 >> (64u - sh)); s1v = tk1 << sh; }
-                        const uint32_t kb = 8u * ga;                                 // kept bits
+                        const uint32_t kb = 8u * ga2;                                 // kept bits
                         const uint64_t k0m = kb >= 64u ? ~0ull : (kb ? ~0ull << (64u - kb) : 0ull);
                         const uint64_t k1m = kb <= 64u ? 0ull : ~0ull << (128u - kb);
                         tk0 = (tk0 & k0m) | (s0v & ~k0m);
                         tk1 = (tk1 & k1m) | (s1v & ~k1m);
-                        gaps = (gaps >> (ga + gl)) << ga;
+                        mgaps = (mgaps >> (ga2 + gl)) << ga2;
                         tlen -= gl;
                     }
                 }
@@ -647,7 +726,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                     nslow += (uint32_t)__builtin_popcountll(sm);
                 }
                 my_tokens += fast ? 1u : 0u;
-                emit(A, table, s_bcount, s_bcap, s_bbase, fast, tk0, tk1, tlen, At + s, n, docid);
+                emit_fast(A, abl, table, s_bcount, s_bcap, s_bbase, pool, fast, tk0, tk1, docid);
             }
             // deferred slow tokens: the exact per-codepoint walker, one token per lane (forward
             // reads only: the staged bytes are [At, whi))
@@ -696,6 +775,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     };
     if (c < nb) {
         IA = locate_blk(A, c, dcur);
+        first_blk = IA;
         load_blk(IA, XA);
     }
     while (c < nb) {
