@@ -230,7 +230,8 @@ struct LdsTable {
     // key of the FIRST tag-matching slot (a second candidate only where one exists: tags are 7 bits,
     // so about 6% of probes see one).  A key seen only in a third candidate slot, or not at all, is
     // a miss -- harmless: misses go to the tail and are summed exactly later.
-    __device__ __forceinline__ bool insert_wave(bool act, uint64_t a, uint64_t b, uint32_t d, uint32_t h) {
+    __device__ __forceinline__ bool insert_wave(bool act, uint64_t a, uint64_t b, uint32_t d, uint32_t h,
+                                                uint32_t abl = 0) {
         const uint32_t g = act ? (h & (NG - 1)) : 0u;
         const uint32_t tg = ((h >> 16) & 0x7Fu) | 0x80u;
         const uint32_t rep32 = tg * 0x01010101u;
@@ -249,7 +250,7 @@ struct LdsTable {
                 s = s2;
             }
         }
-        atomicAdd(&cnt[s], hit ? 1u : 0u);  // every lane: no branch (s is a valid slot)
+        if (!(abl & 16u)) atomicAdd(&cnt[s], hit ? 1u : 0u);  // every lane: no branch (s is a valid slot)
         const bool need = act && !hit && zero_bytes(tags) != 0;
         if (__any(need)) {
             if (need) hit = claim(a, b, d, g, tg, tags);
@@ -294,12 +295,12 @@ __device__ __forceinline__ bool walk_token(const RD &rd, uint64_t a, uint64_t do
 // one path: the hash for every lane, LDS adds of 0 or 1, branches only around the store and the
 // rare paths (region overflow).
 template <int CAP, bool IDX>
-__device__ __forceinline__ void emit_fast(const MapArgs &A, uint32_t abl, LdsTable<CAP, IDX> &table,
+__device__ __forceinline__ void emit_fast(const MapArgs &A, uint32_t abl, uint32_t hbits, LdsTable<CAP, IDX> &table,
                                           uint32_t *bcount, const uint32_t *bcap, const unsigned long long *bbase,
                                           GAS uint64_t *pool, bool have, uint64_t tk0, uint64_t tk1, uint32_t docid) {
     const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
-    const uint32_t h = key_hash(tk0, tk1, dkey, A.hash_bits);
-    const bool hit = table.insert_wave(have && !(abl & 2u), tk0, tk1, dkey, h);
+    const uint32_t h = key_hash(tk0, tk1, dkey, hbits);
+    const bool hit = table.insert_wave(have && !(abl & 2u), tk0, tk1, dkey, h, abl);
     const bool tail = have && !hit && !(abl & 1u);
     const uint32_t b = bucket_of(h);
     const uint32_t slot = atomicAdd(&bcount[b], tail ? 1u : 0u);
@@ -508,6 +509,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     uint32_t my_tokens = 0;
     // uniform job parameters used in the hot loop, read once
     const uint32_t abl = A.ablate;
+    const uint32_t hbits = A.hash_bits;
     GAS uint64_t *const pool = gp(A.pool);
     uint8_t *win = s_win[wv];
     const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
@@ -726,7 +728,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                     nslow += (uint32_t)__builtin_popcountll(sm);
                 }
                 my_tokens += fast ? 1u : 0u;
-                emit_fast(A, abl, table, s_bcount, s_bcap, s_bbase, pool, fast, tk0, tk1, docid);
+                emit_fast(A, abl, hbits, table, s_bcount, s_bcap, s_bbase, pool, fast, tk0, tk1, docid);
             }
             // deferred slow tokens: the exact per-codepoint walker, one token per lane (forward
             // reads only: the staged bytes are [At, whi))

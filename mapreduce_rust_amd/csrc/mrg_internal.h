@@ -74,7 +74,8 @@ struct MapArgs {
     uint32_t ablate;             // perf diagnostics only (env MRG_ABLATE; results are WRONG when set):
                                  // 1 = no tail-record stores, 2 = no LDS-table probe (all tokens
                                  // become tail records), 4 = no per-token work after the queue,
-                                 // 8 = every block loads its document's first block (L2-resident)
+                                 // 8 = every block loads its document's first block (L2-resident),
+                                 // 16 = no LDS count add on table hits
 };
 
 // A set of keys with counts (SoA).  len > 16 keys have their bytes at heap[hoff .. hoff+len).
