@@ -134,6 +134,18 @@ __device__ __forceinline__ BlkInfo locate_blk(const MapArgs &A, uint64_t c, uint
     return b;
 }
 
+// Document of block c: the d with chunk_base[d] <= c < chunk_base[d + 1] (binary search; scalar).
+__device__ __forceinline__ uint32_t find_doc(const MapArgs &A, uint64_t c) {
+    const CAS uint64_t *cb = cp(A.chunk_base);
+    uint32_t lo = 0, hi = A.n_docs;  // cb[lo] <= c < cb[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cb[mid] <= c) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
 // 1 KiB tile j of a block, with its staged window [At - 16, At + 1024 + 64) clipped to the document.
 __device__ __forceinline__ TileInfo sub_tile(const BlkInfo &b, uint32_t j) {
     TileInfo t;
@@ -331,6 +343,82 @@ __device__ __forceinline__ void emit_fast(const MapArgs &A, uint32_t abl, uint32
     }
 }
 
+// Two tokens per lane (a and b) through the LDS table in one instruction stream: the tag reads,
+// key reads, count adds and tail-cursor adds of both are issued back to back, so every LDS round
+// trip is paid once for two tokens.  Same semantics as emit_fast() applied to a, then b.
+template <int CAP, bool IDX>
+__device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint32_t hbits, LdsTable<CAP, IDX> &T,
+                                           uint32_t *bcount, const uint32_t *bcap, const unsigned long long *bbase,
+                                           GAS uint64_t *pool, bool ha, uint64_t a0, uint64_t a1, bool hb,
+                                           uint64_t b0, uint64_t b1, uint32_t docid) {
+    constexpr uint32_t NG = LdsTable<CAP, IDX>::NG;
+    const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
+    const uint32_t hA = key_hash(a0, a1, dkey, hbits), hB = key_hash(b0, b1, dkey, hbits);
+    const bool actA = ha && !(abl & 2u), actB = hb && !(abl & 2u);
+    const uint32_t gA = actA ? (hA & (NG - 1)) : 0u, gB = actB ? (hB & (NG - 1)) : 0u;
+    const uint32_t tgA = ((hA >> 16) & 0x7Fu) | 0x80u, tgB = ((hB >> 16) & 0x7Fu) | 0x80u;
+    const uint32_t bA = bucket_of(hA), bB = bucket_of(hB);
+    const uint32_t capA = bcap[bA], capB = bcap[bB];  // independent of the probe: issued early
+    const uint64_t tagsA = T.tag[gA], tagsB = T.tag[gB];
+    auto rep = [](uint32_t tg) {
+        const uint32_t r32 = tg * 0x01010101u;
+        return (uint64_t)r32 | ((uint64_t)r32 << 32);
+    };
+    uint64_t cA = actA ? zero_bytes(tagsA ^ rep(tgA)) : 0ull, cB = actB ? zero_bytes(tagsB ^ rep(tgB)) : 0ull;
+    auto slot_of = [](uint32_t g, uint64_t c) { return g * 8u + min((uint32_t)__builtin_ctzll(c | (1ull << 63)) >> 3, 7u); };
+    uint32_t sA = slot_of(gA, cA), sB = slot_of(gB, cB);
+    const KeyPair kA = T.key[sA], kB = T.key[sB];
+    bool hitA = cA != 0 && ((kA.a ^ a0) | (kA.b ^ a1)) == 0 && (!IDX || T.doc[sA] == dkey);
+    bool hitB = cB != 0 && ((kB.a ^ b0) | (kB.b ^ b1)) == 0 && (!IDX || T.doc[sB] == dkey);
+    cA &= cA - 1u;
+    cB &= cB - 1u;
+    const bool t2A = !hitA && cA != 0, t2B = !hitB && cB != 0;
+    if (__any(t2A || t2B)) {
+        const uint32_t s2A = slot_of(gA, cA), s2B = slot_of(gB, cB);
+        if (t2A && T.matches(s2A, a0, a1, dkey)) { hitA = true; sA = s2A; }
+        if (t2B && T.matches(s2B, b0, b1, dkey)) { hitB = true; sB = s2B; }
+    }
+    if (!(abl & 16u)) {
+        atomicAdd(&T.cnt[sA], hitA ? 1u : 0u);  // every lane: no branch (the slot is valid)
+        atomicAdd(&T.cnt[sB], hitB ? 1u : 0u);
+    }
+    const bool nA = actA && !hitA && zero_bytes(tagsA) != 0, nB = actB && !hitB && zero_bytes(tagsB) != 0;
+    if (__any(nA || nB)) {
+        if (nA) hitA = T.claim(a0, a1, dkey, gA, tgA, tagsA);
+        if (nB) hitB = T.claim(b0, b1, dkey, gB, tgB, tagsB);
+    }
+    const bool tA = ha && !hitA && !(abl & 1u), tB = hb && !hitB && !(abl & 1u);
+    const uint32_t slA = atomicAdd(&bcount[bA], tA ? 1u : 0u);
+    const uint32_t slB = atomicAdd(&bcount[bB], tB ? 1u : 0u);
+    const bool okA = tA && slA < capA, okB = tB && slB < capB;
+    if (okA) {
+        GAS uint64_t *dst = pool + (bbase[bA] + slA) * (IDX ? 3u : 2u);
+        if (IDX) { dst[0] = a0; dst[1] = a1; dst[2] = docid; }
+        else *reinterpret_cast<GAS u64x2 *>(dst) = u64x2{a0, a1};
+    }
+    if (okB) {
+        GAS uint64_t *dst = pool + (bbase[bB] + slB) * (IDX ? 3u : 2u);
+        if (IDX) { dst[0] = b0; dst[1] = b1; dst[2] = docid; }
+        else *reinterpret_cast<GAS u64x2 *>(dst) = u64x2{b0, b1};
+    }
+    const bool oA = tA && !okA, oB = tB && !okB;
+    if (__any(oA || oB)) {  // region full (rare): the bucket's shared overflow list
+        auto spill = [&](uint32_t b, uint64_t k0, uint64_t k1) {
+            const uint32_t j = g_add(&A.onext[b], 1u);
+            if (j < A.ocap) {
+                GAS uint64_t *dst = gp(A.ovf) + ((uint64_t)b * A.ocap + j) * (IDX ? 3u : 2u);
+                dst[0] = k0;
+                dst[1] = k1;
+                if (IDX) dst[2] = docid;
+            } else {
+                g_add(&A.counters[CNT_OVF], 1ull);
+            }
+        };
+        if (oA) spill(bA, a0, a1);
+        if (oB) spill(bB, b0, b1);
+    }
+}
+
 // One round of token emission by a whole wave (all 64 lanes call it): LDS-table insert of short
 // keys; a miss is appended to its hash bucket's region of this workgroup (an LDS counter per
 // bucket, no HBM atomics).  Long keys become long-token records.
@@ -476,6 +564,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ uint32_t s_bcap[MRG_NBUCKET];
     __shared__ unsigned long long s_bbase[MRG_NBUCKET];  // first pool record of (bucket, this WG)
     __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
+    __shared__ uint32_t s_next, s_ngen;                  // next block of the workgroup's share; list length
     static_assert(sizeof(s_q) >= CAP * sizeof(uint16_t), "flush ranks reuse the queues");
 
     const int tid = threadIdx.x;
@@ -493,6 +582,10 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const uint32_t cap = gp(A.bcap)[b];
         s_bcap[b] = cap;
         s_bbase[b] = gp(A.rbase)[b] + (uint64_t)blockIdx.x * cap;
+    }
+    if (tid == 0) {
+        s_next = 0;
+        s_ngen = 0;
     }
     if (tid < 128) {
         const uint32_t c = mrg_uclass((uint32_t)tid);
@@ -552,18 +645,28 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         X.e = ld(lane == 0 ? 0u : 128u + (uint32_t)lane);
     };
 
-    // non-ASCII tiles: bit k of this wave's bitmap = its k-th 1 KiB tile (one 64-bit word per 64)
-    GAS uint64_t *gbits = gp(A.gbits) + (uint64_t)(blockIdx.x * NW + wv) * A.kwords;
-    uint64_t gword = 0;
-    uint32_t kt = 0;  // this wave's tile counter (NSUB per block)
+    // Work split: workgroup w owns blocks [wlo_b, whi_b) (equal shares); its waves take the next
+    // block from an LDS counter, so a wave that the SIMD's age-ordered issue leaves behind simply
+    // takes fewer blocks (a static per-wave split left the youngest waves finishing last).
+    const uint64_t nb = A.n_chunks;  // blocks of the job
+    const uint64_t wlo_b = nb * blockIdx.x / gridDim.x, whi_b = nb * (blockIdx.x + 1) / gridDim.x;
+    // non-ASCII tiles: appended to this workgroup's list (tile index relative to wlo_b * NSUB),
+    // processed after the main loop by all 16 waves
+    GAS uint32_t *glist = gp(A.gbits) + (uint64_t)blockIdx.x * A.kwords;
 
     // one block: masks of its 1 KiB tiles up front, then tile by tile through the
     // wave's LDS window
-    auto process_blk = [&](const BlkInfo &I, const Blk &X) {
-        if (kt && (kt & 63u) == 0) {
-            if (lane == 0) gbits[(kt >> 6) - 1] = gword;
-            gword = 0;
-        }
+    // phase clocks (MRG_PROF only; wave-uniform): 0 wait for the block's loads, 1 classify,
+    // 2 stage + scan + queue, 3 token rounds, 4 slow tokens, 5 non-ASCII tiles, 6 flush
+    const bool P = A.prof != nullptr;
+    uint64_t pacc[7] = {0, 0, 0, 0, 0, 0, 0}, tl = P ? clock64() : 0;
+#define MRG_PT(i)                          \
+    if (P) {                               \
+        const uint64_t t_ = clock64();     \
+        pacc[i] += t_ - tl;                \
+        tl = t_;                           \
+    }
+    auto process_blk = [&](const BlkInfo &I, const Blk &X, uint64_t cblk) {
         const uint64_t Ab = I.Ab, doc_lo = I.doc_lo, doc_hi = I.doc_hi;
         const uint32_t docid = I.docid;
         // classify segment [B, B + 16) (relative to Ab) into W16 | S16 << 16; bytes outside the
@@ -600,12 +703,12 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         // class of the byte before the block (lane 0's e, byte 15)
         const uint32_t prev_blk =
             Ab > doc_lo ? (uint32_t)(s_lut[(lane_u32(X.e.w, 0) >> 24) & 0x7Fu] >> 8) : 1u;
+        MRG_PT(1);
 
 #pragma unroll 1
         for (uint32_t j = 0; j < NSUB; ++j) {
             const uint64_t At = Ab + (uint64_t)j * TILE;
             if (At >= doc_hi) break;
-            const uint32_t tj = kt + j;
             const bool last = j == NSUB - 1;
             const uint4 x = j == 0 ? X.v0 : X.v1;
             const uint4 xh = j == 0 ? X.v1 : X.e;  // halo source
@@ -618,7 +721,10 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const uint32_t hl = last ? 1u : 0u;  // lane holding the first halo segment
             const bool nonascii = nx || ((uint32_t)lane == hl && nh) || ((uint32_t)lane == (j ? 63u : 0u) && np);
             if (__any(nonascii)) {  // recorded; processed after the main loop
-                gword |= 1ull << (tj & 63u);
+                if (lane == 0) {
+                    const uint32_t k = atomicAdd(&s_ngen, 1u);
+                    glist[k] = (uint32_t)((cblk - wlo_b) * NSUB + j);
+                }
                 continue;
             }
             const uint64_t t1 = min(At + (uint64_t)TILE, doc_hi);
@@ -652,15 +758,17 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 queue[pos++] = (uint16_t)(l16 + kb);
             }
             const uint32_t total = (abl & 4u) ? 0u : lane_u32(incl, 63);
+            MRG_PT(2);
             uint32_t nslow = 0;
             my_tokens += (abl & 4u) ? cnt : 0u;
             wave_sync_lds();
 
-            // tokens of the queue, one per lane per round (queue, masks and window are read-only now)
-            for (uint32_t base = 0; base < total; base += 64) {
-                const uint32_t q = base + (uint32_t)lane;
+            // tokens of the queue, TWO per lane per round (entries q and q + 64: two independent LDS
+            // dependency chains in one instruction stream, so each wait covers both); the queue, masks
+            // and window are read-only now
+            auto extract = [&](uint32_t q, bool &fast, bool &slow, uint32_t &s, uint64_t &tk0, uint64_t &tk1) {
                 const bool act = q < total;
-                const uint32_t s = act ? (uint32_t)queue[q] : 0u;
+                s = act ? (uint32_t)queue[q] : 0u;
                 const uint64_t mw = mp[s >> 4];
                 const uint32_t Wp = (uint32_t)mw, Sp = (uint32_t)(mw >> 32);
                 const uint32_t i = s & 15u;
@@ -671,8 +779,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 const uint32_t first = (uint32_t)__builtin_ctz(w | 0x80000000u);
                 const uint32_t last = 31u - (uint32_t)__builtin_clz(w | 1u);
                 const uint32_t span = last - first + 1u;
-                const bool fast = act && ended && w != 0u && span <= 16u;
-                const bool slow = act && (!ended || (w != 0u && span > 16u));
+                fast = act && ended && w != 0u && span <= 16u;
+                slow = act && (!ended || (w != 0u && span > 16u));
                 // deleted bytes inside the token ("don't"): one 1-byte gap is folded into the selectors
                 // below (key bytes from the gap on come from one window byte later); tokens with more
                 // gaps squeeze them out afterwards
@@ -696,42 +804,56 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 const uint32_t o1 = __builtin_amdgcn_perm(d2, d1, sel(1));
                 const uint32_t o2 = __builtin_amdgcn_perm(d3, d2, sel(2));
                 const uint32_t o3 = __builtin_amdgcn_perm(d4, d3, sel(3));
-                uint64_t tk0 = ((uint64_t)o0 << 32) | o1, tk1 = ((uint64_t)o2 << 32) | o3;
-                uint32_t mgaps = one_gap ? 0u : gaps;
-                if (__any(mgaps != 0u)) {
-                    while (mgaps) {
-                        const uint32_t ga2 = (uint32_t)__builtin_ctz(mgaps);          // gap start (key byte)
-                        const uint32_t gl = (uint32_t)__builtin_ctz(~(mgaps >> ga2)); // gap length
-                        const uint32_t sh = 8u * gl;                                  // 8..120 bits
-                        // shifted = (tk0:tk1) << sh; keep the top ga2 bytes, take the rest from shifted
-                        uint64_t s0v, s1v;
-                        if (sh >= 64u) { s0v = tk1 << (sh - 64u); s1v = 0; }
-                        else { s0v = (tk0 << sh) | (tk1 >> (64u - sh)); s1v = tk1 << sh; }
-                        const uint32_t kb = 8u * ga2;                                 // kept bits
-                        const uint64_t k0m = kb >= 64u ? ~0ull : (kb ? ~0ull << (64u - kb) : 0ull);
-                        const uint64_t k1m = kb <= 64u ? 0ull : ~0ull << (128u - kb);
-                        tk0 = (tk0 & k0m) | (s0v & ~k0m);
-                        tk1 = (tk1 & k1m) | (s1v & ~k1m);
-                        mgaps = (mgaps >> (ga2 + gl)) << ga2;
-                        tlen -= gl;
-                    }
+                tk0 = ((uint64_t)o0 << 32) | o1;
+                tk1 = ((uint64_t)o2 << 32) | o3;
+                return one_gap ? 0u : gaps;  // gaps still to squeeze out
+            };
+            // squeeze out the remaining gaps (more than one deleted run inside the token; rare)
+            auto squeeze = [](uint32_t mgaps, uint64_t &tk0, uint64_t &tk1) {
+                while (mgaps) {
+                    const uint32_t ga2 = (uint32_t)__builtin_ctz(mgaps);          // gap start (key byte)
+                    const uint32_t gl = (uint32_t)__builtin_ctz(~(mgaps >> ga2)); // gap length
+                    const uint32_t sh = 8u * gl;                                  // 8..120 bits
+                    // shifted = (tk0:tk1) << sh; keep the top ga2 bytes, take the rest from shifted
+                    uint64_t s0v, s1v;
+                    if (sh >= 64u) { s0v = tk1 << (sh - 64u); s1v = 0; }
+                    else { s0v = (tk0 << sh) | (tk1 >> (64u - sh)); s1v = tk1 << sh; }
+                    const uint32_t kb = 8u * ga2;                                 // kept bits
+                    const uint64_t k0m = kb >= 64u ? ~0ull : (kb ? ~0ull << (64u - kb) : 0ull);
+                    const uint64_t k1m = kb <= 64u ? 0ull : ~0ull << (128u - kb);
+                    tk0 = (tk0 & k0m) | (s0v & ~k0m);
+                    tk1 = (tk1 & k1m) | (s1v & ~k1m);
+                    mgaps = (mgaps >> (ga2 + gl)) << ga2;
+                }
+            };
+            for (uint32_t base = 0; base < total; base += 128) {
+                bool fa, sa, fb, sb;
+                uint32_t sA, sB;
+                uint64_t a0, a1, b0, b1;
+                uint32_t ga = extract(base + (uint32_t)lane, fa, sa, sA, a0, a1);
+                uint32_t gb = extract(base + 64u + (uint32_t)lane, fb, sb, sB, b0, b1);
+                if (__any((ga | gb) != 0u)) {
+                    squeeze(ga, a0, a1);
+                    squeeze(gb, b0, b1);
                 }
                 // slow tokens (past the 2-segment window, or > 16 raw key bytes) are deferred: their
-                // starts go to the consumed front of the queue (every lane has read its own entry,
-                // and nslow + rank <= base + lane)
-                const uint64_t sm = __ballot(slow);
-                if (sm) {
-                    if (slow)
-                        queue[nslow + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u))] =
-                            (uint16_t)s;
-                    nslow += (uint32_t)__builtin_popcountll(sm);
+                // starts go to the consumed front of the queue (every lane has read both its entries,
+                // and the deferred count never exceeds the entries read so far)
+                const uint64_t ma = __ballot(sa), mb = __ballot(sb);
+                if (ma | mb) {
+                    const uint32_t ra = __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, 0u));
+                    const uint32_t rb = __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+                    const uint32_t na = (uint32_t)__builtin_popcountll(ma);
+                    if (sa) queue[nslow + ra] = (uint16_t)sA;
+                    if (sb) queue[nslow + na + rb] = (uint16_t)sB;
+                    nslow += na + (uint32_t)__builtin_popcountll(mb);
                 }
-                my_tokens += fast ? 1u : 0u;
-                emit_fast(A, abl, hbits, table, s_bcount, s_bcap, s_bbase, pool, fast, tk0, tk1, docid);
+                my_tokens += (fa ? 1u : 0u) + (fb ? 1u : 0u);
+                emit_fast2(A, abl, hbits, table, s_bcount, s_bcap, s_bbase, pool, fa, a0, a1, fb, b0, b1, docid);
             }
             // deferred slow tokens: the exact per-codepoint walker, one token per lane (forward
             // reads only: the staged bytes are [At, whi))
+            MRG_PT(3);
             if (nslow) {
                 wave_sync_lds();
                 auto rd = [&](uint64_t a) -> uint32_t {
@@ -756,16 +878,19 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 }
             }
         }
-        kt += NSUB;
+        MRG_PT(4);
     };
 
     // Main loop: two register sets, A and B.  Block c's loads were issued one block earlier; the
     // next block's loads go out before c is processed, so exactly five loads are younger than c's
     // when its data is first used.  Past the end, the "next" block is a reload of the current one.
-    const uint64_t stride = (uint64_t)gridDim.x * NW;
-    const uint64_t nb = A.n_chunks;  // blocks of the job
-    uint64_t c = (uint64_t)blockIdx.x * NW + wv;
-    uint32_t dcur = 0;
+    auto grab = [&]() -> uint64_t {
+        uint32_t r = 0;
+        if (lane == 0) r = atomicAdd(&s_next, 1u);
+        return wlo_b + (uint64_t)first_u32(r);
+    };
+    uint64_t c = grab();
+    uint32_t dcur = c < whi_b ? find_doc(A, c) : 0u;
     Blk XA, XB;
     BlkInfo IA{}, IB{};
     // Make a block's registers available HERE (the compiler waits for its loads at this point, when
@@ -775,40 +900,40 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         asm volatile("" : "+v"(X.v0.x), "+v"(X.v0.y), "+v"(X.v0.z), "+v"(X.v0.w), "+v"(X.v1.x), "+v"(X.v1.y),
                      "+v"(X.v1.z), "+v"(X.v1.w), "+v"(X.e.x), "+v"(X.e.y), "+v"(X.e.z), "+v"(X.e.w));
     };
-    if (c < nb) {
+    if (c < whi_b) {
         IA = locate_blk(A, c, dcur);
         first_blk = IA;
         load_blk(IA, XA);
     }
-    while (c < nb) {
-        const uint64_t cB = c + stride;
-        IB = cB < nb ? locate_blk(A, cB, dcur) : IA;
+    while (c < whi_b) {
+        const uint64_t cB = grab();
+        IB = cB < whi_b ? locate_blk(A, cB, dcur) : IA;
         settle(XA);
+        MRG_PT(0);
         load_blk(IB, XB);
-        process_blk(IA, XA);
+        process_blk(IA, XA, c);
         c = cB;
-        if (c >= nb) break;
-        const uint64_t cA = c + stride;
-        IA = cA < nb ? locate_blk(A, cA, dcur) : IB;
+        if (c >= whi_b) break;
+        const uint64_t cA = grab();
+        IA = cA < whi_b ? locate_blk(A, cA, dcur) : IB;
         settle(XB);
+        MRG_PT(0);
         load_blk(IA, XA);
-        process_blk(IB, XB);
+        process_blk(IB, XB, c);
         c = cA;
     }
-    if (lane == 0 && kt) gbits[(kt - 1) >> 6] = gword;  // the last (partial) word
 
+    MRG_PT(4);
     // ---- non-ASCII tiles recorded by the main loop
+    __syncthreads();  // the list is complete (global writes of this workgroup, then the barrier)
     {
-        const uint32_t nk = kt;
-        uint32_t dgen = 0;
-        const uint64_t c0 = (uint64_t)blockIdx.x * NW + wv;
-        for (uint32_t wi = 0; wi * 64u < nk; ++wi) {
-            const uint64_t gw = gbits[wi];
-            uint64_t bits = (uint64_t)first_u32((uint32_t)gw) | ((uint64_t)first_u32((uint32_t)(gw >> 32)) << 32);
-            while (bits) {
-                const uint32_t kk = wi * 64u + (uint32_t)__builtin_ctzll(bits);
-                bits &= bits - 1u;
-                const BlkInfo b = locate_blk(A, c0 + (uint64_t)(kk / NSUB) * stride, dgen);
+        const uint32_t ng = s_ngen;
+        for (uint32_t i = (uint32_t)wv; i < ng; i += NW) {
+            {
+                const uint32_t kk = first_u32(glist[i]);
+                const uint64_t cb = wlo_b + kk / NSUB;
+                uint32_t dgen = find_doc(A, cb);
+                const BlkInfo b = locate_blk(A, cb, dgen);
                 const TileInfo T = sub_tile(b, kk % NSUB);
                 uint4 x0, x1;
                 load(T, x0, x1);
@@ -822,6 +947,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         }
     }
 
+    MRG_PT(5);
     // ---- flush the LDS table into this workgroup's region, sorted by bucket
     __syncthreads();
     uint16_t *s_rank = &s_q[0][0];
@@ -865,14 +991,18 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         gp(A.fcnt)[pos2] = s_cnt[i];
         if (IDX) gp(A.fdoc)[pos2] = d;
     }
-    uint32_t t = my_tokens, tl = my_tail;
+    uint32_t t = my_tokens, ttl = my_tail;
     for (int off = 32; off > 0; off >>= 1) {
         t += __shfl_down(t, off);
-        tl += __shfl_down(tl, off);
+        ttl += __shfl_down(ttl, off);
     }
     if (lane == 0) {
         g_add(&A.counters[CNT_TOKENS], (unsigned long long)t);
-        g_add(&A.counters[CNT_REC], (unsigned long long)tl);
+        g_add(&A.counters[CNT_REC], (unsigned long long)ttl);
+    }
+    MRG_PT(6);
+    if (P && lane == 0) {
+        for (int i = 0; i < 7; ++i) g_add(&A.prof[i], (unsigned long long)pacc[i]);
     }
 }
 

@@ -65,10 +65,10 @@ struct MapArgs {
     uint64_t *lstart;
     uint32_t *llen, *ldoc;
     uint64_t lcap;
-    // non-ASCII tiles, recorded by the main loop and processed after it: wave w's k-th tile is bit
-    // k % 64 of gbits[w * kwords + k / 64]
-    uint64_t *gbits;
-    uint32_t kwords;
+    // non-ASCII tiles, recorded by the main loop and processed after it: workgroup g appends the
+    // index of each such tile (relative to its first block's first tile) to gbits[g * kwords ..)
+    uint32_t *gbits;
+    uint32_t kwords;             // list capacity per workgroup (tiles of its share)
     unsigned long long *counters;
     uint32_t hash_bits;          // 0 = full; else truncate internal hashes (collision test knob)
     uint32_t ablate;             // perf diagnostics only (env MRG_ABLATE; results are WRONG when set):
@@ -76,6 +76,7 @@ struct MapArgs {
                                  // become tail records), 4 = no per-token work after the queue,
                                  // 8 = every block loads its document's first block (L2-resident),
                                  // 16 = no LDS count add on table hits
+    unsigned long long *prof;    // perf diagnostics (env MRG_PROF): per-phase wave clocks, [7]; else null
 };
 
 // A set of keys with counts (SoA).  len > 16 keys have their bytes at heap[hoff .. hoff+len).

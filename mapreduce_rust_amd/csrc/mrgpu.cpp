@@ -315,8 +315,10 @@ struct MapBufs {
     uint32_t *fcnt = nullptr, *fdoc = nullptr, *foff = nullptr;
     uint64_t *lstart = nullptr;
     uint32_t *llen = nullptr, *ldoc = nullptr;
-    uint64_t *gbits = nullptr;
+    uint32_t *gbits = nullptr;
+    unsigned long long *prof = nullptr;
     void release(Pool &p) {
+        p.put(prof);
         p.put(pool); p.put(rbase); p.put(bcap); p.put(bcount); p.put(dargs); p.put(ovf); p.put(onext);
         p.put(fk0); p.put(fk1); p.put(fcnt); p.put(fdoc); p.put(foff);
         p.put(lstart); p.put(llen); p.put(ldoc); p.put(gbits);
@@ -474,16 +476,21 @@ void job_map(mrg_ctx *c) {
         A.ovf = M.ovf; A.onext = M.onext; A.ocap = (uint32_t)ocap;
         A.fk0 = M.fk0; A.fk1 = M.fk1; A.fcnt = M.fcnt; A.fdoc = M.fdoc; A.foff = M.foff;
         A.lstart = M.lstart; A.llen = M.llen; A.ldoc = M.ldoc; A.lcap = lcap;
-        {  // one bit per tile of each wave (written whole by the kernel: no clearing needed)
-            const uint64_t waves = (uint64_t)grid * MRG_MAP_WAVES;
-            const uint64_t per_wave = MRG_MAP_NSUB * ((n_chunks + waves - 1) / waves);  // 1 KiB tiles per wave
-            A.kwords = (uint32_t)std::max<uint64_t>(1, (per_wave + 63) / 64);
-            M.gbits = pget<uint64_t>(p, waves * A.kwords);
+        {  // non-ASCII tile lists: one entry per tile of a workgroup's share at most
+            const uint64_t per_wg_blocks = (n_chunks + grid - 1) / grid + 1;
+            A.kwords = (uint32_t)(MRG_MAP_NSUB * per_wg_blocks);
+            M.gbits = pget<uint32_t>(p, (uint64_t)grid * A.kwords);
             A.gbits = M.gbits;
         }
         A.counters = c->d_cnt;
         A.hash_bits = hash_bits(c);
         A.ablate = getenv("MRG_ABLATE") ? (uint32_t)atoi(getenv("MRG_ABLATE")) : 0u;
+        A.prof = nullptr;
+        if (getenv("MRG_PROF")) {
+            M.prof = pget<unsigned long long>(p, 8);
+            HIPCHK(hipMemsetAsync(M.prof, 0, 64, s));
+            A.prof = M.prof;
+        }
         HIPCHK(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long) * CNT_N, s));
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_ERRPOS], 0xFF, sizeof(unsigned long long), s));
         ev_rec(c, 0);
@@ -492,6 +499,17 @@ void job_map(mrg_ctx *c) {
         HIPCHK(hipGetLastError());
         ++launches;
         read_counters(c);
+        if (M.prof) {
+            unsigned long long pr[8];
+            HIPCHK(hipMemcpy(pr, M.prof, sizeof pr, hipMemcpyDeviceToHost));
+            double tot = 0;
+            for (int i = 0; i < 7; ++i) tot += (double)pr[i];
+            static const char *nm[7] = {"load-wait", "classify", "stage+scan+queue", "token rounds", "slow tokens",
+                                        "non-ascii", "flush"};
+            fprintf(stderr, "[mrgpu] map phase clocks (sum over waves %.3e):", tot);
+            for (int i = 0; i < 7; ++i) fprintf(stderr, " %s %.1f%%", nm[i], 100.0 * (double)pr[i] / (tot > 0 ? tot : 1));
+            fprintf(stderr, "\n");
+        }
         const uint64_t nl = c->h_cnt[CNT_LONG];
         if (c->h_cnt[CNT_OVF] == 0 && nl <= lcap) break;
         // capacity exceeded: grow each bucket's regions to its demand (remembered), run again
