@@ -208,7 +208,7 @@ struct LdsTable {
     // Claim an empty slot of group g for the key, or find it in a slot filled meanwhile (per lane;
     // only lanes whose key missed a group with empty slots get here -- rare once the table is full).
     __device__ __forceinline__ bool claim(uint64_t a, uint64_t b, uint32_t d, uint32_t g, uint32_t tg, uint64_t tags) {
-        const uint32_t rep32 = tg * 0x01010101u;
+        const uint32_t rep32 = __builtin_amdgcn_perm(0u, tg, 0u);
         const uint64_t rep = (uint64_t)rep32 | ((uint64_t)rep32 << 32);
         uint64_t empty = zero_bytes(tags);
         while (empty) {
@@ -361,22 +361,29 @@ __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint3
     const uint32_t capA = bcap[bA], capB = bcap[bB];  // independent of the probe: issued early
     const uint64_t tagsA = T.tag[gA], tagsB = T.tag[gB];
     auto rep = [](uint32_t tg) {
-        const uint32_t r32 = tg * 0x01010101u;
+        const uint32_t r32 = __builtin_amdgcn_perm(0u, tg, 0u);  // tg in every byte
         return (uint64_t)r32 | ((uint64_t)r32 << 32);
     };
-    uint64_t cA = actA ? zero_bytes(tagsA ^ rep(tgA)) : 0ull, cB = actB ? zero_bytes(tagsB ^ rep(tgB)) : 0ull;
+    // branch-free: masks instead of conditions, so the two chains stay in one basic block
+    uint64_t cA = zero_bytes(tagsA ^ rep(tgA)) & (0ull - (uint64_t)actA);
+    uint64_t cB = zero_bytes(tagsB ^ rep(tgB)) & (0ull - (uint64_t)actB);
     auto slot_of = [](uint32_t g, uint64_t c) { return g * 8u + min((uint32_t)__builtin_ctzll(c | (1ull << 63)) >> 3, 7u); };
     uint32_t sA = slot_of(gA, cA), sB = slot_of(gB, cB);
     const KeyPair kA = T.key[sA], kB = T.key[sB];
-    bool hitA = cA != 0 && ((kA.a ^ a0) | (kA.b ^ a1)) == 0 && (!IDX || T.doc[sA] == dkey);
-    bool hitB = cB != 0 && ((kB.a ^ b0) | (kB.b ^ b1)) == 0 && (!IDX || T.doc[sB] == dkey);
+    bool hitA = (cA != 0) & ((((kA.a ^ a0) | (kA.b ^ a1)) == 0) & (!IDX || T.doc[sA] == dkey));
+    bool hitB = (cB != 0) & ((((kB.a ^ b0) | (kB.b ^ b1)) == 0) & (!IDX || T.doc[sB] == dkey));
     cA &= cA - 1u;
     cB &= cB - 1u;
     const bool t2A = !hitA && cA != 0, t2B = !hitB && cB != 0;
-    if (__any(t2A || t2B)) {
+    if (__any(t2A || t2B)) {  // second tag-matching candidate: both reads unconditional
         const uint32_t s2A = slot_of(gA, cA), s2B = slot_of(gB, cB);
-        if (t2A && T.matches(s2A, a0, a1, dkey)) { hitA = true; sA = s2A; }
-        if (t2B && T.matches(s2B, b0, b1, dkey)) { hitB = true; sB = s2B; }
+        const KeyPair k2A = T.key[s2A], k2B = T.key[s2B];
+        const bool m2A = t2A & ((((k2A.a ^ a0) | (k2A.b ^ a1)) == 0) & (!IDX || T.doc[s2A] == dkey));
+        const bool m2B = t2B & ((((k2B.a ^ b0) | (k2B.b ^ b1)) == 0) & (!IDX || T.doc[s2B] == dkey));
+        hitA |= m2A;
+        hitB |= m2B;
+        sA = m2A ? s2A : sA;
+        sB = m2B ? s2B : sB;
     }
     if (!(abl & 16u)) {
         atomicAdd(&T.cnt[sA], hitA ? 1u : 0u);  // every lane: no branch (the slot is valid)
@@ -698,7 +705,19 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         auto na = [](const uint4 &x) { return ((x.x | x.y | x.z | x.w) & 0x80808080u) != 0u; };
         const uint32_t l16 = (uint32_t)lane * SEG;
         const uint32_t m0 = classify(X.v0, l16), m1 = classify(X.v1, 1024u + l16);
-        const uint32_t mh = lane_u32(lane == 1 ? classify(X.e, (uint32_t)BLK) : 0u, 1);
+        // the first halo segment (lane 1's e) by 16 lanes, one byte each, through two ballots
+        uint32_t mh;
+        {
+            const uint32_t e0 = lane_u32(X.e.x, 1), e1 = lane_u32(X.e.y, 1), e2 = lane_u32(X.e.z, 1),
+                           e3 = lane_u32(X.e.w, 1);
+            const uint32_t k = (uint32_t)lane & 15u;
+            const uint32_t dwv = k < 8u ? (k < 4u ? e0 : e1) : (k < 12u ? e2 : e3);
+            const uint32_t cl = s_lut[__builtin_amdgcn_ubfe(dwv, 8u * (k & 3u), 7)];
+            const bool in = (uint32_t)BLK + k < hi_rel;  // bytes past the document are White_Space
+            const uint32_t wm = (uint32_t)__ballot(lane < 16 && in && (cl & 1u));
+            const uint32_t sm = (uint32_t)__ballot(lane < 16 && (!in || (cl & 0x100u)));
+            mh = (wm & 0xFFFFu) | (sm << 16);
+        }
         const bool n0 = na(X.v0), n1 = na(X.v1), ne = na(X.e);
         // class of the byte before the block (lane 0's e, byte 15)
         const uint32_t prev_blk =
@@ -766,9 +785,10 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             // tokens of the queue, TWO per lane per round (entries q and q + 64: two independent LDS
             // dependency chains in one instruction stream, so each wait covers both); the queue, masks
             // and window are read-only now
-            auto extract = [&](uint32_t q, bool &fast, bool &slow, uint32_t &s, uint64_t &tk0, uint64_t &tk1) {
+            auto extract = [&](uint32_t q, uint32_t sraw, bool &fast, bool &slow, uint32_t &s, uint64_t &tk0,
+                               uint64_t &tk1) {
                 const bool act = q < total;
-                s = act ? (uint32_t)queue[q] : 0u;
+                s = act ? sraw : 0u;
                 const uint64_t mw = mp[s >> 4];
                 const uint32_t Wp = (uint32_t)mw, Sp = (uint32_t)(mw >> 32);
                 const uint32_t i = s & 15u;
@@ -796,7 +816,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                                d4 = win32[dw + 4];
                 const uint32_t *zm = s_zm[fast ? tlen : 0u];
                 const uint32_t *gm = s_zm[ga];
-                const uint32_t bsel = 0x00010203u + r * 0x01010101u;
+                const uint32_t bsel = 0x00010203u + __builtin_amdgcn_perm(0u, r, 0u);  // + r in every byte
                 auto sel = [&](int j) {
                     return ((bsel + (gm[j] & 0x01010101u)) & ~zm[j]) | (0x0C0C0C0Cu & zm[j]);
                 };
@@ -830,8 +850,12 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 bool fa, sa, fb, sb;
                 uint32_t sA, sB;
                 uint64_t a0, a1, b0, b1;
-                uint32_t ga = extract(base + (uint32_t)lane, fa, sa, sA, a0, a1);
-                uint32_t gb = extract(base + 64u + (uint32_t)lane, fb, sb, sB, b0, b1);
+                // both queue entries first, unconditionally (entries past `total` are stale but in
+                // bounds), so the two chains share every LDS wait
+                const uint32_t qa = base + (uint32_t)lane, qb = qa + 64u;
+                const uint32_t ra = queue[min(qa, (uint32_t)QCAP - 1u)], rb = queue[min(qb, (uint32_t)QCAP - 1u)];
+                uint32_t ga = extract(qa, ra, fa, sa, sA, a0, a1);
+                uint32_t gb = extract(qb, rb, fb, sb, sB, b0, b1);
                 if (__any((ga | gb) != 0u)) {
                     squeeze(ga, a0, a1);
                     squeeze(gb, b0, b1);
