@@ -560,8 +560,10 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[NW][WIN];
     __shared__ __attribute__((aligned(8))) uint64_t s_mp[NW][64];  // W(g)|W(g+1)<<16 | (S(g)|S(g+1)<<16)<<32
     __shared__ uint16_t s_q[NW][QCAP];
-    __shared__ uint16_t s_lut[128];                               // ASCII class: W | S << 8
-    __shared__ __attribute__((aligned(16))) uint32_t s_zm[17][4];  // key-length byte masks
+    // LUT and length masks first in LDS (highest alignment): their base then fits the 16-bit
+    // offset field of ds_read, so a lookup needs no separate address add
+    __shared__ __attribute__((aligned(2048))) uint16_t s_lut[128];  // ASCII class: W | S << 8
+    __shared__ __attribute__((aligned(1024))) uint32_t s_zm[17][4];  // key-length byte masks
     // workgroup: combine table + tail-region cursors
     __shared__ KeyPair s_key[CAP];
     __shared__ unsigned int s_cnt[CAP];
