@@ -675,7 +675,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         pacc[i] += t_ - tl;                \
         tl = t_;                           \
     }
-    auto process_blk = [&](const BlkInfo &I, const Blk &X, uint64_t cblk) {
+    auto process_blk = [&](const BlkInfo &I, const Blk &X, uint64_t cblk, auto &&mid) {
         const uint64_t Ab = I.Ab, doc_lo = I.doc_lo, doc_hi = I.doc_hi;
         const uint32_t docid = I.docid;
         // classify segment [B, B + 16) (relative to Ab) into W16 | S16 << 16; bytes outside the
@@ -725,6 +725,11 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const uint32_t prev_blk =
             Ab > doc_lo ? (uint32_t)(s_lut[(lane_u32(X.e.w, 0) >> 24) & 0x7Fu] >> 8) : 1u;
         MRG_PT(1);
+        // the next block's registers are waited for HERE, before this block's tail stores are
+        // issued: vmcnt also counts stores, so a wait placed after them would wait for their
+        // acknowledgements too
+        mid();
+        MRG_PT(0);
 
 #pragma unroll 1
         for (uint32_t j = 0; j < NSUB; ++j) {
@@ -930,25 +935,21 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         IA = locate_blk(A, c, dcur);
         first_blk = IA;
         load_blk(IA, XA);
+        settle(XA);
     }
     while (c < whi_b) {
         const uint64_t cB = grab();
         IB = cB < whi_b ? locate_blk(A, cB, dcur) : IA;
-        settle(XA);
-        MRG_PT(0);
         load_blk(IB, XB);
-        process_blk(IA, XA, c);
+        process_blk(IA, XA, c, [&]() { settle(XB); });
         c = cB;
         if (c >= whi_b) break;
         const uint64_t cA = grab();
         IA = cA < whi_b ? locate_blk(A, cA, dcur) : IB;
-        settle(XB);
-        MRG_PT(0);
         load_blk(IA, XA);
-        process_blk(IB, XB, c);
+        process_blk(IB, XB, c, [&]() { settle(XA); });
         c = cA;
     }
-
     MRG_PT(4);
     // ---- non-ASCII tiles recorded by the main loop
     __syncthreads();  // the list is complete (global writes of this workgroup, then the barrier)
