@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--vocab", type=int, default=1 << 20)
     ap.add_argument("--zipf-s", type=float, default=1.1)
     ap.add_argument("--seed", type=int, default=0x5EED2026)
-    ap.add_argument("--cpu-sample-mib", type=int, default=48)
+    ap.add_argument("--cpu-sample-mib", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lds-cap", type=int, default=0)
     return ap.parse_args()

@@ -646,7 +646,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const BlkInfo &b = (A.ablate & 8u) ? first_blk : b0;  // a real block: its own base and bounds
         const GAS uint8_t *src = gp(A.in) + (b.Ab - (uint64_t)BEHIND);
         auto ld = [&](uint32_t idx) -> uint4 {
-            const u32x4 t = *reinterpret_cast<const GAS u32x4 *>(src + 16u * min(max(idx, b.v0), b.v1 - 1u));
+            const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const GAS u32x4 *>(src + 16u * min(max(idx, b.v0), b.v1 - 1u)));
             return uint4{t.x, t.y, t.z, t.w};
         };
         X.v0 = ld(1u + (uint32_t)lane);
