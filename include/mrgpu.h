@@ -44,6 +44,7 @@ extern "C" {
 /* ---- flags ---- */
 #define MRG_FLAG_NO_COMPAT_DROP_LAST 0x1u  /* default (flag clear): reproduce worker.rs:169-184, which never
                                               writes the last group of a partition.  Set: write it. */
+#define MRG_FLAG_FINAL_TXT 0x2u  /* mrg_run_job: also write out_dir/final.txt (src/run.sh:16-20) */
 /* bits 8..15: truncate every internal (non-partition) hash to this many bits; 0 = full 64 bits.
    A test knob that forces hash collisions so the full-string tie-break paths are exercised. */
 #define MRG_FLAG_DEBUG_HASH_BITS(n) (((uint32_t)(n) & 0xFFu) << 8)
@@ -119,6 +120,11 @@ int mrg_job_reduce(mrg_ctx *ctx, uint64_t *h_out_bytes);
 int mrg_job_output(mrg_ctx *ctx, const uint8_t **d_out, uint64_t *h_part_off);
 /* Copy the output to host memory (h_dst of at least *h_out_bytes). */
 int mrg_job_copy_output(mrg_ctx *ctx, uint8_t *h_dst, uint64_t cap);
+/* final.txt of src/run.sh:16-20 (generate_output: cat mr-* | sort > final.txt, with LC_ALL=C), built
+ * on the device from the job's keys: every line of every mr-{r}.txt this context holds, sorted
+ * bytewise (= by key: key bytes are all > ' ').  *d_out stays valid until the next job call. */
+int mrg_job_final(mrg_ctx *ctx, const uint8_t **d_out, uint64_t *h_bytes);
+int mrg_job_copy_final(mrg_ctx *ctx, uint8_t *h_dst, uint64_t cap);
 
 /* ---- plugin-surface equivalents, host buffers (one map task / one reduce task) ---- */
 
@@ -135,7 +141,8 @@ void mrg_parts_free(mrg_parts *parts);
 int mrg_reduce(mrg_ctx *ctx, int app, uint32_t r, const mrg_parts *const *in, size_t k, uint32_t n_reduce,
                uint32_t flags, const char *const *doc_names, uint32_t n_docs, uint8_t **h_out, size_t *h_out_len);
 
-/* The whole job on one GPU: files are read, mapped, reduced; out_dir/mr-{r}.txt written.
+/* The whole job on one GPU: files are read, mapped, reduced; out_dir/mr-{r}.txt written (and
+ * out_dir/final.txt with MRG_FLAG_FINAL_TXT).
  * Indexer document names are the file paths as given (the reference opens "data/gut-{m}.txt"). */
 int mrg_run_job(const char *const *files, size_t n_files, uint32_t n_reduce, int app, const char *out_dir,
                 uint32_t flags, int device);

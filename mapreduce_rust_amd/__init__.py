@@ -6,13 +6,12 @@ package is the host-side mirror of the reference's interfaces over that ABI:
   mapreduce_rust_amd.native   ctypes binding of every entry point of include/mrgpu.h
   mapreduce_rust_amd.worker   Worker.map / Worker.reduce with the reference's file conventions
                               (src/mr/worker.rs: data/gut-{m}.txt -> mr-{r}.txt)
-  mapreduce_rust_amd.app      the plugin surface: wc / indexer `map` and `reduce` (src/app/wc.rs)
   mapreduce_rust_amd.shuffle  multi-GPU static plan + all-to-all exchange over torch.distributed
 
 There is no CPU fallback: if the HIP library is missing or no GPU is present, calls raise.
 """
-from .native import (APP_INDEXER, APP_WC, FLAG_NO_COMPAT_DROP_LAST, MrgError, Context, debug_hash_bits,
-                     lib_path, load)
+from .native import (APP_INDEXER, APP_WC, FLAG_FINAL_TXT, FLAG_NO_COMPAT_DROP_LAST, MrgError, Context,
+                     debug_hash_bits, lib_path, load)
 
-__all__ = ["APP_WC", "APP_INDEXER", "FLAG_NO_COMPAT_DROP_LAST", "MrgError", "Context", "debug_hash_bits",
-           "lib_path", "load"]
+__all__ = ["APP_WC", "APP_INDEXER", "FLAG_NO_COMPAT_DROP_LAST", "FLAG_FINAL_TXT", "MrgError", "Context",
+           "debug_hash_bits", "lib_path", "load"]

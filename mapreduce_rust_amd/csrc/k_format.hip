@@ -173,12 +173,36 @@ __global__ void k_idx_write(const SortRec *r, uint64_t n, uint64_t G, KeySet ks,
     *q = (i + 1 == e) ? '\n' : ',';
 }
 
+// final.txt (src/run.sh:16-20): every line of every mr-{r}.txt, sorted bytewise.  Keys are distinct
+// across partitions and their bytes are all > ' ', so the line order is the key order; the only keys
+// missing are those the per-partition pass dropped (the last group of each partition, worker.rs:
+// 169-184).  part2[key] = 1 for those, 0 for the rest; a sort by (part2, key) then puts final.txt in
+// "partition" 0.  r is sorted by (partition, full key bytes[, doc]).
+__global__ void k_final_part(const SortRec *r, uint64_t n, KeySet ks, const uint8_t *heap, int drop_last,
+                             uint32_t *part2) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t e = i + 1;  // first record of the next group (indexer groups span several docs)
+    while (e < n && same_key(r[i], r[e], ks, heap)) ++e;
+    const bool dropped = drop_last && (e == n || r[e].part != r[i].part);
+    part2[r[i].idx] = dropped ? 1u : 0u;
+}
+
 __global__ void k_gather_first(const SortRec *r, const uint64_t *H, uint64_t G, SortRec *out) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g < G) out[g] = r[H[g]];
 }
 
 }  // namespace
+
+void mrg_launch_fix_runs(SortRec *r, uint64_t n, KeySet ks, const uint8_t *heap, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_fix_runs, grid_for(n), dim3(256), 0, s, r, n, ks, heap);
+}
+
+void mrg_launch_final_part(const SortRec *r, uint64_t n, KeySet ks, const uint8_t *heap, int drop_last,
+                           uint32_t *part2, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_final_part, grid_for(n), dim3(256), 0, s, r, n, ks, heap, drop_last, part2);
+}
 
 uint64_t mrg_format(const FormatArgs &f, DevPool &pool, uint8_t **out_buf, uint64_t *out_cap,
                     uint64_t *part_off_host, hipStream_t s) {

@@ -205,6 +205,11 @@ struct FormatArgs {
 // partition byte offsets to part_off_host[0..n_reduce].  Returns the total byte count.
 uint64_t mrg_format(const FormatArgs &f, DevPool &pool, uint8_t **out_buf, uint64_t *out_cap,
                     uint64_t *part_off_host, hipStream_t s);
+// Insertion-sort runs of equal (part, 16-byte prefix) that involve a long key by full key bytes.
+void mrg_launch_fix_runs(SortRec *r, uint64_t n, KeySet ks, const uint8_t *heap, hipStream_t s);
+// final.txt: part2[key] = 1 for the keys the per-partition pass drops (drop-last), else 0.
+void mrg_launch_final_part(const SortRec *r, uint64_t n, KeySet ks, const uint8_t *heap, int drop_last,
+                           uint32_t *part2, hipStream_t s);
 
 // ---- k_gen.hip
 int mrg_gen_zipf_impl(uint8_t *dst, uint64_t n, uint64_t seed, uint64_t file_index, uint32_t vocab, double s,

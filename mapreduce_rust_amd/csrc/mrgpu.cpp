@@ -159,6 +159,9 @@ struct mrg_ctx {
     uint64_t out_cap = 0, out_bytes = 0;
     std::vector<uint64_t> part_off;
     bool reduced = false;
+    uint8_t *d_final = nullptr;     // final.txt (mrg_job_final)
+    uint64_t final_cap = 0, final_bytes = 0;
+    bool finalized = false;
     mrg_stats st{};
 };
 
@@ -394,6 +397,8 @@ void job_begin(mrg_ctx *c, int app, uint32_t R, uint32_t flags) {
     c->n_owners = 0;
     c->out_bytes = 0;
     c->part_off.assign(R + 1, 0);
+    c->final_bytes = 0;
+    c->finalized = false;
     c->st = mrg_stats{};
 }
 
@@ -571,74 +576,137 @@ uint32_t bytes_for(uint64_t maxval) {
     return b;
 }
 
+// Indexer document order = bytewise order of the names (the indexer reduce sorts its values):
+// rank of each global document id, and the names concatenated in rank order, on the device.
+struct DocRank {
+    uint32_t *rank = nullptr;
+    uint8_t *names = nullptr;
+    uint64_t *name_off = nullptr;
+    void release(Pool &p) {
+        p.put(rank); p.put(names); p.put(name_off);
+        *this = DocRank{};
+    }
+};
+
+DocRank doc_ranks(mrg_ctx *c) {
+    DocRank d;
+    if (!is_idx(c)) return d;
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const uint32_t nn = (uint32_t)c->names.size();
+    if (nn == 0) raise(MRG_EINVAL, "indexer needs document names (mrg_job_set_doc_names)");
+    std::vector<uint32_t> order(nn);
+    for (uint32_t i = 0; i < nn; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c->names[a] < c->names[b]; });
+    std::vector<uint32_t> rank(nn);
+    std::vector<uint64_t> noff(nn + 1, 0);
+    std::string cat;
+    for (uint32_t r = 0; r < nn; ++r) {
+        rank[order[r]] = r;
+        cat += c->names[order[r]];
+        noff[r + 1] = cat.size();
+    }
+    d.rank = pget<uint32_t>(p, nn);
+    d.names = pget<uint8_t>(p, cat.size() + 1);
+    d.name_off = pget<uint64_t>(p, nn + 1);
+    HIPCHK(hipMemcpyAsync(d.rank, rank.data(), 4ull * nn, hipMemcpyHostToDevice, s));
+    if (!cat.empty()) HIPCHK(hipMemcpyAsync(d.names, cat.data(), cat.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d.name_off, noff.data(), 8ull * (nn + 1), hipMemcpyHostToDevice, s));
+    sync(c);  // host vectors go out of scope
+    return d;
+}
+
+// Sort records of the keys `ks` by (partition < R, key bytes[, doc rank]) (worker.rs:162-164).
+// Returns a or b.
+SortRec *sort_keys(mrg_ctx *c, KeySet ks, uint32_t R, const uint32_t *d_rank, SortRec *a, SortRec *b, void *stmp) {
+    const uint64_t n = c->keys.n;
+    const bool idx = is_idx(c);
+    mrg_launch_make_sortrec(ks, n, d_rank, a, c->stream);
+    SortPlan plan{};
+    plan.use_part = R > 1;
+    plan.part_bytes = bytes_for(R - 1);
+    plan.use_k0 = plan.use_k1 = true;
+    plan.use_doc = idx;
+    plan.doc_bytes = idx ? bytes_for(c->names.size() - 1) : 0;
+    int passes = 0;
+    return mrg_radix_sort(a, b, n, plan, stmp, c->stream, &passes);
+}
+
+FormatArgs format_args(mrg_ctx *c, const SortRec *recs, KeySet ks, uint32_t R, int drop_last, const DocRank &dr) {
+    FormatArgs f{};
+    f.recs = recs;
+    f.n = c->keys.n;
+    f.ks = ks;
+    f.heap = c->keys.heap;
+    f.n_reduce = R;
+    f.drop_last = drop_last;
+    f.indexer = is_idx(c);
+    f.any_long = c->keys.any_long;
+    f.names = dr.names;
+    f.name_off = dr.name_off;
+    return f;
+}
+
+int compat_drop_last(const mrg_ctx *c) { return (c->flags & MRG_FLAG_NO_COMPAT_DROP_LAST) ? 0 : 1; }
+
 void job_reduce(mrg_ctx *c) {
     need_job(c);
     if (!c->mapped) raise(MRG_EINVAL, "nothing to reduce: call mrg_job_map or mrg_job_import first");
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     const uint64_t n = c->keys.n;
-    const bool idx = is_idx(c);
-    // indexer: document order = bytewise order of the names (indexer reduce sorts its values)
-    uint32_t *d_rank = nullptr;
-    uint8_t *d_names = nullptr;
-    uint64_t *d_name_off = nullptr;
-    std::vector<uint32_t> order;
-    if (idx) {
-        const uint32_t nn = (uint32_t)c->names.size();
-        if (nn == 0) raise(MRG_EINVAL, "indexer needs document names (mrg_job_set_doc_names)");
-        order.resize(nn);
-        for (uint32_t i = 0; i < nn; ++i) order[i] = i;
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c->names[a] < c->names[b]; });
-        std::vector<uint32_t> rank(nn);
-        std::vector<uint64_t> noff(nn + 1, 0);
-        std::string cat;
-        for (uint32_t r = 0; r < nn; ++r) {
-            rank[order[r]] = r;
-            cat += c->names[order[r]];
-            noff[r + 1] = cat.size();
-        }
-        d_rank = pget<uint32_t>(p, nn);
-        d_names = pget<uint8_t>(p, cat.size() + 1);
-        d_name_off = pget<uint64_t>(p, nn + 1);
-        HIPCHK(hipMemcpyAsync(d_rank, rank.data(), 4ull * nn, hipMemcpyHostToDevice, s));
-        if (!cat.empty()) HIPCHK(hipMemcpyAsync(d_names, cat.data(), cat.size(), hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(d_name_off, noff.data(), 8ull * (nn + 1), hipMemcpyHostToDevice, s));
-        sync(c);  // host vectors go out of scope
-    }
+    DocRank dr = doc_ranks(c);
     ev_rec(c, 4);
     SortRec *a = pget<SortRec>(p, n), *b = pget<SortRec>(p, n);
     void *stmp = p.get(mrg_sort_tmp_bytes(n));
-    mrg_launch_make_sortrec(c->keys.ks, n, d_rank, a, s);
-    SortPlan plan{};
-    plan.use_part = c->R > 1;
-    plan.part_bytes = bytes_for(c->R - 1);
-    plan.use_k0 = plan.use_k1 = true;
-    plan.use_doc = idx;
-    plan.doc_bytes = idx ? bytes_for(c->names.size() - 1) : 0;
-    int passes = 0;
-    SortRec *sorted = mrg_radix_sort(a, b, n, plan, stmp, s, &passes);
+    SortRec *sorted = sort_keys(c, c->keys.ks, c->R, dr.rank, a, b, stmp);
     ev_rec(c, 5);
-    FormatArgs f{};
-    f.recs = sorted;
-    f.n = n;
-    f.ks = c->keys.ks;
-    f.heap = c->keys.heap;
-    f.n_reduce = c->R;
-    f.drop_last = (c->flags & MRG_FLAG_NO_COMPAT_DROP_LAST) ? 0 : 1;
-    f.indexer = idx;
-    f.any_long = c->keys.any_long;
-    f.names = d_names;
-    f.name_off = d_name_off;
+    const FormatArgs f = format_args(c, sorted, c->keys.ks, c->R, compat_drop_last(c), dr);
     c->part_off.assign(c->R + 1, 0);
     c->out_bytes = mrg_format(f, p, &c->d_out, &c->out_cap, c->part_off.data(), s);
     ev_rec(c, 6);
     HIPCHK(hipGetLastError());
     p.put(a); p.put(b); p.put(stmp);
-    p.put(d_rank); p.put(d_names); p.put(d_name_off);
+    dr.release(p);
     c->st.ms_sort = ev_ms(c, 4, 5);
     c->st.ms_format = ev_ms(c, 5, 6);
     c->st.output_bytes = c->out_bytes;
     c->reduced = true;
+}
+
+// final.txt (src/run.sh:16-20 with LC_ALL=C): the lines of every partition this context holds,
+// sorted bytewise, written on the device.  The keys the per-partition pass drops (drop-last) are
+// found in the partition order, moved to a second "partition" and the rest re-sorted by key alone.
+void job_final(mrg_ctx *c) {
+    need_job(c);
+    if (!c->mapped) raise(MRG_EINVAL, "no keys: call mrg_job_map or mrg_job_import first");
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const uint64_t n = c->keys.n;
+    DocRank dr = doc_ranks(c);
+    SortRec *a = pget<SortRec>(p, n), *b = pget<SortRec>(p, n);
+    void *stmp = p.get(mrg_sort_tmp_bytes(n));
+    const int drop = compat_drop_last(c);
+    uint32_t *part2 = pget<uint32_t>(p, std::max<uint64_t>(n, 1));
+    KeySet ks2 = c->keys.ks;
+    ks2.part = part2;
+    if (drop) {
+        SortRec *s1 = sort_keys(c, c->keys.ks, c->R, dr.rank, a, b, stmp);
+        if (c->keys.any_long) mrg_launch_fix_runs(s1, n, c->keys.ks, c->keys.heap, s);
+        mrg_launch_final_part(s1, n, c->keys.ks, c->keys.heap, drop, part2, s);
+    } else {
+        mrg_launch_fill_u32(part2, 0u, n, s);
+    }
+    const uint32_t R2 = drop ? 2u : 1u;
+    SortRec *s2 = sort_keys(c, ks2, R2, dr.rank, a, b, stmp);
+    const FormatArgs f = format_args(c, s2, ks2, R2, 0, dr);
+    uint64_t po[3] = {0, 0, 0};
+    mrg_format(f, p, &c->d_final, &c->final_cap, po, s);
+    HIPCHK(hipGetLastError());
+    p.put(a); p.put(b); p.put(stmp); p.put(part2);
+    dr.release(p);
+    c->final_bytes = po[1];
+    c->finalized = true;
 }
 
 void export_sizes(mrg_ctx *c, uint32_t n_owners, uint64_t *h_rec, uint64_t *h_heap) {
@@ -878,6 +946,26 @@ int mrg_job_copy_output(mrg_ctx *c, uint8_t *h_dst, uint64_t cap) {
     });
 }
 
+int mrg_job_final(mrg_ctx *c, const uint8_t **d_out, uint64_t *h_bytes) {
+    return guard([&] {
+        job_final(c);
+        if (d_out) *d_out = c->d_final;
+        if (h_bytes) *h_bytes = c->final_bytes;
+    });
+}
+
+int mrg_job_copy_final(mrg_ctx *c, uint8_t *h_dst, uint64_t cap) {
+    return guard([&] {
+        need_job(c);
+        if (!c->finalized) raise(MRG_EINVAL, "no final.txt: call mrg_job_final first");
+        if (cap < c->final_bytes) raise(MRG_EINVAL, "destination too small (%llu < %llu)", (unsigned long long)cap,
+                                        (unsigned long long)c->final_bytes);
+        if (c->final_bytes)
+            HIPCHK(hipMemcpyAsync(h_dst, c->d_final, c->final_bytes, hipMemcpyDeviceToHost, c->stream));
+        sync(c);
+    });
+}
+
 // ---- plugin surface (host buffers)
 
 int mrg_map(mrg_ctx *c, int app, const uint8_t *h_bytes, size_t n, const char *doc, uint32_t doc_id,
@@ -1025,6 +1113,19 @@ int mrg_run_job(const char *const *files, size_t n_files, uint32_t n_reduce, int
             const size_t w = b > a ? fwrite(out.data() + a, 1, b - a, f) : 0;
             fclose(f);
             if (w != b - a) raise(MRG_EIO, "short write on %s", path.c_str());
+        }
+        if (flags & MRG_FLAG_FINAL_TXT) {  // run.sh:16-20 generate_output, on the device
+            job_final(c);
+            std::vector<uint8_t> fin(c->final_bytes);
+            if (c->final_bytes)
+                HIPCHK(hipMemcpyAsync(fin.data(), c->d_final, c->final_bytes, hipMemcpyDeviceToHost, c->stream));
+            sync(c);
+            const std::string path = std::string(out_dir) + "/final.txt";
+            FILE *f = fopen(path.c_str(), "wb");
+            if (!f) raise(MRG_EIO, "cannot create %s", path.c_str());
+            const size_t w = fin.empty() ? 0 : fwrite(fin.data(), 1, fin.size(), f);
+            fclose(f);
+            if (w != fin.size()) raise(MRG_EIO, "short write on %s", path.c_str());
         }
         c->pool.put(d);
     });

@@ -3,7 +3,8 @@
 //   outputs mr-{r}.txt in the working directory (src/mr/worker.rs:67, 167).
 // The coordinator's task assignment (src/mr/coordinator.rs:137-215) becomes a static plan: one GPU
 // job maps every file and reduces every partition.
-//   usage: mrgpu <map_n> <reduce_n> [--app wc|indexer] [--device N] [--no-compat-drop-last]
+// --final also writes final.txt, the output of src/run.sh:16-20 (cat mr-* | sort, LC_ALL=C), built on the GPU.
+//   usage: mrgpu <map_n> <reduce_n> [--app wc|indexer] [--device N] [--no-compat-drop-last] [--final]
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -16,7 +17,7 @@
 int main(int argc, char **argv) {
     if (argc < 3) {
         fprintf(stderr, "Usage: mrgpu <input files number> <reduce task number> [--app wc|indexer] [--device N] "
-                        "[--no-compat-drop-last]\n");
+                        "[--no-compat-drop-last] [--final]\n");
         return 2;
     }
     const int map_n = atoi(argv[1]);
@@ -31,6 +32,8 @@ int main(int argc, char **argv) {
             device = atoi(argv[++i]);
         } else if (!strcmp(argv[i], "--no-compat-drop-last")) {
             flags |= MRG_FLAG_NO_COMPAT_DROP_LAST;
+        } else if (!strcmp(argv[i], "--final")) {
+            flags |= MRG_FLAG_FINAL_TXT;
         }
     }
     if (map_n < 0 || reduce_n <= 0) {

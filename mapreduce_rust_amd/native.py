@@ -12,6 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 APP_WC = 0
 APP_INDEXER = 1
 FLAG_NO_COMPAT_DROP_LAST = 0x1
+FLAG_FINAL_TXT = 0x2
 XREC_BYTES = 40
 
 OK, EINVAL, EUTF8, EHIP, ENOMEM, EIO = 0, -1, -2, -3, -4, -5
@@ -68,6 +69,8 @@ _SIGS = {
     "mrg_job_reduce": (C.c_int, [_vp, _u64p]),
     "mrg_job_output": (C.c_int, [_vp, C.POINTER(_vp), _u64p]),
     "mrg_job_copy_output": (C.c_int, [_vp, _vp, C.c_uint64]),
+    "mrg_job_final": (C.c_int, [_vp, C.POINTER(_vp), _u64p]),
+    "mrg_job_copy_final": (C.c_int, [_vp, _vp, C.c_uint64]),
     "mrg_map": (C.c_int, [_vp, C.c_int, C.c_char_p, C.c_size_t, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32,
                           C.POINTER(_vp)]),
     "mrg_parts_get": (C.c_int, [_vp, C.c_uint32, C.POINTER(_vp), _u64p, C.POINTER(_vp), _u64p]),
@@ -233,6 +236,15 @@ class Context:
         """mr-{r}.txt contents for every partition r."""
         data, off = self.copy_output()
         return [data[off[r]:off[r + 1]] for r in range(self.n_reduce)]
+
+    def final(self):
+        """final.txt (src/run.sh:16-20, LC_ALL=C) of this job, built on the device."""
+        d = _vp()
+        n = C.c_uint64()
+        _check(load().mrg_job_final(self.h, C.byref(d), C.byref(n)))
+        buf = C.create_string_buffer(max(n.value, 1))
+        _check(load().mrg_job_copy_final(self.h, buf, n.value))
+        return buf.raw[:n.value]
 
     # ---- plugin surface (host buffers)
     def map_task(self, app, data, doc, doc_id, n_reduce, flags=0):

@@ -291,3 +291,71 @@ def test_worker_indexer_tasks(tmp_path, corpus):
         w.reduce(r)
         assert sha((tmp_path / f"mr-{r}.txt").read_bytes()) == GOLDEN["indexer"]["10"][f"mr-{r}.txt"], r
     w.close()
+
+
+# ---- final.txt (src/run.sh:16-20, LC_ALL=C) built on the device: SURVEY.md §8 row f3
+
+def _final_of(outs):
+    """run.sh:16-20 restated: every line of every mr-{r}.txt, sorted bytewise."""
+    lines = [l for o in outs for l in o.split(b"\n") if l]
+    return b"".join(l + b"\n" for l in sorted(lines))
+
+
+@pytest.mark.parametrize("R", ["10", "1", "3", "64"])
+def test_final_txt_golden(ctx, corpus, R):
+    from gpu_util import run_wc
+    outs = run_wc(ctx, corpus, int(R))
+    fin = ctx.final()
+    assert sha(fin) == GOLDEN["wc"][R]["final.txt"]
+    assert fin == _final_of(outs)
+
+
+def test_final_txt_no_drop_and_collisions(ctx, corpus):
+    """Last groups kept (nothing dropped) and forced internal hash collisions (long-key tie-breaks)."""
+    import mapreduce_rust_amd as M
+    from gpu_util import run_wc
+    for flags in (M.FLAG_NO_COMPAT_DROP_LAST, M.debug_hash_bits(4), M.FLAG_NO_COMPAT_DROP_LAST | M.debug_hash_bits(1)):
+        outs = run_wc(ctx, corpus[:3], 7, flags=flags)
+        assert ctx.final() == _final_of(outs), flags
+
+
+def test_final_txt_long_keys_and_unicode(ctx):
+    import mapreduce_rust_amd as M
+    from gpu_util import run_wc
+    rnd = random.Random(7)
+    words = ["x" * n + s for n in (15, 16, 17, 30) for s in ("", "a", "b", "é")] + ["naïve", "ſong", "Ærø", "a"]
+    text = " ".join(rnd.choice(words) for _ in range(5000)).encode()
+    for flags in (0, M.FLAG_NO_COMPAT_DROP_LAST):
+        outs = run_wc(ctx, [text], 5, flags=flags)
+        assert ctx.final() == _final_of(outs)
+
+
+def test_final_txt_indexer(ctx, corpus):
+    import mapreduce_rust_amd as M
+    from gpu_util import run_wc
+    names = [f"data/gut-{m}.txt" for m in range(6)]
+    outs = run_wc(ctx, corpus, 10, app=M.APP_INDEXER, names=names)
+    assert ctx.final() == _final_of(outs)
+
+
+def test_final_txt_empty(ctx):
+    from gpu_util import run_wc
+    run_wc(ctx, [b"", b"  \n"], 4)
+    assert ctx.final() == b""
+
+
+def test_run_job_writes_final_txt(tmp_path, corpus):
+    import mapreduce_rust_amd as M
+    d = tmp_path / "data"
+    d.mkdir()
+    files = []
+    for m in range(6):
+        (d / f"gut-{m}.txt").write_bytes(corpus[m])
+        files.append(f"data/gut-{m}.txt")
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        M.native.run_job(files, 10, M.APP_WC, ".", M.FLAG_FINAL_TXT)
+    finally:
+        os.chdir(cwd)
+    assert sha((tmp_path / "final.txt").read_bytes()) == GOLDEN["wc"]["10"]["final.txt"]
