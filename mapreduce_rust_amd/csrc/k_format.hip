@@ -71,6 +71,14 @@ __global__ void k_wc_len(const SortRec *r, uint64_t n, KeySet ks, int drop_last,
 }
 
 __device__ __forceinline__ uint8_t *put_u64(uint8_t *o, uint64_t v, uint32_t nd) {
+    if (v <= 0xFFFFFFFFull) {  // 32-bit division (a 64-bit one is a long software sequence)
+        uint32_t w = (uint32_t)v;
+        for (uint32_t k = nd; k > 0; --k) {
+            o[k - 1] = (uint8_t)('0' + w % 10u);
+            w /= 10u;
+        }
+        return o + nd;
+    }
     for (uint32_t k = nd; k > 0; --k) {
         o[k - 1] = (uint8_t)('0' + v % 10u);
         v /= 10u;
@@ -83,12 +91,18 @@ __global__ void k_wc_write(const SortRec *r, uint64_t n, KeySet ks, const uint8_
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || L[i] == 0) return;
     const uint32_t e = r[i].idx;
-    const uint32_t len = ks.len[e];
+    const uint32_t len = ks.len[e];  // read once: the byte stores below may alias any global pointer
+    const uint64_t c = ks.cnt[e];
     uint8_t *o = out + O[i];
-    for (uint32_t b = 0; b < len; ++b) o[b] = (uint8_t)key_byte_at(ks, heap, e, b, r[i].k0, r[i].k1);
+    if (len <= 16u) {
+        const uint64_t k0 = r[i].k0, k1 = r[i].k1;
+        for (uint32_t b = 0; b < len; ++b) o[b] = (uint8_t)mrg_key_byte(k0, k1, b);
+    } else {
+        const uint8_t *src = heap + ks.hoff[e];
+        for (uint32_t b = 0; b < len; ++b) o[b] = src[b];
+    }
     o += len;
     *o++ = ' ';
-    const uint64_t c = ks.cnt[e];
     o = put_u64(o, c, mrg_ndigits(c));
     *o = '\n';
 }

@@ -316,6 +316,96 @@ __global__ void k_partition(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t
     ks.part[i] = (uint32_t)(h % (uint64_t)n_reduce);
 }
 
+// ---------------------------------------------------------------- wide (sort-based) aggregation
+// High-cardinality inputs (~1e9 near-unique keys): almost every token misses the
+// map-side combine and no per-bucket LDS table can hold a bucket's keys, so instead of hashing, every
+// map record (tail regions, flushed tables, overflow lists) is gathered as a sort record with its
+// partition (SipHash-1-3 % nReduce, worker.rs:111-115, 129) and count, sorted by (partition, key),
+// and equal keys are summed by a segmented scan.  The key set then comes out in output order, so the
+// reduce-side sort (worker.rs:162-164) is skipped.  wc only (no doc component).
+//
+// Segments: [nreg * NB tail regions, s = b * nreg + w] [nreg flush regions] [NB overflow lists].
+__global__ void k_wide_counts(BucketArgs A, uint64_t *cnt) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nt = (uint64_t)A.nreg * MRG_NBUCKET;
+    if (s < nt) {
+        const uint32_t b = (uint32_t)(s / A.nreg), w = (uint32_t)(s % A.nreg);
+        cnt[s] = min(A.bcount[(uint64_t)w * MRG_NBUCKET + b], A.bcap[b]);
+    } else if (s < nt + A.nreg) {
+        const uint64_t w = s - nt;
+        cnt[s] = A.foff[w * (MRG_NBUCKET + 1) + MRG_NBUCKET];
+    } else if (s < nt + A.nreg + MRG_NBUCKET) {
+        const uint32_t b = (uint32_t)(s - nt - A.nreg);
+        cnt[s] = min(A.monext[b], A.mocap);
+    }
+}
+
+// one workgroup per segment; record -> SortRec{k0, k1, part, doc = 0, idx = count}
+__global__ void k_wide_gather(BucketArgs A, const uint64_t *off, uint32_t n_reduce, SortRec *out) {
+    const uint64_t s = blockIdx.x;
+    const uint64_t nt = (uint64_t)A.nreg * MRG_NBUCKET;
+    const uint64_t o = off[s], n = off[s + 1] - o;
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        uint64_t k0, k1;
+        uint32_t c = 1;
+        if (s < nt) {
+            const uint32_t b = (uint32_t)(s / A.nreg), w = (uint32_t)(s % A.nreg);
+            const uint64_t j = A.rbase[b] + (uint64_t)w * A.bcap[b] + i;
+            k0 = A.pool[2 * j];
+            k1 = A.pool[2 * j + 1];
+        } else if (s < nt + A.nreg) {
+            const uint64_t j = (s - nt) * A.regcap + i;
+            k0 = A.fk0[j];
+            k1 = A.fk1[j];
+            c = A.fcnt[j];
+        } else {
+            const uint64_t b = s - nt - A.nreg;
+            const uint64_t j = b * A.mocap + i;
+            k0 = A.movf[2 * j];
+            k1 = A.movf[2 * j + 1];
+        }
+        SortRec r;
+        r.k0 = k0;
+        r.k1 = k1;
+        r.part = (uint32_t)(mrg_siphash_short(k0, k1, mrg_short_len(k0, k1)) % (uint64_t)n_reduce);
+        r.doc = 0;
+        r.idx = c;
+        r.pad = 0;
+        out[o + i] = r;
+    }
+}
+
+__global__ void k_wide_heads(const SortRec *r, uint64_t n, uint64_t *head, uint64_t *cv) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    head[i] = (i == 0 || r[i].k0 != r[i - 1].k0 || r[i].k1 != r[i - 1].k1) ? 1u : 0u;  // part follows the key
+    cv[i] = r[i].idx;
+}
+
+// E = exclusive scan of head (run index), C = exclusive scan of counts.  The head of run k writes
+// the key and F[k] = its first record.
+__global__ void k_wide_keys(const SortRec *r, uint64_t n, const uint64_t *head, const uint64_t *E, KeySet ks,
+                            uint64_t *F) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !head[i]) return;
+    const uint64_t k = E[i];
+    ks.k0[k] = r[i].k0;
+    ks.k1[k] = r[i].k1;
+    ks.doc[k] = MRG_EMPTY_DOC;
+    ks.len[k] = mrg_short_len(r[i].k0, r[i].k1);
+    ks.part[k] = r[i].part;
+    ks.hoff[k] = MRG_NO_HEAP;
+    F[k] = i;
+}
+
+// count of run k = sum of the counts of its records (C[end] - C[first], C[n] = total)
+__global__ void k_wide_cnt(const uint64_t *F, uint64_t runs, uint64_t n, const uint64_t *C, uint64_t ctot, KeySet ks) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= runs) return;
+    const uint64_t e = k + 1 < runs ? C[F[k + 1]] : ctot;
+    ks.cnt[k] = e - C[F[k]];
+}
+
 // Long keys after the fingerprint sort: element i (sorted order) belongs to the run of equal
 // fingerprints; within the run its representative is the FIRST element with equal full key bytes
 // (and doc): the collision-safe tie-break, equal fingerprints never merge different strings.
@@ -501,6 +591,24 @@ void mrg_launch_export_pack(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t
 void mrg_launch_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, void *recs, hipStream_t s) {
     if (!n) return;
     hipLaunchKernelGGL(k_make_sortrec, grid_for(n), dim3(256), 0, s, ks, n, doc_rank, (SortRec *)recs);
+}
+void mrg_launch_wide_counts(const BucketArgs &a, uint64_t *cnt, uint64_t nseg, hipStream_t s) {
+    hipLaunchKernelGGL(k_wide_counts, grid_for(nseg), dim3(256), 0, s, a, cnt);
+}
+void mrg_launch_wide_gather(const BucketArgs &a, const uint64_t *off, uint64_t nseg, uint32_t n_reduce, SortRec *out,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_wide_gather, dim3((unsigned)nseg), dim3(256), 0, s, a, off, n_reduce, out);
+}
+void mrg_launch_wide_heads(const SortRec *r, uint64_t n, uint64_t *head, uint64_t *cv, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_wide_heads, grid_for(n), dim3(256), 0, s, r, n, head, cv);
+}
+void mrg_launch_wide_keys(const SortRec *r, uint64_t n, const uint64_t *head, const uint64_t *E, KeySet ks,
+                          uint64_t *F, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_wide_keys, grid_for(n), dim3(256), 0, s, r, n, head, E, ks, F);
+}
+void mrg_launch_wide_cnt(const uint64_t *F, uint64_t runs, uint64_t n, const uint64_t *C, uint64_t ctot, KeySet ks,
+                         hipStream_t s) {
+    if (runs) hipLaunchKernelGGL(k_wide_cnt, grid_for(runs), dim3(256), 0, s, F, runs, n, C, ctot, ks);
 }
 void mrg_launch_fill_u32(uint32_t *p, uint32_t v, uint64_t n, hipStream_t s) {
     if (!n) return;

@@ -141,6 +141,16 @@ struct BucketArgs {
     uint32_t hash_bits;
 };
 void mrg_launch_bucket_agg(const BucketArgs &a, bool indexer, hipStream_t s);
+// wide (sort-based) aggregation of the map records, wc only (k_keys.hip)
+struct SortRec;
+void mrg_launch_wide_counts(const BucketArgs &a, uint64_t *cnt, uint64_t nseg, hipStream_t s);
+void mrg_launch_wide_gather(const BucketArgs &a, const uint64_t *off, uint64_t nseg, uint32_t n_reduce, SortRec *out,
+                            hipStream_t s);
+void mrg_launch_wide_heads(const SortRec *r, uint64_t n, uint64_t *head, uint64_t *cv, hipStream_t s);
+void mrg_launch_wide_keys(const SortRec *r, uint64_t n, const uint64_t *head, const uint64_t *E, KeySet ks,
+                          uint64_t *F, hipStream_t s);
+void mrg_launch_wide_cnt(const uint64_t *F, uint64_t runs, uint64_t n, const uint64_t *C, uint64_t ctot, KeySet ks,
+                         hipStream_t s);
 void mrg_launch_table_clear(const TableArgs &t, bool indexer, hipStream_t s);
 void mrg_launch_table_insert(const TableArgs &t, const uint64_t *k0, const uint64_t *k1, const uint32_t *cnt32,
                              const uint32_t *doc, uint64_t n, bool indexer, hipStream_t s);

@@ -126,6 +126,7 @@ struct KeysBuf {
     uint8_t *heap = nullptr;
     uint64_t heap_bytes = 0;
     bool any_long = false;
+    bool sorted = false;  // keys already in (partition, key) order (wide aggregation, no long keys)
 };
 
 }  // namespace
@@ -376,6 +377,71 @@ void bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
     finish_keys(c);
 }
 
+uint32_t bytes_for(uint64_t maxval) {
+    uint32_t b = 0;
+    while (maxval) { ++b; maxval >>= 8; }
+    return b;
+}
+
+// Wide (sort-based) aggregation for high-cardinality inputs (k_keys.hip k_wide_*): every map
+// record is gathered with its partition, sorted by (partition, key) and summed per key; the key set
+// comes out in output order.
+void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap, LongItems li) {
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    BucketArgs B{};
+    B.pool = A.pool; B.rbase = A.rbase; B.bcap = A.bcap; B.bcount = A.bcount;
+    B.movf = A.ovf; B.monext = A.onext; B.mocap = A.ocap;
+    B.fk0 = A.fk0; B.fk1 = A.fk1; B.fcnt = A.fcnt; B.fdoc = A.fdoc; B.foff = A.foff;
+    B.nreg = nreg; B.regcap = regcap;
+    const uint64_t nseg = (uint64_t)nreg * MRG_NBUCKET + nreg + MRG_NBUCKET;
+    uint64_t *segc = pget<uint64_t>(p, nseg + 1), *sego = pget<uint64_t>(p, nseg + 1);
+    uint64_t *stmp1 = pget<uint64_t>(p, mrg_scan_tmp_elems(nseg + 1));
+    HIPCHK(hipMemsetAsync(segc + nseg, 0, 8, s));
+    mrg_launch_wide_counts(B, segc, nseg, s);
+    mrg_scan_u64(segc, sego, nseg + 1, stmp1, s);  // sego[nseg] = total
+    uint64_t n = 0;
+    HIPCHK(hipMemcpyAsync(&n, sego + nseg, 8, hipMemcpyDeviceToHost, s));
+    sync(c);
+    SortRec *a = pget<SortRec>(p, std::max<uint64_t>(n, 1)), *b = pget<SortRec>(p, std::max<uint64_t>(n, 1));
+    mrg_launch_wide_gather(B, sego, nseg, c->R, a, s);
+    p.put(segc); p.put(sego); p.put(stmp1);
+    SortPlan plan{};
+    plan.use_part = c->R > 1;
+    plan.part_bytes = bytes_for(c->R - 1);
+    plan.use_k0 = plan.use_k1 = true;
+    void *stmp = p.get(mrg_sort_tmp_bytes(n));
+    int passes = 0;
+    SortRec *r = mrg_radix_sort(a, b, n, plan, stmp, s, &passes);
+    p.put(stmp);
+    uint64_t *head = pget<uint64_t>(p, n + 1), *cv = pget<uint64_t>(p, n + 1);
+    uint64_t *E = pget<uint64_t>(p, n + 1), *C = pget<uint64_t>(p, n + 1);
+    uint64_t *stmp2 = pget<uint64_t>(p, mrg_scan_tmp_elems(n + 1));
+    mrg_launch_wide_heads(r, n, head, cv, s);
+    mrg_scan_u64(head, E, n, stmp2, s);
+    mrg_scan_u64(cv, C, n, stmp2, s);
+    uint64_t tail[4] = {0, 0, 0, 0};
+    if (n) {
+        HIPCHK(hipMemcpyAsync(&tail[0], E + (n - 1), 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&tail[1], head + (n - 1), 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&tail[2], C + (n - 1), 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&tail[3], cv + (n - 1), 8, hipMemcpyDeviceToHost, s));
+    }
+    sync(c);
+    const uint64_t runs = tail[0] + tail[1], ctot = tail[2] + tail[3];
+    keys_reserve(c, runs + li.n + 1);
+    uint64_t *F = pget<uint64_t>(p, runs + 1);
+    mrg_launch_wide_keys(r, n, head, E, c->keys.ks, F, s);
+    mrg_launch_wide_cnt(F, runs, n, C, ctot, c->keys.ks, s);
+    HIPCHK(hipMemcpyAsync(&c->d_cnt[CNT_KEYS], &runs, 8, hipMemcpyHostToDevice, s));
+    sync(c);  // `runs` is a host local
+    p.put(a); p.put(b); p.put(head); p.put(cv); p.put(E); p.put(C); p.put(stmp2); p.put(F);
+    c->st.overflow_keys = 0;
+    c->keys.sorted = li.n == 0;
+    long_aggregate(c, li);
+    finish_keys(c);
+}
+
 void need_job(mrg_ctx *c) {
     if (!c) raise(MRG_EINVAL, "null context");
     if (!c->job) raise(MRG_EINVAL, "no job: call mrg_job_begin first");
@@ -563,17 +629,15 @@ void job_map(mrg_ctx *c) {
     LongItems li{};
     li.base = c->d_in; li.start = M.lstart; li.rawlen = M.llen; li.doc = M.ldoc; li.cnt = nullptr;
     li.n = c->h_cnt[CNT_LONG];
-    bucket_aggregate(c, A, (uint32_t)grid, cap, li);
+    // high cardinality (most tokens missed the map-side combine): sort-based aggregation
+    bool wide = !idx && c->h_cnt[CNT_REC] > (32ull << 20) && 2 * c->h_cnt[CNT_REC] > c->h_cnt[CNT_TOKENS];
+    if (const char *v = getenv("MRG_WIDE")) wide = !idx && atoi(v) != 0;  // test / tuning override
+    if (wide) wide_aggregate(c, A, (uint32_t)grid, cap, li);
+    else bucket_aggregate(c, A, (uint32_t)grid, cap, li);
     ev_rec(c, 3);
     release_map();
     c->st.ms_aggregate = ev_ms(c, 2, 3);
     c->mapped = true;
-}
-
-uint32_t bytes_for(uint64_t maxval) {
-    uint32_t b = 0;
-    while (maxval) { ++b; maxval >>= 8; }
-    return b;
 }
 
 // Indexer document order = bytewise order of the names (the indexer reduce sorts its values):
@@ -659,7 +723,9 @@ void job_reduce(mrg_ctx *c) {
     ev_rec(c, 4);
     SortRec *a = pget<SortRec>(p, n), *b = pget<SortRec>(p, n);
     void *stmp = p.get(mrg_sort_tmp_bytes(n));
-    SortRec *sorted = sort_keys(c, c->keys.ks, c->R, dr.rank, a, b, stmp);
+    SortRec *sorted = a;
+    if (c->keys.sorted && !c->keys.any_long && !is_idx(c)) mrg_launch_make_sortrec(c->keys.ks, n, nullptr, a, s);
+    else sorted = sort_keys(c, c->keys.ks, c->R, dr.rank, a, b, stmp);
     ev_rec(c, 5);
     const FormatArgs f = format_args(c, sorted, c->keys.ks, c->R, compat_drop_last(c), dr);
     c->part_off.assign(c->R + 1, 0);

@@ -359,3 +359,49 @@ def test_run_job_writes_final_txt(tmp_path, corpus):
     finally:
         os.chdir(cwd)
     assert sha((tmp_path / "final.txt").read_bytes()) == GOLDEN["wc"]["10"]["final.txt"]
+
+
+# ---- wide (sort-based) aggregation: the high-cardinality path (C5) forced on small inputs
+
+@pytest.fixture
+def wide():
+    os.environ["MRG_WIDE"] = "1"
+    yield
+    del os.environ["MRG_WIDE"]
+
+
+@pytest.mark.parametrize("R", ["10", "64"])
+def test_wide_path_c1_golden(ctx, corpus, wide, R):
+    from gpu_util import run_wc
+    outs = run_wc(ctx, corpus, int(R))
+    g = GOLDEN["wc"][R]
+    assert [sha(o) for o in outs] == [g[f"mr-{r}.txt"] for r in range(int(R))]
+    assert sha(ctx.final()) == g["final.txt"]
+
+
+def test_wide_path_synthetic_and_unicode(ctx, wide):
+    import torch
+    import mapreduce_rust_amd as M
+    import oracle_lib as O
+    from gpu_util import run_wc
+    n = 8 << 20
+    t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
+    ctx.gen_unique(t.data_ptr(), n, 0xC5, 5)
+    host = t[:n].cpu().numpy().tobytes()
+    ctx.job_begin(M.APP_WC, 16)
+    ctx.set_input(t.data_ptr(), [0, n])
+    ctx.map()
+    ctx.reduce()
+    assert ctx.outputs() == O.wc([host], 16, O.FAST)
+    ctx.gen_zipf(t.data_ptr(), n, 0x5EED2026, 1, 1 << 14, 1.1)
+    host = t[:n].cpu().numpy().tobytes()
+    ctx.job_begin(M.APP_WC, 7)
+    ctx.set_input(t.data_ptr(), [0, n])
+    ctx.map()
+    ctx.reduce()
+    assert ctx.outputs() == O.wc([host], 7, O.FAST)
+    rnd = random.Random(11)
+    words = ["x" * k + e for k in (3, 16, 17, 40) for e in ("", "é", "q")] + ["naïve", "a", "don't"]
+    text = " ".join(rnd.choice(words) for _ in range(20000)).encode()
+    for flags in (0, M.debug_hash_bits(3)):
+        assert run_wc(ctx, [text], 5, flags=flags) == O.wc([text], 5, O.FAST), flags
