@@ -16,6 +16,9 @@
  *                  wc::reduce                                       src/app/wc.rs:15-17
  *   mrg_run_job    the whole mrcoordinator + N x mrworker run       src/bin/mrworker.rs:43-149,
  *                  (static plan instead of coordinator.rs:137-215 task assignment)
+ *   mrg_map_text   write_key_value_to_file, byte-exact mr-{m}-{r}.txt  src/mr/worker.rs:117-140
+ *   mrg_reduce_text read_file_to_mem_reduce over mr-{m}-{r}.txt      src/mr/worker.rs:79-109, 157-193
+ *   mrg_job_final  generate_output: cat mr-* | sort > final.txt     src/run.sh:16-20
  *   mrg_job_*      the same path with device-resident input, split at the shuffle so that a
  *                  multi-GPU host can exchange partitions between GPUs (RCCL all-to-all).
  */
@@ -141,13 +144,28 @@ void mrg_parts_free(mrg_parts *parts);
 int mrg_reduce(mrg_ctx *ctx, int app, uint32_t r, const mrg_parts *const *in, size_t k, uint32_t n_reduce,
                uint32_t flags, const char *const *doc_names, uint32_t n_docs, uint8_t **h_out, size_t *h_out_len);
 
+/* ---- the reference's text intermediates, byte for byte (wc) ---- */
+
+/* One map task writing mr-{m}-{r}.txt exactly as Worker::write_key_value_to_file does
+ * (src/mr/worker.rs:117-140): "{key} 1\n" for every token of wc::map (src/app/wc.rs:6-13) in input
+ * order, into file r = SipHash-1-3(key) % n_reduce (worker.rs:111-115, 129).  *h_out receives the
+ * n_reduce files' bytes concatenated (free with mrg_free); h_part_off[n_reduce + 1] their offsets. */
+int mrg_map_text(mrg_ctx *ctx, const uint8_t *h_bytes, size_t n, uint32_t n_reduce, uint8_t **h_out,
+                 uint64_t *h_part_off);
+/* One reduce task over k intermediate files' contents (Worker::read_file_to_mem_reduce + reduce,
+ * worker.rs:79-109, 157-193): UTF-8 checked (MRG_EUTF8), every non-empty line must be exactly
+ * "key value" (MRG_EINVAL, the reference's assert!), values counted per key (wc.rs:15-17), keys in
+ * byte order, the last group dropped unless MRG_FLAG_NO_COMPAT_DROP_LAST.  Returns mr-{r}.txt. */
+int mrg_reduce_text(mrg_ctx *ctx, const uint8_t *const *h_files, const uint64_t *h_sizes, size_t k, uint32_t flags,
+                    uint8_t **h_out, size_t *h_out_len);
+
 /* The whole job on one GPU: files are read, mapped, reduced; out_dir/mr-{r}.txt written (and
  * out_dir/final.txt with MRG_FLAG_FINAL_TXT).
  * Indexer document names are the file paths as given (the reference opens "data/gut-{m}.txt"). */
 int mrg_run_job(const char *const *files, size_t n_files, uint32_t n_reduce, int app, const char *out_dir,
                 uint32_t flags, int device);
 
-/* Free host memory returned by the library (mrg_reduce output). */
+/* Free host memory returned by the library (mrg_reduce / mrg_map_text / mrg_reduce_text output). */
 void mrg_free(void *p);
 
 /* ---- synthetic inputs for the benchmark (not on the data path) ---- */

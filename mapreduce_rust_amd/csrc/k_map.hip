@@ -1037,7 +1037,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
 // bytes; internal grouping only), packed prefix and key length.  Input was validated by k_map.
 __global__ void k_long_prep(const uint8_t *in, const uint64_t *lstart, const uint32_t *llen, uint64_t n,
                             uint64_t *ok0, uint64_t *ok1, uint32_t *oflen, uint64_t *oflen64, uint64_t *ofp,
-                            uint32_t hash_bits) {
+                            uint32_t hash_bits, int verbatim) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t a = lstart[i], e = a + llen[i];
@@ -1045,6 +1045,13 @@ __global__ void k_long_prep(const uint8_t *in, const uint64_t *lstart, const uin
     uint64_t k0 = 0, k1 = 0, h = 0xcbf29ce484222325ull;
     uint32_t L = 0;
     for (uint64_t p = a; p < e;) {
+        if (verbatim) {  // the range already holds exactly the key bytes (exchange heap, text key)
+            const uint32_t by = in[p++];
+            mrg_key_append(k0, k1, L, by);
+            h = (h ^ by) * 0x100000001b3ull;
+            ++L;
+            continue;
+        }
         uint32_t cp, raw;
         int l = mrg_utf8_decode(rd, p, e, &cp, &raw);
         if (!l) l = 1;  // cannot happen on validated input
@@ -1064,12 +1071,16 @@ __global__ void k_long_prep(const uint8_t *in, const uint64_t *lstart, const uin
 
 // Copy the filtered key bytes of long token i to heap[dst_off[i] ..).
 __global__ void k_long_gather(const uint8_t *in, const uint64_t *lstart, const uint32_t *llen, uint64_t n,
-                              const uint64_t *dst_off, uint8_t *heap) {
+                              const uint64_t *dst_off, uint8_t *heap, int verbatim) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t a = lstart[i], e = a + llen[i];
     auto rd = [&](uint64_t x) -> uint32_t { return in[x]; };
     uint8_t *dst = heap + dst_off[i];
+    if (verbatim) {
+        for (uint64_t p = a; p < e; ++p) *dst++ = in[p];
+        return;
+    }
     for (uint64_t p = a; p < e;) {
         uint32_t cp, raw;
         int l = mrg_utf8_decode(rd, p, e, &cp, &raw);
@@ -1118,15 +1129,15 @@ int mrg_map_max_grid(int app, int lds_cap, int device) {
 
 void mrg_launch_long_prep(const uint8_t *base, const uint64_t *start, const uint32_t *rawlen, uint64_t n,
                           uint64_t *k0, uint64_t *k1, uint32_t *flen, uint64_t *flen64, uint64_t *fp,
-                          uint32_t hash_bits, hipStream_t s) {
+                          uint32_t hash_bits, int verbatim, hipStream_t s) {
     if (!n) return;
     hipLaunchKernelGGL(k_long_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, base, start, rawlen, n, k0,
-                       k1, flen, flen64, fp, hash_bits);
+                       k1, flen, flen64, fp, hash_bits, verbatim);
 }
 
 void mrg_launch_long_gather(const uint8_t *base, const uint64_t *start, const uint32_t *rawlen, uint64_t n,
-                            const uint64_t *dst_off, uint8_t *heap, hipStream_t s) {
+                            const uint64_t *dst_off, uint8_t *heap, int verbatim, hipStream_t s) {
     if (!n) return;
     hipLaunchKernelGGL(k_long_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, base, start, rawlen, n,
-                       dst_off, heap);
+                       dst_off, heap, verbatim);
 }

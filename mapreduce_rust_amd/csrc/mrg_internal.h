@@ -107,6 +107,8 @@ struct LongItems {
     uint32_t *rawlen, *doc;
     uint64_t *cnt;               // null: 1 each
     uint64_t n;
+    int verbatim;                // 1: the ranges hold the key bytes exactly (exchange heap, text keys);
+                                 // 0: raw token bytes, X-class codepoints are dropped (wc.rs:7-8)
 };
 
 // ---- k_map.hip
@@ -117,9 +119,9 @@ int mrg_map_cap(int lds_cap);  // LDS-table entries per map workgroup actually u
 int mrg_map_max_grid(int app, int lds_cap, int device);
 void mrg_launch_long_prep(const uint8_t *base, const uint64_t *start, const uint32_t *rawlen, uint64_t n,
                           uint64_t *k0, uint64_t *k1, uint32_t *flen, uint64_t *flen64, uint64_t *fp,
-                          uint32_t hash_bits, hipStream_t s);
+                          uint32_t hash_bits, int verbatim, hipStream_t s);
 void mrg_launch_long_gather(const uint8_t *base, const uint64_t *start, const uint32_t *rawlen, uint64_t n,
-                            const uint64_t *dst_off, uint8_t *heap, hipStream_t s);
+                            const uint64_t *dst_off, uint8_t *heap, int verbatim, hipStream_t s);
 
 // ---- k_keys.hip
 struct BucketArgs {
@@ -220,6 +222,26 @@ void mrg_launch_fix_runs(SortRec *r, uint64_t n, KeySet ks, const uint8_t *heap,
 // final.txt: part2[key] = 1 for the keys the per-partition pass drops (drop-last), else 0.
 void mrg_launch_final_part(const SortRec *r, uint64_t n, KeySet ks, const uint8_t *heap, int drop_last,
                            uint32_t *part2, hipStream_t s);
+
+// ---- k_text.hip: the reference's text intermediates (mr-{m}-{r}.txt)
+struct TextTok {  // one token of a map task, input order
+    uint64_t k0, k1, start;
+    uint32_t rawlen, klen, part, pad;
+};
+uint64_t mrg_text_segments(uint64_t n);  // 64-byte segments (threads) over n bytes
+void mrg_launch_text_tok(const uint8_t *in, uint64_t n, uint32_t n_reduce, const uint64_t *base, uint64_t *cnt,
+                         TextTok *out, unsigned long long *err, hipStream_t s);
+void mrg_launch_text_keys(const TextTok *t, uint64_t n, uint64_t *part, uint32_t *idx, hipStream_t s);
+void mrg_launch_text_len(const TextTok *t, const uint32_t *idx, uint64_t n, uint64_t *L, hipStream_t s);
+void mrg_launch_text_part_off(const uint64_t *part, const uint64_t *O, uint64_t n, uint32_t R, uint64_t total,
+                              uint64_t *part_off, hipStream_t s);
+void mrg_launch_text_write(const uint8_t *in, const TextTok *t, const uint32_t *idx, uint64_t n, const uint64_t *O,
+                           uint8_t *out, hipStream_t s);
+void mrg_launch_utf8_check(const uint8_t *in, uint64_t n, unsigned long long *err, hipStream_t s);
+void mrg_launch_text_lines(const uint8_t *in, const uint64_t *fo, const uint64_t *fe, uint32_t nf, uint64_t nseg,
+                           const uint64_t *base, uint64_t *cnt, XRec *out, unsigned long long *err,
+                           unsigned long long *nempty, hipStream_t s);
+void mrg_launch_add_first(const SortRec *r, KeySet ks, uint64_t v, hipStream_t s);
 
 // ---- k_gen.hip
 int mrg_gen_zipf_impl(uint8_t *dst, uint64_t n, uint64_t seed, uint64_t file_index, uint32_t vocab, double s,

@@ -163,6 +163,7 @@ struct mrg_ctx {
     uint8_t *d_final = nullptr;     // final.txt (mrg_job_final)
     uint64_t final_cap = 0, final_bytes = 0;
     bool finalized = false;
+    uint64_t extra_first = 0;       // text reduce: values of empty-key lines, folded into the first group
     mrg_stats st{};
 };
 
@@ -264,7 +265,7 @@ void long_aggregate(mrg_ctx *c, LongItems li) {
         uint64_t *fl64 = pget<uint64_t>(p, n), *hoff = pget<uint64_t>(p, n), *acc = pget<uint64_t>(p, n);
         uint32_t *fl = pget<uint32_t>(p, n), *ix = pget<uint32_t>(p, n), *rep = pget<uint32_t>(p, n);
         uint64_t *scantmp = pget<uint64_t>(p, mrg_scan_tmp_elems(n));
-        mrg_launch_long_prep(li.base, li.start, li.rawlen, n, k0, k1, fl, fl64, fp, hash_bits(c), s);
+        mrg_launch_long_prep(li.base, li.start, li.rawlen, n, k0, k1, fl, fl64, fp, hash_bits(c), li.verbatim, s);
         mrg_scan_u64(fl64, hoff, n, scantmp, s);
         uint64_t last[2];
         HIPCHK(hipMemcpyAsync(&last[0], hoff + (n - 1), 8, hipMemcpyDeviceToHost, s));
@@ -273,7 +274,7 @@ void long_aggregate(mrg_ctx *c, LongItems li) {
         const uint64_t heap_bytes = last[0] + last[1];
         c->keys.heap = pget<uint8_t>(p, heap_bytes + 16);
         c->keys.heap_bytes = heap_bytes;
-        mrg_launch_long_gather(li.base, li.start, li.rawlen, n, hoff, c->keys.heap, s);
+        mrg_launch_long_gather(li.base, li.start, li.rawlen, n, hoff, c->keys.heap, li.verbatim, s);
         // fingerprint sort (collision-safe: k_long_group compares full bytes inside equal runs)
         uint64_t *fps = pget<uint64_t>(p, n);
         HIPCHK(hipMemcpyAsync(fps, fp, 8 * n, hipMemcpyDeviceToDevice, s));
@@ -462,6 +463,7 @@ void job_begin(mrg_ctx *c, int app, uint32_t R, uint32_t flags) {
     c->mapped = c->reduced = false;
     c->n_owners = 0;
     c->out_bytes = 0;
+    c->extra_first = 0;
     c->part_off.assign(R + 1, 0);
     c->final_bytes = 0;
     c->finalized = false;
@@ -726,6 +728,12 @@ void job_reduce(mrg_ctx *c) {
     SortRec *sorted = a;
     if (c->keys.sorted && !c->keys.any_long && !is_idx(c)) mrg_launch_make_sortrec(c->keys.ks, n, nullptr, a, s);
     else sorted = sort_keys(c, c->keys.ks, c->R, dr.rank, a, b, stmp);
+    // text reduce (worker.rs:169-173): lines with an empty key sort first and, since `prev` is still
+    // empty when the first real key arrives, their values join that key's group
+    if (c->extra_first && n) {
+        if (c->keys.any_long) mrg_launch_fix_runs(sorted, n, c->keys.ks, c->keys.heap, s);
+        mrg_launch_add_first(sorted, c->keys.ks, c->extra_first, s);
+    }
     ev_rec(c, 5);
     const FormatArgs f = format_args(c, sorted, c->keys.ks, c->R, compat_drop_last(c), dr);
     c->part_off.assign(c->R + 1, 0);
@@ -846,6 +854,7 @@ void job_import(mrg_ctx *c, const void *d_rec, uint64_t n_rec, const void *d_hea
     li.rawlen = pget<uint32_t>(p, n_rec);
     li.doc = pget<uint32_t>(p, n_rec);
     li.cnt = pget<uint64_t>(p, n_rec);
+    li.verbatim = 1;  // the exchange heap holds exact key bytes
     HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_LONG], 0, 8, s));
     mrg_launch_x_split_long((const XRec *)d_rec, n_rec, d_seg, d_seg + n_segs, n_segs, li, &c->d_cnt[CNT_LONG], s);
     read_counters(c);
@@ -875,6 +884,146 @@ void check_names(const char *const *names, uint32_t n) {
 }  // namespace
 
 // ===================================================================== C ABI
+
+// ---- text intermediates: the reference's mr-{m}-{r}.txt, byte for byte
+
+// One map task's intermediates: "key 1\n" per token in input order, partition by SipHash % R
+// (worker.rs:117-140).  out = the R files' bytes concatenated, off[R + 1] their offsets.
+void text_map(mrg_ctx *c, const uint8_t *h, uint64_t n, uint32_t R, std::vector<uint8_t> &out,
+              std::vector<uint64_t> &off) {
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    uint8_t *d = pget<uint8_t>(p, n + 64);
+    if (n) HIPCHK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s));
+    const uint64_t nseg = mrg_text_segments(n);
+    uint64_t *cnt = pget<uint64_t>(p, nseg + 1), *base = pget<uint64_t>(p, nseg + 1);
+    uint64_t *stmp = pget<uint64_t>(p, mrg_scan_tmp_elems(nseg + 1));
+    HIPCHK(hipMemsetAsync(cnt, 0, 8 * (nseg + 1), s));
+    HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_ERRPOS], 0xFF, 8, s));
+    mrg_launch_text_tok(d, n, R, nullptr, cnt, nullptr, &c->d_cnt[CNT_ERRPOS], s);
+    mrg_scan_u64(cnt, base, nseg + 1, stmp, s);
+    uint64_t T = 0;
+    HIPCHK(hipMemcpyAsync(&T, base + nseg, 8, hipMemcpyDeviceToHost, s));
+    read_counters(c);
+    auto done = [&]() { p.put(d); p.put(cnt); p.put(base); p.put(stmp); };
+    if (c->h_cnt[CNT_ERRPOS] != ~0ull) {
+        done();
+        raise(MRG_EUTF8, "stream did not contain valid UTF-8: byte offset %llu", (unsigned long long)c->h_cnt[CNT_ERRPOS]);
+    }
+    off.assign(R + 1, 0);
+    out.clear();
+    if (T) {
+        TextTok *tok = pget<TextTok>(p, T);
+        mrg_launch_text_tok(d, n, R, base, cnt, tok, &c->d_cnt[CNT_ERRPOS], s);
+        uint64_t *part = pget<uint64_t>(p, T), *kv = pget<uint64_t>(p, 4 * T);
+        uint32_t *idx = pget<uint32_t>(p, T);
+        void *stmp2 = p.get(mrg_sort_tmp_bytes(T));
+        mrg_launch_text_keys(tok, T, part, idx, s);
+        mrg_radix_sort_u64(part, idx, kv, T, stmp2, s);  // stable: input order inside a partition
+        uint64_t *L = pget<uint64_t>(p, T + 1), *O = pget<uint64_t>(p, T + 1);
+        uint64_t *stmp3 = pget<uint64_t>(p, mrg_scan_tmp_elems(T + 1));
+        mrg_launch_text_len(tok, idx, T, L, s);
+        mrg_scan_u64(L, O, T, stmp3, s);
+        uint64_t last[2];
+        HIPCHK(hipMemcpyAsync(&last[0], O + (T - 1), 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&last[1], L + (T - 1), 8, hipMemcpyDeviceToHost, s));
+        sync(c);
+        const uint64_t total = last[0] + last[1];
+        uint8_t *ob = pget<uint8_t>(p, total + 16);
+        uint64_t *doff = pget<uint64_t>(p, R + 1);
+        mrg_launch_text_write(d, tok, idx, T, O, ob, s);
+        mrg_launch_text_part_off(part, O, T, R, total, doff, s);
+        out.resize(total);
+        HIPCHK(hipMemcpyAsync(out.data(), ob, total, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(off.data(), doff, 8ull * (R + 1), hipMemcpyDeviceToHost, s));
+        sync(c);
+        p.put(tok); p.put(part); p.put(kv); p.put(idx); p.put(stmp2); p.put(L); p.put(O); p.put(stmp3);
+        p.put(ob); p.put(doff);
+    }
+    done();
+}
+
+// One reduce task from text intermediates (worker.rs:79-109, 157-193): returns mr-{r}.txt.
+void text_reduce(mrg_ctx *c, const uint8_t *const *files, const uint64_t *sizes, size_t k, uint32_t flags,
+                 std::vector<uint8_t> &out) {
+    job_begin(c, MRG_APP_WC, 1, flags);  // every key read goes to the one output file
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    std::vector<uint64_t> fo(k + 1, 0), fe(k);
+    for (size_t i = 0; i < k; ++i) {
+        fe[i] = fo[i] + sizes[i];
+        fo[i + 1] = (fe[i] + 63) & ~63ull;  // files on 64-byte boundaries (one file per segment)
+    }
+    const uint64_t total = fo[k];
+    uint8_t *d = pget<uint8_t>(p, total + 64);
+    HIPCHK(hipMemsetAsync(d, 0, total + 64, s));
+    for (size_t i = 0; i < k; ++i)
+        if (sizes[i]) HIPCHK(hipMemcpyAsync(d + fo[i], files[i], sizes[i], hipMemcpyHostToDevice, s));
+    const uint32_t nf = (uint32_t)std::max<size_t>(k, 1);
+    uint64_t *dfo = pget<uint64_t>(p, nf + 1), *dfe = pget<uint64_t>(p, nf);
+    if (k) {
+        HIPCHK(hipMemcpyAsync(dfo, fo.data(), 8 * k, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(dfe, fe.data(), 8 * k, hipMemcpyHostToDevice, s));
+    }
+    unsigned long long *err = pget<unsigned long long>(p, 3);  // [utf8 pos, format pos, empty-key lines]
+    HIPCHK(hipMemsetAsync(err, 0xFF, 16, s));
+    HIPCHK(hipMemsetAsync(err + 2, 0, 8, s));
+    mrg_launch_utf8_check(d, total, err, s);  // read_to_string (worker.rs:93); zero padding is valid
+    const uint64_t nseg = total / 64;
+    uint64_t *cnt = pget<uint64_t>(p, nseg + 1), *base = pget<uint64_t>(p, nseg + 1);
+    uint64_t *stmp = pget<uint64_t>(p, mrg_scan_tmp_elems(nseg + 1));
+    HIPCHK(hipMemsetAsync(cnt, 0, 8 * (nseg + 1), s));
+    if (k) mrg_launch_text_lines(d, dfo, dfe, nf, nseg, nullptr, cnt, nullptr, err, err + 2, s);
+    mrg_scan_u64(cnt, base, nseg + 1, stmp, s);
+    std::vector<uint64_t> fb(k + 1, 0);  // records before file i = base[fo[i] / 64]
+    for (size_t i = 0; i <= k; ++i) HIPCHK(hipMemcpyAsync(&fb[i], base + fo[i] / 64, 8, hipMemcpyDeviceToHost, s));
+    unsigned long long herr[3];
+    HIPCHK(hipMemcpyAsync(herr, err, sizeof herr, hipMemcpyDeviceToHost, s));
+    sync(c);
+    auto done = [&]() { p.put(d); p.put(dfo); p.put(dfe); p.put(err); p.put(cnt); p.put(base); p.put(stmp); };
+    auto where = [&](uint64_t pos, uint64_t &f) {
+        f = 0;
+        while (f + 1 < k && fo[f + 1] <= pos) ++f;
+        return pos - fo[f];
+    };
+    if (herr[0] != ~0ull) {
+        uint64_t f;
+        const uint64_t at = where(herr[0], f);
+        done();
+        raise(MRG_EUTF8, "intermediate file %llu is not valid UTF-8 (byte offset %llu)", (unsigned long long)f,
+              (unsigned long long)at);
+    }
+    if (herr[1] != ~0ull) {
+        uint64_t f;
+        const uint64_t at = where(herr[1], f);
+        done();
+        raise(MRG_EINVAL, "intermediate file %llu: the line at byte %llu does not split into `key value` "
+              "(worker.rs:100 asserts two space-separated fields; keys hold no NUL)", (unsigned long long)f,
+              (unsigned long long)at);
+    }
+    const uint64_t N = fb[k];
+    XRec *x = pget<XRec>(p, std::max<uint64_t>(N, 1));
+    if (k) mrg_launch_text_lines(d, dfo, dfe, nf, nseg, base, cnt, x, err, err + 2, s);  // also counts empty keys
+    HIPCHK(hipMemcpyAsync(&herr[2], err + 2, 8, hipMemcpyDeviceToHost, s));
+    sync(c);
+    std::vector<uint64_t> seg_rec(nf, 0), seg_heap(nf, 0);
+    for (size_t i = 0; i < k; ++i) {
+        seg_rec[i] = fb[i + 1] - fb[i];
+        seg_heap[i] = fo[i + 1] - fo[i];  // heap segment of file i = its slot in the buffer
+    }
+    job_import(c, x, N, d, k ? total : 0, seg_rec.data(), seg_heap.data(), nf);
+    c->extra_first = herr[2];
+    job_reduce(c);
+    out.resize(c->out_bytes);
+    if (c->out_bytes) HIPCHK(hipMemcpyAsync(out.data(), c->d_out, c->out_bytes, hipMemcpyDeviceToHost, s));
+    sync(c);
+    if (c->keys.n == 0 && herr[2] && (flags & MRG_FLAG_NO_COMPAT_DROP_LAST)) {  // only empty keys, group kept
+        const std::string line = " " + std::to_string(herr[2]) + "\n";
+        out.assign(line.begin(), line.end());
+    }
+    p.put(x);
+    done();
+}
 
 extern "C" {
 
@@ -1029,6 +1178,41 @@ int mrg_job_copy_final(mrg_ctx *c, uint8_t *h_dst, uint64_t cap) {
         if (c->final_bytes)
             HIPCHK(hipMemcpyAsync(h_dst, c->d_final, c->final_bytes, hipMemcpyDeviceToHost, c->stream));
         sync(c);
+    });
+}
+
+// ---- text intermediates
+int mrg_map_text(mrg_ctx *c, const uint8_t *h_bytes, size_t n, uint32_t n_reduce, uint8_t **h_out,
+                 uint64_t *h_part_off) {
+    return guard([&] {
+        if (!c || !h_out || !h_part_off || (n && !h_bytes)) raise(MRG_EINVAL, "null argument");
+        if (n_reduce == 0) raise(MRG_EINVAL, "n_reduce must be > 0");
+        HIPCHK(hipSetDevice(c->device));
+        std::vector<uint8_t> out;
+        std::vector<uint64_t> off;
+        text_map(c, h_bytes, n, n_reduce, out, off);
+        uint8_t *o = (uint8_t *)malloc(out.size() + 1);
+        if (!o) raise(MRG_ENOMEM, "host allocation failed");
+        if (!out.empty()) memcpy(o, out.data(), out.size());
+        memcpy(h_part_off, off.data(), 8ull * (n_reduce + 1));
+        *h_out = o;
+    });
+}
+
+int mrg_reduce_text(mrg_ctx *c, const uint8_t *const *h_files, const uint64_t *h_sizes, size_t k, uint32_t flags,
+                    uint8_t **h_out, size_t *h_out_len) {
+    return guard([&] {
+        if (!c || !h_out || !h_out_len || (k && (!h_files || !h_sizes))) raise(MRG_EINVAL, "null argument");
+        for (size_t i = 0; i < k; ++i)
+            if (h_sizes[i] && !h_files[i]) raise(MRG_EINVAL, "null file %zu", i);
+        HIPCHK(hipSetDevice(c->device));
+        std::vector<uint8_t> out;
+        text_reduce(c, h_files, h_sizes, k, flags, out);
+        uint8_t *o = (uint8_t *)malloc(out.size() + 1);
+        if (!o) raise(MRG_ENOMEM, "host allocation failed");
+        if (!out.empty()) memcpy(o, out.data(), out.size());
+        *h_out = o;
+        *h_out_len = out.size();
     });
 }
 

@@ -77,6 +77,9 @@ _SIGS = {
     "mrg_parts_free": (None, [_vp]),
     "mrg_reduce": (C.c_int, [_vp, C.c_int, C.c_uint32, C.POINTER(_vp), C.c_size_t, C.c_uint32, C.c_uint32,
                              C.POINTER(C.c_char_p), C.c_uint32, C.POINTER(_vp), C.POINTER(C.c_size_t)]),
+    "mrg_map_text": (C.c_int, [_vp, C.c_char_p, C.c_size_t, C.c_uint32, C.POINTER(_vp), _u64p]),
+    "mrg_reduce_text": (C.c_int, [_vp, C.POINTER(C.c_char_p), _u64p, C.c_size_t, C.c_uint32, C.POINTER(_vp),
+                                  C.POINTER(C.c_size_t)]),
     "mrg_run_job": (C.c_int, [C.POINTER(C.c_char_p), C.c_size_t, C.c_uint32, C.c_int, C.c_char_p, C.c_uint32,
                               C.c_int]),
     "mrg_free": (None, [_vp]),
@@ -259,6 +262,27 @@ class Context:
         n = C.c_size_t()
         _check(load().mrg_reduce(self.h, app, r, arr, len(parts), n_reduce, flags, names, len(doc_names),
                                  C.byref(out), C.byref(n)))
+        data = C.string_at(out, n.value) if n.value else b""
+        load().mrg_free(out)
+        return data
+
+    # ---- the reference's text intermediates (wc)
+    def map_text(self, data, n_reduce):
+        """mr-{m}-{r}.txt contents of one map task (worker.rs:117-140), for r < n_reduce."""
+        out = _vp()
+        off = (C.c_uint64 * (n_reduce + 1))()
+        _check(load().mrg_map_text(self.h, data, len(data), n_reduce, C.byref(out), off))
+        blob = C.string_at(out, off[n_reduce]) if off[n_reduce] else b""
+        load().mrg_free(out)
+        return [blob[off[r]:off[r + 1]] for r in range(n_reduce)]
+
+    def reduce_text(self, files, flags=0):
+        """mr-{r}.txt from the contents of the intermediate files mr-{m}-{r}.txt (worker.rs:79-109)."""
+        arr = (C.c_char_p * max(len(files), 1))(*files)
+        sizes = _u64arr([len(f) for f in files])
+        out = _vp()
+        n = C.c_size_t()
+        _check(load().mrg_reduce_text(self.h, arr, sizes, len(files), flags, C.byref(out), C.byref(n)))
         data = C.string_at(out, n.value) if n.value else b""
         load().mrg_free(out)
         return data

@@ -2,14 +2,15 @@
 
 Same task structure and file conventions as the reference:
   Worker(map_n, reduce_n)                     worker.rs:28-37
-  Worker.map(m):    data/gut-{m}.txt  ->  mr-{m}-{r}.rec for r < reduce_n     worker.rs:142-155
-  Worker.reduce(r): mr-{m}-{r}.rec for m < map_n  ->  mr-{r}.txt              worker.rs:157-193
-Map output per partition is the engine's combined form (per-key counts as 40-byte exchange
-records + long-key heap, include/mrgpu.h) instead of one "key 1" text line per token; mr-{r}.txt
-is byte-identical to the reference's.  A map task and a reduce task may run in different
+  Worker.map(m):    data/gut-{m}.txt  ->  mr-{m}-{r}.txt for r < reduce_n     worker.rs:142-155
+  Worker.reduce(r): mr-{m}-{r}.txt for m < map_n  ->  mr-{r}.txt              worker.rs:157-193
+intermediates="text" (default, wc): mr-{m}-{r}.txt byte-identical to the reference's ("key 1" per
+token in input order, mrg_map_text / mrg_reduce_text), so GPU and reference CPU workers can take
+each other's tasks.  intermediates="records": the engine's combined form, mr-{m}-{r}.rec (per-key
+counts as 40-byte exchange records + long-key heap, include/mrgpu.h; little-endian u64 n_records,
+u64 heap_bytes, records, heap) -- far smaller, and the only form for the indexer.  mr-{r}.txt is
+byte-identical to the reference's either way.  A map task and a reduce task may run in different
 processes, as in the reference (the files in the working directory are the hand-off).
-
-Record file layout (little-endian): u64 n_records, u64 heap_bytes, records, heap.
 """
 import os
 import struct
@@ -23,14 +24,23 @@ def _rec_path(m, r, cwd):
     return os.path.join(cwd, f"mr-{m}-{r}.rec")
 
 
+def _txt_path(m, r, cwd):
+    return os.path.join(cwd, f"mr-{m}-{r}.txt")      # worker.rs:120
+
+
 class Worker:
-    def __init__(self, map_n, reduce_n, app="wc", device=0, flags=0, cwd="."):
+    def __init__(self, map_n, reduce_n, app="wc", device=0, flags=0, cwd=".", intermediates=None):
         if app not in APPS:
             raise ValueError(f"unknown app {app!r}")
+        if intermediates is None:
+            intermediates = "text" if app == "wc" else "records"
+        if intermediates not in ("text", "records") or (intermediates == "text" and app != "wc"):
+            raise ValueError(f"intermediates={intermediates!r} not available for app {app!r}")
         self.map_n, self.reduce_n = map_n, reduce_n
         self.app = APPS[app]
         self.flags = flags
         self.cwd = cwd
+        self.text = intermediates == "text"
         self.ctx = native.Context(device)
 
     def doc_name(self, m):
@@ -40,6 +50,11 @@ class Worker:
         """Map task m: the input file's bytes -> per-partition records."""
         with open(os.path.join(self.cwd, self.doc_name(m)), "rb") as f:   # worker.rs:73-75
             data = f.read()
+        if self.text:
+            for r, blob in enumerate(self.ctx.map_text(data, self.reduce_n)):
+                with open(_txt_path(m, r, self.cwd), "wb") as f:
+                    f.write(blob)
+            return True
         parts = self.ctx.map_task(self.app, data, self.doc_name(m), m, self.reduce_n, self.flags)
         try:
             for r in range(self.reduce_n):                                 # worker.rs:120-125
@@ -54,7 +69,15 @@ class Worker:
 
     def reduce(self, r):
         """Reduce task r: every map task's records of partition r -> mr-{r}.txt."""
-        import ctypes
+        if self.text:
+            files = []
+            for m in range(self.map_n):                                    # worker.rs:84-93
+                with open(_txt_path(m, r, self.cwd), "rb") as f:
+                    files.append(f.read())
+            out = self.ctx.reduce_text(files, self.flags)
+            with open(os.path.join(self.cwd, f"mr-{r}.txt"), "wb") as f:   # worker.rs:167-168
+                f.write(out)
+            return True
         recs, heaps, seg_r, seg_h = [], [], [], []
         for m in range(self.map_n):                                        # worker.rs:84-107
             with open(_rec_path(m, r, self.cwd), "rb") as f:

@@ -268,10 +268,10 @@ def test_worker_tasks_through_files(tmp_path, corpus):
     (tmp_path / "data").mkdir()
     for m in range(6):
         (tmp_path / "data" / f"gut-{m}.txt").write_bytes(corpus[m])
-    w = Worker(6, 10, cwd=str(tmp_path))
+    w = Worker(6, 10, cwd=str(tmp_path), intermediates="records")
     for m in range(6):
         assert w.map(m)
-    w2 = Worker(6, 10, cwd=str(tmp_path))   # a second worker process would do the same
+    w2 = Worker(6, 10, cwd=str(tmp_path), intermediates="records")   # a second worker process would do the same
     for r in range(10):
         assert w2.reduce(r)
         assert sha((tmp_path / f"mr-{r}.txt").read_bytes()) == GOLDEN["wc"]["10"][f"mr-{r}.txt"], r
@@ -405,3 +405,99 @@ def test_wide_path_synthetic_and_unicode(ctx, wide):
     text = " ".join(rnd.choice(words) for _ in range(20000)).encode()
     for flags in (0, M.debug_hash_bits(3)):
         assert run_wc(ctx, [text], 5, flags=flags) == O.wc([text], 5, O.FAST), flags
+
+
+# ---- the reference's text intermediates mr-{m}-{r}.txt
+
+def _ref_reduce(files, drop_last=True):
+    """worker.rs:79-109 + 157-193 restated over intermediate file contents (wc::reduce = len)."""
+    kvs = []
+    for c in files:
+        for line in c.decode("utf-8").split("\n"):
+            if not line:
+                continue
+            f = line.split(" ")
+            assert len(f) == 2
+            kvs.append((f[0], f[1]))
+    kvs.sort(key=lambda kv: kv[0].encode())
+    out, prev, vals = [], "", []
+    for k, v in kvs:
+        if prev == "":
+            prev = k
+        if k != prev:
+            out.append(f"{prev} {len(vals)}\n")
+            vals = []
+            prev = k
+        vals.append(v)
+    if not drop_last and vals:
+        out.append(f"{prev} {len(vals)}\n")
+    return "".join(out).encode()
+
+
+@pytest.mark.parametrize("R", ["10", "1", "3", "64"])
+def test_map_text_golden_intermediates(ctx, corpus, R):
+    n = int(R)
+    blobs = []
+    for m in range(6):
+        blobs += ctx.map_text(corpus[m], n)
+    assert sha(b"".join(blobs)) == GOLDEN["wc"][R]["intermediates"]
+    outs = [ctx.reduce_text([blobs[m * n + r] for m in range(6)]) for r in range(n)]
+    assert [sha(o) for o in outs] == [GOLDEN["wc"][R][f"mr-{r}.txt"] for r in range(n)]
+
+
+def test_map_text_unicode_and_long_tokens(ctx):
+    import oracle_lib as O
+    rnd = random.Random(5)
+    words = ["x" * k + e for k in (3, 16, 17, 40) for e in ("", "é", "q")] + ["naïve", "a", "don't", "--", "ſong",
+                                                                              "«quoted»", "1685-1732"]
+    seps = [" ", "\n", "\t", "　", "   "]
+    text = "".join(rnd.choice(words) + rnd.choice(seps) for _ in range(30000)).encode()
+    for n in (1, 7):
+        parts = ctx.map_text(text, n)
+        assert [ctx.reduce_text([p]) for p in parts] == [_ref_reduce([p]) for p in parts]
+        assert [ctx.reduce_text([p]) for p in parts] == O.wc([text], n, O.FAST)
+
+
+def test_reduce_text_edge_cases(ctx):
+    import mapreduce_rust_amd as M
+    cases = [
+        [b"b 1\na 1\n", b"a 1\nc 7\n\n\nb x\n"],          # values other than "1" still count 1 each
+        [b" 1\n 1\nzz 1\nab 1\n"],                        # empty keys join the first group (prev == "")
+        [b" 1\n"],                                        # only empty keys
+        [b"a-b 1\nx\xc3\xa9y 1\na-b 1\nq 1"],             # non-\w key bytes kept verbatim, no final \n
+        [("k" * 40 + " 1\n").encode() * 3 + ("k" * 39 + "j 1\n").encode() + b"z 1\n"],  # long keys
+        [b"", b"\n\n", b"w 1\n"],                         # empty files and empty lines
+        [],
+    ]
+    for files in cases:
+        for flags, drop in ((0, True), (M.FLAG_NO_COMPAT_DROP_LAST, False)):
+            assert ctx.reduce_text(files, flags) == _ref_reduce(files, drop), (files, flags)
+
+
+def test_reduce_text_errors(ctx):
+    import mapreduce_rust_amd as M
+    for files, code in (([b"a b c\n"], M.native.EINVAL), ([b"abc\n"], M.native.EINVAL),
+                        ([b"a 1\n", b"\xff 1\n"], M.native.EUTF8), ([b"a\x00b 1\n"], M.native.EINVAL)):
+        with pytest.raises(M.MrgError) as ei:
+            ctx.reduce_text(files)
+        assert ei.value.code == code, files
+    with pytest.raises(M.MrgError) as ei:
+        ctx.map_text(b"ok \xe2\x82 bad", 4)
+    assert ei.value.code == M.native.EUTF8
+
+
+def test_worker_text_intermediates_through_files(tmp_path, corpus):
+    """Reference task structure with the reference's own intermediate files (default for wc)."""
+    from mapreduce_rust_amd.worker import Worker
+    (tmp_path / "data").mkdir()
+    for m in range(6):
+        (tmp_path / "data" / f"gut-{m}.txt").write_bytes(corpus[m])
+    w = Worker(6, 10, cwd=str(tmp_path))
+    for m in range(6):
+        assert w.map(m)
+    inter = b"".join((tmp_path / f"mr-{m}-{r}.txt").read_bytes() for m in range(6) for r in range(10))
+    assert sha(inter) == GOLDEN["wc"]["10"]["intermediates"]
+    for r in range(10):
+        assert w.reduce(r)
+        assert sha((tmp_path / f"mr-{r}.txt").read_bytes()) == GOLDEN["wc"]["10"][f"mr-{r}.txt"], r
+    w.close()
