@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--cpu-sample-mib", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lds-cap", type=int, default=0)
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl = RCCL over xGMI (the product); gloo = host-staged exchange, for rehearsing N > 1 "
+                         "with several ranks on one GPU")
     return ap.parse_args()
 
 
@@ -77,17 +80,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = local % max(1, torch.cuda.device_count())  # = local on a node with one GPU per rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     files = a.files_per_gpu or (40 if world == 1 else 50)
     fbytes = a.file_mib * MIB
     shard = files * fbytes
 
     if a.lds_cap:
         os.environ["MRG_LDS_CAP"] = str(a.lds_cap)
-    ctx = M.Context(local)
+    ctx = M.Context(gpu)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     buf = torch.empty(shard + 64, dtype=torch.uint8, device=dev)
     for i in range(files):

@@ -31,6 +31,11 @@ def alltoall_exchange(send_rec, send_heap, rec_counts, heap_counts, group=None):
     Returns (recv_rec, recv_heap, recv_rec_counts, recv_heap_counts), ordered by sender."""
     world = dist.get_world_size(group)
     dev = send_rec.device
+    if dev.type == "cuda" and dist.get_backend(group) == "gloo":
+        # gloo moves host tensors only: stage through host memory (rehearsal of N > 1 on one GPU;
+        # the product path is RCCL, which exchanges device buffers directly)
+        rr, rh, r_rec, r_heap = alltoall_exchange(send_rec.cpu(), send_heap.cpu(), rec_counts, heap_counts, group)
+        return rr.to(dev), rh.to(dev), r_rec, r_heap
     counts = torch.tensor(list(rec_counts) + list(heap_counts), dtype=torch.int64, device=dev)
     # [rec_0..rec_{G-1}, heap_0..heap_{G-1}] -> per destination (rec_o, heap_o) pairs
     send_c = counts.view(2, world).t().contiguous().view(-1)
