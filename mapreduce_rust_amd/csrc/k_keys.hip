@@ -55,7 +55,7 @@ struct alignas(16) BaKey {
 template <bool IDX>
 __device__ __forceinline__ bool ba_add(BaKey *key, unsigned long long *cnt, unsigned int *doc, uint64_t a,
                                        uint64_t b, uint32_t d, uint64_t c, uint32_t h) {
-    uint32_t slot = (h >> 11) & (BA_CAP - 1);  // bits disjoint from the bucket (top 9)
+    uint32_t slot = (h >> (20 - MRG_NBUCKET_LOG2)) & (BA_CAP - 1);  // the 12 bits below the bucket bits
     for (int p = 0; p < BA_PROBE; ++p) {
         const BaKey k = key[slot];
         const bool dk = !IDX || doc[slot] == d;

@@ -667,6 +667,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // wave's LDS window
     // phase clocks (MRG_PROF only; wave-uniform): 0 wait for the block's loads, 1 classify,
     // 2 stage + scan + queue, 3 token rounds, 4 slow tokens, 5 non-ASCII tiles, 6 flush
+    // (a diagnostic build only: -DMRG_MAP_PROF; the accumulators would otherwise take 16 SGPRs of
+    // a kernel that already spills SGPRs)
+#ifdef MRG_MAP_PROF
     const bool P = A.prof != nullptr;
     uint64_t pacc[7] = {0, 0, 0, 0, 0, 0, 0}, tl = P ? clock64() : 0;
 #define MRG_PT(i)                          \
@@ -675,6 +678,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         pacc[i] += t_ - tl;                \
         tl = t_;                           \
     }
+#else
+#define MRG_PT(i)
+#endif
     auto process_blk = [&](const BlkInfo &I, const Blk &X, uint64_t cblk, auto &&mid) {
         const uint64_t Ab = I.Ab, doc_lo = I.doc_lo, doc_hi = I.doc_hi;
         const uint32_t docid = I.docid;
@@ -730,6 +736,10 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         // acknowledgements too
         mid();
         MRG_PT(0);
+        if (abl & 32u) {  // timing only: classification alone
+            my_tokens += (m0 ^ m1 ^ mh ^ prev_blk) & 1u;
+            return;
+        }
 
 #pragma unroll 1
         for (uint32_t j = 0; j < NSUB; ++j) {
@@ -778,12 +788,16 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const uint32_t cnt = __builtin_popcount(st);
             const uint32_t incl = wave_incl_scan(cnt);
             uint32_t pos = incl - cnt;
+            if (abl & 64u) {  // timing only: no queue writes, no tokens
+                my_tokens += st & 1u;
+                st = 0;
+            }
             while (st) {
                 const uint32_t kb = (uint32_t)__builtin_ctz(st);
                 st &= st - 1u;
                 queue[pos++] = (uint16_t)(l16 + kb);
             }
-            const uint32_t total = (abl & 4u) ? 0u : lane_u32(incl, 63);
+            const uint32_t total = (abl & 68u) ? 0u : lane_u32(incl, 63);
             MRG_PT(2);
             uint32_t nslow = 0;
             my_tokens += (abl & 4u) ? cnt : 0u;
@@ -1028,9 +1042,11 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         g_add(&A.counters[CNT_REC], (unsigned long long)ttl);
     }
     MRG_PT(6);
+#ifdef MRG_MAP_PROF
     if (P && lane == 0) {
         for (int i = 0; i < 7; ++i) g_add(&A.prof[i], (unsigned long long)pacc[i]);
     }
+#endif
 }
 
 // Long tokens: filter the raw token bytes (drop X codepoints), fingerprint (FNV-1a-64 of the key
@@ -1098,14 +1114,24 @@ static void launch_map_t(const MapArgs *a, int grid, hipStream_t s) {
     hipLaunchKernelGGL((k_map<CAP, IDX>), dim3(grid), dim3(WG), 0, s, a);
 }
 
+static int map_cap_for(int app, int lds_cap) {
+    (void)app;
+    return lds_cap >= 4096 ? 4096 : 2048;
+}
+
 void mrg_launch_map(const MapArgs &h, MapArgs *a, int app, int grid, int lds_cap, hipStream_t s) {
     const bool idx = app == 1;
     (void)hipMemcpyAsync(a, &h, sizeof(MapArgs), hipMemcpyHostToDevice, s);
-    if (lds_cap >= 4096) { if (idx) launch_map_t<4096, true>(a, grid, s); else launch_map_t<4096, false>(a, grid, s); }
-    else { if (idx) launch_map_t<2048, true>(a, grid, s); else launch_map_t<2048, false>(a, grid, s); }
+    if (map_cap_for(app, lds_cap) == 4096) {
+        if (idx) launch_map_t<4096, true>(a, grid, s);
+        else launch_map_t<4096, false>(a, grid, s);
+    } else {
+        if (idx) launch_map_t<2048, true>(a, grid, s);
+        else launch_map_t<2048, false>(a, grid, s);
+    }
 }
 
-int mrg_map_cap(int lds_cap) { return lds_cap >= 4096 ? 4096 : 2048; }
+int mrg_map_cap(int app, int lds_cap) { return map_cap_for(app, lds_cap); }
 
 // BLK-byte blocks of a document [lo, hi): on the 16-byte grid starting at lo & ~15
 uint64_t mrg_map_tiles(uint64_t lo, uint64_t hi) {
@@ -1117,12 +1143,12 @@ int mrg_map_max_grid(int app, int lds_cap, int device) {
     int ncu = 256;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
     int per = 1;
-    const bool idx = app == 1;
     hipError_t e;
-    if (lds_cap >= 4096) e = idx ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<4096, true>, WG, 0)
-                                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<4096, false>, WG, 0);
-    else e = idx ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<2048, true>, WG, 0)
-                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<2048, false>, WG, 0);
+    if (map_cap_for(app, lds_cap) == 4096)
+        e = app == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<4096, true>, WG, 0)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<4096, false>, WG, 0);
+    else if (app == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<2048, true>, WG, 0);
+    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<2048, false>, WG, 0);
     if (e != hipSuccess || per < 1) per = 1;
     return ncu * per;
 }

@@ -75,7 +75,8 @@ struct MapArgs {
                                  // 1 = no tail-record stores, 2 = no LDS-table probe (all tokens
                                  // become tail records), 4 = no per-token work after the queue,
                                  // 8 = every block loads its document's first block (L2-resident),
-                                 // 16 = no LDS count add on table hits
+                                 // 16 = no LDS count add on table hits, 32 = classification
+                                 // only, 64 = no queue writes (and no tokens)
     unsigned long long *prof;    // perf diagnostics (env MRG_PROF): per-phase wave clocks, [7]; else null
 };
 
@@ -115,7 +116,7 @@ struct LongItems {
 // `dev_args` is device memory for one MapArgs (the kernel reads its arguments from there)
 void mrg_launch_map(const MapArgs &a, MapArgs *dev_args, int app, int grid, int lds_cap, hipStream_t s);
 uint64_t mrg_map_tiles(uint64_t doc_lo, uint64_t doc_hi);  // wave blocks (NSUB KiB) of a document (16-B grid)
-int mrg_map_cap(int lds_cap);  // LDS-table entries per map workgroup actually used for lds_cap
+int mrg_map_cap(int app, int lds_cap);  // LDS-table entries per map workgroup actually used for lds_cap
 int mrg_map_max_grid(int app, int lds_cap, int device);
 void mrg_launch_long_prep(const uint8_t *base, const uint64_t *start, const uint32_t *rawlen, uint64_t n,
                           uint64_t *k0, uint64_t *k1, uint32_t *flen, uint64_t *flen64, uint64_t *fp,

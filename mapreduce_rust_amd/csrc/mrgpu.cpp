@@ -491,7 +491,7 @@ void job_map(mrg_ctx *c) {
 
     if (!c->map_grid) c->map_grid = mrg_map_max_grid(c->app, c->lds_cap, c->device);
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->map_grid, n_chunks));
-    const uint32_t cap = (uint32_t)mrg_map_cap(c->lds_cap);
+    const uint32_t cap = (uint32_t)mrg_map_cap(c->app, c->lds_cap);
     const bool idx = is_idx(c);
     const uint32_t RW = idx ? 3u : 2u;
     uint64_t lcap = std::max<uint64_t>(c->long_hint, total / 1024 + 1024);
