@@ -741,7 +741,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             return;
         }
 
-#pragma unroll 1
+#pragma unroll
         for (uint32_t j = 0; j < NSUB; ++j) {
             const uint64_t At = Ab + (uint64_t)j * TILE;
             if (At >= doc_hi) break;
