@@ -358,7 +358,6 @@ __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint3
     const uint32_t gA = actA ? (hA & (NG - 1)) : 0u, gB = actB ? (hB & (NG - 1)) : 0u;
     const uint32_t tgA = ((hA >> 16) & 0x7Fu) | 0x80u, tgB = ((hB >> 16) & 0x7Fu) | 0x80u;
     const uint32_t bA = bucket_of(hA), bB = bucket_of(hB);
-    const uint32_t capA = bcap[bA], capB = bcap[bB];  // independent of the probe: issued early
     const uint64_t tagsA = T.tag[gA], tagsB = T.tag[gB];
     auto rep = [](uint32_t tg) {
         const uint32_t r32 = __builtin_amdgcn_perm(0u, tg, 0u);  // tg in every byte
@@ -377,17 +376,17 @@ __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint3
     const bool t2A = !hitA && cA != 0, t2B = !hitB && cB != 0;
     if (__any(t2A || t2B)) {  // second tag-matching candidate: both reads unconditional
         const uint32_t s2A = slot_of(gA, cA), s2B = slot_of(gB, cB);
-        const KeyPair k2A = T.key[s2A], k2B = T.key[s2B];
-        const bool m2A = t2A & ((((k2A.a ^ a0) | (k2A.b ^ a1)) == 0) & (!IDX || T.doc[s2A] == dkey));
-        const bool m2B = t2B & ((((k2B.a ^ b0) | (k2B.b ^ b1)) == 0) & (!IDX || T.doc[s2B] == dkey));
+        bool m2A = false, m2B = false;  // reads only by the lanes that need them (LDS array time)
+        if (t2A) m2A = T.matches(s2A, a0, a1, dkey);
+        if (t2B) m2B = T.matches(s2B, b0, b1, dkey);
         hitA |= m2A;
         hitB |= m2B;
         sA = m2A ? s2A : sA;
         sB = m2B ? s2B : sB;
     }
     if (!(abl & 16u)) {
-        atomicAdd(&T.cnt[sA], hitA ? 1u : 0u);  // every lane: no branch (the slot is valid)
-        atomicAdd(&T.cnt[sB], hitB ? 1u : 0u);
+        if (hitA) atomicAdd(&T.cnt[sA], 1u);
+        if (hitB) atomicAdd(&T.cnt[sB], 1u);
     }
     const bool nA = actA && !hitA && zero_bytes(tagsA) != 0, nB = actB && !hitB && zero_bytes(tagsB) != 0;
     if (__any(nA || nB)) {
@@ -395,8 +394,15 @@ __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint3
         if (nB) hitB = T.claim(b0, b1, dkey, gB, tgB, tagsB);
     }
     const bool tA = ha && !hitA && !(abl & 1u), tB = hb && !hitB && !(abl & 1u);
-    const uint32_t slA = atomicAdd(&bcount[bA], tA ? 1u : 0u);
-    const uint32_t slB = atomicAdd(&bcount[bB], tB ? 1u : 0u);
+    uint32_t slA = 0, slB = 0, capA = 0, capB = 0;
+    if (tA) {
+        slA = atomicAdd(&bcount[bA], 1u);
+        capA = bcap[bA];
+    }
+    if (tB) {
+        slB = atomicAdd(&bcount[bB], 1u);
+        capB = bcap[bB];
+    }
     const bool okA = tA && slA < capA, okB = tB && slB < capB;
     if (okA) {
         GAS uint64_t *dst = pool + (bbase[bA] + slA) * (IDX ? 3u : 2u);
