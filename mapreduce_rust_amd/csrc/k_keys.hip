@@ -80,7 +80,7 @@ __device__ __forceinline__ bool ba_add(BaKey *key, unsigned long long *cnt, unsi
                 }
             }
         }
-        slot = (slot + 1u) & (BA_CAP - 1);
+        slot = (slot + 1u + (uint32_t)p) & (BA_CAP - 1);  // triangular steps: no primary clustering
     }
     return false;
 }
