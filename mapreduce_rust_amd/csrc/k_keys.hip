@@ -56,8 +56,13 @@ template <bool IDX>
 __device__ __forceinline__ bool ba_add(BaKey *key, unsigned long long *cnt, unsigned int *doc, uint64_t a,
                                        uint64_t b, uint32_t d, uint64_t c, uint32_t h) {
     uint32_t slot = (h >> (20 - MRG_NBUCKET_LOG2)) & (BA_CAP - 1);  // the 12 bits below the bucket bits
+    BaKey kn = key[slot];
     for (int p = 0; p < BA_PROBE; ++p) {
-        const BaKey k = key[slot];
+        const BaKey k = kn;
+        // the next probe slot's key is read now, beside this one's processing (a stale EMPTY there is
+        // resolved by the CAS below; a filled slot never changes)
+        const uint32_t nxt = (slot + 1u + (uint32_t)p) & (BA_CAP - 1);  // triangular steps
+        kn = key[nxt];
         const bool dk = !IDX || doc[slot] == d;
         if (k.a == a && k.b == b && dk) {
             atomicAdd(&cnt[slot], (unsigned long long)c);
@@ -80,7 +85,7 @@ __device__ __forceinline__ bool ba_add(BaKey *key, unsigned long long *cnt, unsi
                 }
             }
         }
-        slot = (slot + 1u + (uint32_t)p) & (BA_CAP - 1);  // triangular steps: no primary clustering
+        slot = nxt;
     }
     return false;
 }
