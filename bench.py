@@ -31,6 +31,7 @@ import mapreduce_rust_amd as M  # noqa: E402
 from mapreduce_rust_amd import shuffle as S  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+XGMI_LINK_GBS = 153.0  # one xGMI link, one direction; 7 links per GPU, one to each peer of the node
 MIB = 1 << 20
 
 
@@ -130,6 +131,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    S.EXCHANGES.clear()
     t0 = time.perf_counter()
     out_bytes = 0
     for _ in range(a.steps):
@@ -165,6 +167,22 @@ def main():
         except Exception:
             traffic = None
 
+    # xGMI roofline of the exchange (N > 1 over RCCL): peer bytes per rank (max of sent and received)
+    # / average time of the data all-to-alls, against (N - 1) links x 153 GB/s one way (each GPU of
+    # the node has a direct link to each peer).  Max over ranks of the time, sum of the bytes.
+    xgmi = None
+    if world > 1 and S.EXCHANGES:
+        ex_ms = sum(e["start"].elapsed_time(e["end"]) for e in S.EXCHANGES) / len(S.EXCHANGES)
+        ex_b = max(sum(e["sent"] for e in S.EXCHANGES), sum(e["received"] for e in S.EXCHANGES)) / len(S.EXCHANGES)
+        tx = torch.tensor([ex_ms, ex_b], dtype=torch.float64, device=dev)
+        dist.all_reduce(tx, op=dist.ReduceOp.MAX)
+        ex_ms, ex_b = tx.tolist()
+        peak = (world - 1) * XGMI_LINK_GBS
+        ach = ex_b / (ex_ms / 1e3) / 1e9 if ex_ms > 0 else 0.0
+        xgmi = {"bytes_per_rank": int(ex_b), "ms_exchange": round(ex_ms, 3), "achieved": round(ach, 1),
+                "peak": peak, "unit": "GB/s", "frac": round(ach / peak, 4),
+                "note": "max-over-ranks peer bytes of the record + heap all-to-alls / their event time"}
+
     line = {
         "metric": "word-count input GB/s (whole node) at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 3),
@@ -188,6 +206,7 @@ def main():
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "whole_job_frac": round(value / world / HBM_PEAK_GBS, 4)},
+        "xgmi": xgmi,
         "stages_ms": {k: round(v, 3) for k, v in stage.items()},
         "job": {"tokens": st["tokens"], "map_records": st["map_records"], "distinct_keys": st["distinct_keys"],
                 "output_bytes": out_bytes},

@@ -14,6 +14,11 @@ import torch.distributed as dist
 
 XREC = 40
 
+# Per-exchange record of the data all-to-alls (device runs only): start/end events on the current
+# stream around the two data collectives, and the bytes this rank sent to / received from peers
+# (its own slice stays in HBM).  bench.py turns them into the xGMI roofline fraction.
+EXCHANGES = []
+
 
 def owner_of(partition, n_owners):
     """Static plan: partition r is reduced by rank r % G."""
@@ -46,10 +51,22 @@ def alltoall_exchange(send_rec, send_heap, rec_counts, heap_counts, group=None):
     r_heap = [int(b) for _, b in rc]
     recv_rec = torch.empty(max(sum(r_rec), 1) * XREC, dtype=torch.uint8, device=dev)
     recv_heap = torch.empty(max(sum(r_heap), 1), dtype=torch.uint8, device=dev)
+    timed = dev.type == "cuda"
+    if timed:
+        me = dist.get_rank(group)
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
     dist.all_to_all_single(recv_rec[:sum(r_rec) * XREC], send_rec[:sum(rec_counts) * XREC],
                            [x * XREC for x in r_rec], [x * XREC for x in rec_counts], group=group)
     dist.all_to_all_single(recv_heap[:sum(r_heap)], send_heap[:sum(heap_counts)], r_heap, list(heap_counts),
                            group=group)
+    if timed:
+        ev1.record()
+        peers = [o for o in range(world) if o != me]
+        EXCHANGES.append({"start": ev0, "end": ev1,
+                          "sent": sum(rec_counts[o] * XREC + heap_counts[o] for o in peers),
+                          "received": sum(r_rec[o] * XREC + r_heap[o] for o in peers)})
     return recv_rec, recv_heap, r_rec, r_heap
 
 

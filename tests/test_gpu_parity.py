@@ -212,6 +212,42 @@ def test_two_owner_exchange_on_one_gpu(ctx, corpus):
         assert sha(outs[r]) == GOLDEN["wc"]["10"][f"mr-{r}.txt"], r
 
 
+def test_rccl_shuffle_single_rank(tmp_path, corpus):
+    """The product exchange (shuffle.shuffle over RCCL all-to-all) in a one-rank nccl group: the
+    job's own records go out and come back through the collective, output = golden; the exchange's
+    event timing (bench.py's xGMI roofline) is recorded with zero peer bytes."""
+    import torch
+    import torch.distributed as dist
+    import mapreduce_rust_amd as M
+    from mapreduce_rust_amd import shuffle as S
+    from gpu_util import to_device
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1, device_id=dev)
+    c = M.Context(0)
+    try:
+        c.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        t, off = to_device(corpus)
+        S.EXCHANGES.clear()
+        c.job_begin(M.APP_WC, 10)
+        c.set_input(t.data_ptr(), off)
+        c.map()
+        n_rec, _ = S.shuffle(c, 1, dev)
+        c.reduce()
+        outs = c.outputs()
+        torch.cuda.synchronize(dev)
+        assert n_rec > 0
+        for r in range(10):
+            assert sha(outs[r]) == GOLDEN["wc"]["10"][f"mr-{r}.txt"], r
+        assert len(S.EXCHANGES) == 1
+        e = S.EXCHANGES[0]
+        assert e["sent"] == 0 and e["received"] == 0
+        assert e["start"].elapsed_time(e["end"]) >= 0.0
+    finally:
+        c.close()
+        dist.destroy_process_group()
+
+
 def test_zipf_synthetic_vs_oracle(ctx):
     import torch
     import mapreduce_rust_amd as M
