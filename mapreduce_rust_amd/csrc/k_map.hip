@@ -193,11 +193,31 @@ struct alignas(16) KeyPair {
 // written slot, or a claimer that loses its CAS to the same k0, just misses -- harmless: misses go
 // to the tail and every slot is flushed and summed exactly; at worst a key occupies both ways.
 // (Measured by simulation at C3: 8-way tag groups 69.2 % hits, 2-way sets 68.1 %.)
+//
+// Admission (doorkeeper): a key may claim an empty way only on its second sighting in this
+// workgroup -- the first sets its bit in a 32 Kibit LDS bitmap (indexed by hash bits above the set
+// index) and goes to the tail.  The table fills once and keeps its keys, so without the filter it
+// fills with whatever the first few thousand tokens hold, singletons included; with it, mostly with
+// repeated (frequent) keys.  Exactness is untouched: a token either adds to its key's slot or is
+// appended to the tail, and both are summed.
+#ifndef MRG_MAP_DOOR
+#define MRG_MAP_DOOR 1
+#endif
+constexpr uint32_t DOOR_WORDS = 1024;  // 32768 bits
 template <int CAP, bool IDX>
 struct LdsTable {
     static constexpr uint32_t NS = CAP / 2;
     KeyPair *key;
     unsigned int *cnt, *doc;
+    unsigned int *door;
+
+    // first sighting of hash h in this workgroup?  (sets its bit; collisions only admit early)
+    __device__ __forceinline__ bool admitted(uint32_t h) {
+        if (!MRG_MAP_DOOR) return true;
+        const uint32_t di = (h >> 11) & (DOOR_WORDS * 32u - 1u);
+        const uint32_t bit = 1u << (di & 31u);
+        return (atomicOr(&door[di >> 5], bit) & bit) != 0u;
+    }
 
     __device__ __forceinline__ bool matches(uint32_t s, uint64_t a, uint64_t b, uint32_t d) const {
         const KeyPair k = key[s];  // one 16-byte LDS read
@@ -205,7 +225,9 @@ struct LdsTable {
     }
 
     // claim an empty way of set s0 (ways seen empty: e0, e1); true if the key got a slot and its count
-    __device__ __forceinline__ bool claim(uint32_t s0, bool e0, bool e1, uint64_t a, uint64_t b, uint32_t d) {
+    __device__ __forceinline__ bool claim(uint32_t s0, bool e0, bool e1, uint64_t a, uint64_t b, uint32_t d,
+                                          uint32_t h) {
+        if (!admitted(h)) return false;
         for (uint32_t w = 0; w < 2; ++w) {
             if (!(w ? e1 : e0)) continue;
             const uint32_t s = s0 + w;
@@ -233,7 +255,7 @@ struct LdsTable {
         const bool e0 = k0.a == MRG_EMPTY_K0, e1 = k1.a == MRG_EMPTY_K0;
         const bool need = act && !hit && (e0 || e1);
         if (__any(need)) {
-            if (need) hit = claim(s0, e0, e1, a, b, d);
+            if (need) hit = claim(s0, e0, e1, a, b, d, h);
         }
         return hit;
     }
@@ -341,8 +363,8 @@ __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint3
     const bool eB0 = kB0.a == MRG_EMPTY_K0, eB1 = kB1.a == MRG_EMPTY_K0;
     const bool nA = actA && !hitA && (eA0 || eA1), nB = actB && !hitB && (eB0 || eB1);
     if (__any(nA || nB)) {
-        if (nA) hitA = T.claim(sA, eA0, eA1, a0, a1, dkey);
-        if (nB) hitB = T.claim(sB, eB0, eB1, b0, b1, dkey);
+        if (nA) hitA = T.claim(sA, eA0, eA1, a0, a1, dkey, hA);
+        if (nB) hitB = T.claim(sB, eB0, eB1, b0, b1, dkey, hB);
     }
     const bool tA = ha && !hitA && !(abl & 1u), tB = hb && !hitB && !(abl & 1u);
     uint32_t slA = 0, slB = 0, capA = 0, capB = 0;
@@ -530,6 +552,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ unsigned long long s_bbase[MRG_NBUCKET];  // first pool record of (bucket, this WG)
     __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
     __shared__ uint32_t s_next, s_ngen;                  // next block of the workgroup's share; list length
+    __shared__ unsigned int s_door[MRG_MAP_DOOR ? DOOR_WORDS : 1];  // admission bitmap
     static_assert(sizeof(s_q) >= CAP * sizeof(uint16_t), "flush ranks reuse the queues");
 
     const int tid = threadIdx.x;
@@ -541,6 +564,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         s_cnt[i] = 0;
         if (IDX) s_doc[i] = MRG_EMPTY_DOC;
     }
+    if (MRG_MAP_DOOR)
+        for (int i = tid; i < (int)DOOR_WORDS; i += WG) s_door[i] = 0;
     for (int b = tid; b < MRG_NBUCKET; b += WG) {
         s_bcount[b] = 0;
         const uint32_t cap = gp(A.bcap)[b];
@@ -562,7 +587,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             if (4u * j + 3u - p >= L) m |= 0xFFu << (8u * p);
         s_zm[L][j] = m;
     }
-    LdsTable<CAP, IDX> table{s_key, s_cnt, s_doc};
+    LdsTable<CAP, IDX> table{s_key, s_cnt, s_doc, s_door};
     uint32_t my_tokens = 0;
     // uniform job parameters used in the hot loop, read once
     const uint32_t abl = A.ablate;
