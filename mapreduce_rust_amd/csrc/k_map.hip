@@ -195,28 +195,43 @@ struct alignas(16) KeyPair {
 // (Measured by simulation at C3: 8-way tag groups 69.2 % hits, 2-way sets 68.1 %.)
 //
 // Admission (doorkeeper): a key may claim an empty way only on its second sighting in this
-// workgroup -- the first sets its bit in a 32 Kibit LDS bitmap (indexed by hash bits above the set
-// index) and goes to the tail.  The table fills once and keeps its keys, so without the filter it
+// workgroup -- the first sets its bit in a 128 Kibit LDS bitmap (indexed by hash bits above the set
+// index; 32 Kibit for the indexer) and goes to the tail.  The table fills once and keeps its keys, so without the filter it
 // fills with whatever the first few thousand tokens hold, singletons included; with it, mostly with
 // repeated (frequent) keys.  Exactness is untouched: a token either adds to its key's slot or is
 // appended to the tail, and both are summed.
 #ifndef MRG_MAP_DOOR
 #define MRG_MAP_DOOR 1
 #endif
-constexpr uint32_t DOOR_WORDS = 1024;  // 32768 bits
+#ifndef MRG_MAP_DOOR_WORDS
+#define MRG_MAP_DOOR_WORDS 4096
+#endif
+#ifndef MRG_MAP_DOOR_LEVELS
+#define MRG_MAP_DOOR_LEVELS 1
+#endif
 template <int CAP, bool IDX>
 struct LdsTable {
     static constexpr uint32_t NS = CAP / 2;
+    // the indexer's table has a doc word per slot: its bitmap stays at 32 Kibit to fit the LDS
+    static constexpr uint32_t DW = (IDX && MRG_MAP_DOOR_WORDS > 1024) ? 1024u : (uint32_t)MRG_MAP_DOOR_WORDS;
     KeyPair *key;
     unsigned int *cnt, *doc;
     unsigned int *door;
 
-    // first sighting of hash h in this workgroup?  (sets its bit; collisions only admit early)
+    // seen before in this workgroup?  (records this sighting; collisions only admit early).  With
+    // two levels, entries are 2-bit: admitted from the third sighting on.
     __device__ __forceinline__ bool admitted(uint32_t h) {
         if (!MRG_MAP_DOOR) return true;
-        const uint32_t di = (h >> 11) & (DOOR_WORDS * 32u - 1u);
-        const uint32_t bit = 1u << (di & 31u);
-        return (atomicOr(&door[di >> 5], bit) & bit) != 0u;
+        if (MRG_MAP_DOOR_LEVELS == 1) {
+            const uint32_t di = (h >> 11) & (DW * 32u - 1u);
+            const uint32_t bit = 1u << (di & 31u);
+            return (atomicOr(&door[di >> 5], bit) & bit) != 0u;
+        }
+        const uint32_t di = (h >> 11) & (DW * 16u - 1u);
+        const uint32_t lo = 1u << (2u * (di & 15u)), hi = lo << 1;
+        unsigned int *w = &door[di >> 4];
+        if (!(atomicOr(w, lo) & lo)) return false;
+        return (atomicOr(w, hi) & hi) != 0u;
     }
 
     __device__ __forceinline__ bool matches(uint32_t s, uint64_t a, uint64_t b, uint32_t d) const {
@@ -552,7 +567,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ unsigned long long s_bbase[MRG_NBUCKET];  // first pool record of (bucket, this WG)
     __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
     __shared__ uint32_t s_next, s_ngen;                  // next block of the workgroup's share; list length
-    __shared__ unsigned int s_door[MRG_MAP_DOOR ? DOOR_WORDS : 1];  // admission bitmap
+    __shared__ unsigned int s_door[MRG_MAP_DOOR ? LdsTable<CAP, IDX>::DW : 1];  // admission bitmap
     static_assert(sizeof(s_q) >= CAP * sizeof(uint16_t), "flush ranks reuse the queues");
 
     const int tid = threadIdx.x;
@@ -565,7 +580,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         if (IDX) s_doc[i] = MRG_EMPTY_DOC;
     }
     if (MRG_MAP_DOOR)
-        for (int i = tid; i < (int)DOOR_WORDS; i += WG) s_door[i] = 0;
+        for (int i = tid; i < (int)LdsTable<CAP, IDX>::DW; i += WG) s_door[i] = 0;
     for (int b = tid; b < MRG_NBUCKET; b += WG) {
         s_bcount[b] = 0;
         const uint32_t cap = gp(A.bcap)[b];
