@@ -134,15 +134,19 @@ def main():
     S.EXCHANGES.clear()
     t0 = time.perf_counter()
     out_bytes = 0
+    t_prev = t0
     for _ in range(a.steps):
         out_bytes = step()
+        t_now = time.perf_counter()
+        wall_ms = (t_now - t_prev) * 1e3  # the step ends with a host read of the output size
+        t_prev = t_now
         s = ctx.stats()
         map_ms.append(s["ms_map"])
         for k in stage:
             stage[k] += s[k] / a.steps
         if rank == 0:
             log(f"step: map {s['ms_map']:.2f} ms ({s['map_launches']} launch), agg {s['ms_aggregate']:.2f}, "
-                f"sort {s['ms_sort']:.2f}, format {s['ms_format']:.2f}")
+                f"sort {s['ms_sort']:.2f}, format {s['ms_format']:.2f}; wall {wall_ms:.2f}")
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

@@ -505,8 +505,11 @@ void job_map(mrg_ctx *c) {
         bcap[b] = (uint64_t)(est * 1.25) + 32;
     }
     // per-bucket overflow lists absorb the run-to-run variation of the regions' demand (the LDS
-    // table's contents depend on wave timing), so a launch is repeated only when one fills up
-    uint64_t ocap = std::max<uint64_t>(c->ocap_hint, std::max<uint64_t>(1024, total / 20 / MRG_NBUCKET / 16));
+    // table's contents depend on wave timing: a frequent key that finds its set full in one
+    // workgroup sends all its tokens to one region), so a launch is repeated only when one fills
+    // up.  Sized at a quarter of the default region total per bucket (C3: 2 GiB, only touched as
+    // far as used); at 1/16 about one step in ten reran the whole map.
+    uint64_t ocap = std::max<uint64_t>(c->ocap_hint, std::max<uint64_t>(1024, total / 20 / MRG_NBUCKET / 4));
     MapArgs A{};
     MapBufs M;
     uint32_t launches = 0;
@@ -597,7 +600,7 @@ void job_map(mrg_ctx *c) {
                 bcap[b] = std::max<uint64_t>(bcap[b], mx + mx / 4 + 64);
                 c->bcap_rate[b] = (double)mx / per_wg;
             }
-            ocap = c->ocap_hint = 2 * ocap;
+            ocap = c->ocap_hint = 4 * ocap;
         }
         if (nl > lcap) lcap = c->long_hint = nl + nl / 8 + 1024;
         if (getenv("MRG_DEBUG"))
