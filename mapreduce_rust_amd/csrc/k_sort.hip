@@ -121,15 +121,29 @@ struct KVTraits {
     __device__ static __forceinline__ uint32_t digit(const R &r, int q) { return (uint32_t)(r.key >> (8 * q)) & 0xFFu; }
 };
 
-// all-pass histograms in one read: hist[q * 256 + d]
+// all-pass histograms in one read: hist[q * 256 + d], for the passes in qmask only.  A digit that
+// is the same on every active lane (constant bytes: zero padding of short keys, the partition's
+// high bytes) is added once by the first lane instead of by 64 lanes on one LDS address.
 template <class TR>
-__global__ void k_all_hist(const typename TR::R *in, uint64_t n, unsigned long long *hist) {
+__global__ void k_all_hist(const typename TR::R *in, uint64_t n, unsigned long long *hist, uint32_t qmask) {
     __shared__ unsigned int s_h[TR::NPASS * 256];
     for (int i = threadIdx.x; i < TR::NPASS * 256; i += BS) s_h[i] = 0;
     __syncthreads();
+    const uint32_t lane = __lane_id();
     for (uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BS) {
         const typename TR::R r = in[i];
-        for (int q = 0; q < TR::NPASS; ++q) atomicAdd(&s_h[q * 256 + TR::digit(r, q)], 1u);
+        const uint64_t act = __ballot(1);
+        const uint32_t first = (uint32_t)__ffsll((unsigned long long)act) - 1u;
+        for (int q = 0; q < TR::NPASS; ++q) {
+            if (!((qmask >> q) & 1u)) continue;
+            const uint32_t d = TR::digit(r, q);
+            const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+            if (__ballot(d == d0) == act) {
+                if (lane == first) atomicAdd(&s_h[q * 256 + d0], (unsigned int)__popcll(act));
+            } else {
+                atomicAdd(&s_h[q * 256 + d], 1u);
+            }
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < TR::NPASS * 256; i += BS)
@@ -212,7 +226,10 @@ typename TR::R *radix_sort_t(typename TR::R *a, typename TR::R *b, uint64_t n, c
     uint32_t *scantmp = cnt + (uint64_t)256 * ntiles;
     hipMemsetAsync(hist, 0, sizeof(unsigned long long) * TR::NPASS * 256, s);
     const unsigned g = (unsigned)std::min<uint64_t>((n + BS - 1) / BS, 1024);
-    hipLaunchKernelGGL(k_all_hist<TR>, dim3(g), dim3(BS), 0, s, a, n, hist);
+    uint32_t qmask = 0;
+    for (int q = 0; q < TR::NPASS; ++q)
+        if (want[q]) qmask |= 1u << q;
+    hipLaunchKernelGGL(k_all_hist<TR>, dim3(g), dim3(BS), 0, s, a, n, hist, qmask);
     unsigned long long h[TR::NPASS * 256];
     hipMemcpyAsync(h, hist, sizeof h, hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
