@@ -15,7 +15,10 @@
  *                  call_reduce_func(Box::new(wc::reduce), ...)      src/mr/worker.rs:20-25, 174-178
  *                  wc::reduce                                       src/app/wc.rs:15-17
  *   mrg_run_job    the whole mrcoordinator + N x mrworker run       src/bin/mrworker.rs:43-149,
- *                  (static plan instead of coordinator.rs:137-215 task assignment)
+ *                  (static plan instead of coordinator.rs:137-215 task assignment), 1..8 GPUs
+ *   mrg_job_shuffle the mr-{m}-{r}.txt hand-off between map and reduce workers through the shared
+ *                  CWD (write_key_value_to_file worker.rs:117-140 -> read_file_to_mem_reduce
+ *                  worker.rs:79-109), as one RCCL all-to-all over xGMI (owner of r = r % n_ranks)
  *   mrg_map_text   write_key_value_to_file, byte-exact mr-{m}-{r}.txt  src/mr/worker.rs:117-140
  *   mrg_reduce_text read_file_to_mem_reduce over mr-{m}-{r}.txt      src/mr/worker.rs:79-109, 157-193
  *   mrg_job_final  generate_output: cat mr-* | sort > final.txt     src/run.sh:16-20
@@ -39,6 +42,7 @@ extern "C" {
 #define MRG_EHIP (-3)     /* HIP runtime error */
 #define MRG_ENOMEM (-4)   /* device or host allocation failed */
 #define MRG_EIO (-5)      /* file open/read/write failed (reference: unwrap/`?` on fs ops, worker.rs:73,122,168) */
+#define MRG_ECOMM (-6)    /* RCCL communicator error, or another rank of the job failed */
 
 /* ---- apps (the reference selects wc at compile time, worker.rs:5,148,175) ---- */
 #define MRG_APP_WC 0       /* src/app/wc.rs */
@@ -76,8 +80,13 @@ typedef struct {
     double ms_sort;            /* radix sort */
     double ms_format;          /* output formatting */
     uint32_t map_launches;     /* map kernel launches in the last mrg_job_map */
-    uint32_t reserved;
+    uint32_t agg_launches;     /* bucket-aggregation launches (> 1: its overflow list was regrown) */
     uint64_t overflow_keys;    /* records that took the exact HBM-table overflow path */
+    double ms_exchange;        /* mrg_job_shuffle: the data send/recv group, HIP events on the ctx stream */
+    uint64_t exchange_sent;    /* bytes this rank sent to peers (records + heap; its own slice excluded) */
+    uint64_t exchange_recv;    /* bytes this rank received from peers */
+    uint64_t map_spill;        /* map records that overflowed their tail region into a bucket's shared
+                                  overflow list (last map launch) */
 } mrg_stats;
 
 const char *mrg_last_error(void);
@@ -129,6 +138,27 @@ int mrg_job_copy_output(mrg_ctx *ctx, uint8_t *h_dst, uint64_t cap);
 int mrg_job_final(mrg_ctx *ctx, const uint8_t **d_out, uint64_t *h_bytes);
 int mrg_job_copy_final(mrg_ctx *ctx, uint8_t *h_dst, uint64_t cap);
 
+/* ---- multi-GPU: one rank per GPU, the shuffle as an RCCL all-to-all over xGMI ----
+ * The reference moves map output to the reduce workers through mr-{m}-{r}.txt files in a shared
+ * directory (worker.rs:117-140 -> :79-109) and hands out tasks on demand (coordinator.rs:137-215).
+ * Here the plan is static: rank g maps its input shard, partition r is reduced by rank r % n_ranks,
+ * and the hand-off is one exchange of combined per-key records. */
+#define MRG_COMM_ID_BYTES 128
+typedef struct mrg_comm mrg_comm;
+/* A fresh communicator id (an RCCL unique id): made by one rank, given to every rank out of band. */
+int mrg_comm_get_id(uint8_t id[MRG_COMM_ID_BYTES]);
+/* Join the communicator as `rank` of n_ranks, on ctx's device.  Collective over the n_ranks callers
+ * (they must call it concurrently: separate processes, or one thread per GPU). */
+int mrg_comm_init(mrg_ctx *ctx, const uint8_t id[MRG_COMM_ID_BYTES], int n_ranks, int rank, mrg_comm **out);
+int mrg_comm_destroy(mrg_comm *comm);
+/* The exchange step, collective over the communicator, after mrg_job_map on every rank: the job's
+ * keys are packed by owner (r % n_ranks), the per-owner counts go through an all-to-all, the records
+ * and long-key heap bytes through grouped send/recv on the ctx stream, and the received records
+ * replace the job's keys (mrg_job_import).  Then mrg_job_reduce formats the partitions this rank
+ * owns (the others come out empty).  Every rank must reach this call: a rank whose map failed must
+ * still tell the others (the host's concern; mrg_run_job does it). */
+int mrg_job_shuffle(mrg_ctx *ctx, mrg_comm *comm);
+
 /* ---- plugin-surface equivalents, host buffers (one map task / one reduce task) ---- */
 
 /* One map task over one input file's bytes: wc.rs:6-13 + worker.rs:117-140, combined per
@@ -159,11 +189,14 @@ int mrg_map_text(mrg_ctx *ctx, const uint8_t *h_bytes, size_t n, uint32_t n_redu
 int mrg_reduce_text(mrg_ctx *ctx, const uint8_t *const *h_files, const uint64_t *h_sizes, size_t k, uint32_t flags,
                     uint8_t **h_out, size_t *h_out_len);
 
-/* The whole job on one GPU: files are read, mapped, reduced; out_dir/mr-{r}.txt written (and
- * out_dir/final.txt with MRG_FLAG_FINAL_TXT).
+/* The whole job (mrcoordinator + workers, mrworker.rs:43-149) on GPUs 0 .. n_gpus-1, one host thread
+ * per GPU: GPU g reads and maps files m with m % n_gpus == g (the coordinator's map task ids,
+ * coordinator.rs:137-176), the shuffle is mrg_job_shuffle, GPU g reduces and writes out_dir/mr-{r}.txt
+ * for r % n_gpus == g (the reduce task ids, coordinator.rs:178-215).  With MRG_FLAG_FINAL_TXT also
+ * out_dir/final.txt: each GPU sorts the lines it holds, the host merges the n_gpus sorted runs.
  * Indexer document names are the file paths as given (the reference opens "data/gut-{m}.txt"). */
 int mrg_run_job(const char *const *files, size_t n_files, uint32_t n_reduce, int app, const char *out_dir,
-                uint32_t flags, int device);
+                uint32_t flags, int n_gpus);
 
 /* Free host memory returned by the library (mrg_reduce / mrg_map_text / mrg_reduce_text output). */
 void mrg_free(void *p);

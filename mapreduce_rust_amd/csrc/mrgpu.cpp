@@ -12,9 +12,12 @@
 #include <string.h>
 #include <sys/stat.h>
 
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <map>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -44,6 +47,25 @@ struct MrgError {
         hipError_t e_ = (x);                                                           \
         if (e_ != hipSuccess) raise(MRG_EHIP, "%s: %s", #x, hipGetErrorString(e_));    \
     } while (0)
+
+#define NCCLCHK(x)                                                                     \
+    do {                                                                               \
+        ncclResult_t r_ = (x);                                                         \
+        if (r_ != ncclSuccess) raise(MRG_ECOMM, "%s: %s", #x, ncclGetErrorString(r_)); \
+    } while (0)
+
+// The radix sorts index records with 32-bit offsets (k_sort.hip): refuse larger inputs loudly.
+void check_sort_n(uint64_t n, const char *what) {
+    if (n > 0xFFFFFFFFull) raise(MRG_ENOMEM, "%s: %llu records exceed the radix sort's 32-bit index", what,
+                                 (unsigned long long)n);
+}
+
+// Test knobs (env, read once per map): shrink the map's tail regions and overflow lists on the first
+// launch so the spill and grow-and-rerun paths run on small inputs.
+uint64_t env_u64(const char *name, uint64_t dflt) {
+    const char *v = getenv(name);
+    return v && *v ? strtoull(v, nullptr, 10) : dflt;
+}
 
 template <class F>
 int guard(F &&f) {
@@ -167,6 +189,11 @@ struct mrg_ctx {
     mrg_stats st{};
 };
 
+struct mrg_comm {
+    ncclComm_t comm = nullptr;
+    int n = 0, rank = 0, device = 0;
+};
+
 struct mrg_parts {
     uint32_t R = 0;
     std::vector<uint64_t> rec_off, heap_off;  // [R + 1]
@@ -281,6 +308,7 @@ void long_aggregate(mrg_ctx *c, LongItems li) {
         mrg_launch_iota_u32(ix, n, s);
         uint64_t *kv = pget<uint64_t>(p, 4 * n);
         void *stmp = p.get(mrg_sort_tmp_bytes(n));
+        check_sort_n(n, "long-key fingerprint sort");
         mrg_radix_sort_u64(fps, ix, kv, n, stmp, s);
         mrg_launch_long_group(fps, ix, idx ? li.doc : nullptr, c->keys.heap, hoff, fl, n, rep, s);
         HIPCHK(hipMemsetAsync(acc, 0, 8 * n, s));
@@ -339,7 +367,10 @@ void bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
     hipStream_t s = c->stream;
     const bool idx = is_idx(c);
     uint64_t ocap = std::max<uint64_t>(c->ovf_hint, 1u << 20);
+    if (const uint64_t t = env_u64("MRG_TEST_AGG_OCAP", 0)) ocap = t;  // test knob: force the regrow path
+    uint32_t agg_launches = 0;
     for (;;) {
+        ++agg_launches;
         keys_reserve(c, (uint64_t)MRG_NBUCKET * MRG_BA_CAP + ocap + li.n + 1);
         BucketArgs B{};
         B.pool = A.pool; B.rbase = A.rbase; B.bcap = A.bcap; B.bcount = A.bcount;
@@ -372,6 +403,7 @@ void bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         }
         p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
         c->st.overflow_keys = novf;
+        c->st.agg_launches = agg_launches;
         break;
     }
     long_aggregate(c, li);
@@ -413,6 +445,7 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     plan.use_k0 = plan.use_k1 = true;
     void *stmp = p.get(mrg_sort_tmp_bytes(n));
     int passes = 0;
+    check_sort_n(n, "wide aggregation");
     SortRec *r = mrg_radix_sort(a, b, n, plan, stmp, s, &passes);
     p.put(stmp);
     uint64_t *head = pget<uint64_t>(p, n + 1), *cv = pget<uint64_t>(p, n + 1);
@@ -510,6 +543,8 @@ void job_map(mrg_ctx *c) {
     // up.  Sized at a quarter of the default region total per bucket (C3: 2 GiB, only touched as
     // far as used); at 1/16 about one step in ten reran the whole map.
     uint64_t ocap = std::max<uint64_t>(c->ocap_hint, std::max<uint64_t>(1024, total / 20 / MRG_NBUCKET / 4));
+    if (const uint64_t t = env_u64("MRG_TEST_TAIL_CAP", 0)) bcap.assign(MRG_NBUCKET, t);  // test knobs
+    if (const uint64_t t = env_u64("MRG_TEST_OVF_CAP", 0)) ocap = t;
     MapArgs A{};
     MapBufs M;
     uint32_t launches = 0;
@@ -574,7 +609,11 @@ void job_map(mrg_ctx *c) {
         ev_rec(c, 1);
         HIPCHK(hipGetLastError());
         ++launches;
+        std::vector<uint32_t> onext(MRG_NBUCKET);
+        HIPCHK(hipMemcpyAsync(onext.data(), M.onext, 4ull * MRG_NBUCKET, hipMemcpyDeviceToHost, s));
         read_counters(c);
+        c->st.map_spill = 0;
+        for (uint32_t v : onext) c->st.map_spill += std::min<uint64_t>(v, ocap);
         if (M.prof) {
             unsigned long long pr[8];
             HIPCHK(hipMemcpy(pr, M.prof, sizeof pr, hipMemcpyDeviceToHost));
@@ -698,6 +737,7 @@ SortRec *sort_keys(mrg_ctx *c, KeySet ks, uint32_t R, const uint32_t *d_rank, So
     plan.use_doc = idx;
     plan.doc_bytes = idx ? bytes_for(c->names.size() - 1) : 0;
     int passes = 0;
+    check_sort_n(n, "key sort");
     return mrg_radix_sort(a, b, n, plan, stmp, c->stream, &passes);
 }
 
@@ -875,6 +915,84 @@ void job_import(mrg_ctx *c, const void *d_rec, uint64_t n_rec, const void *d_hea
     c->reduced = false;
 }
 
+// The shuffle: the reference's map -> reduce hand-off through mr-{m}-{r}.txt files
+// (worker.rs:117-140 -> 79-109) as one exchange over RCCL.  Owner of partition r = r % G.
+void job_shuffle(mrg_ctx *c, mrg_comm *m) {
+    need_job(c);
+    if (!m || !m->comm) raise(MRG_EINVAL, "null communicator");
+    if (m->device != c->device) raise(MRG_EINVAL, "communicator is on device %d, context on %d", m->device, c->device);
+    if (!c->mapped) raise(MRG_EINVAL, "shuffle before map");
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const uint32_t G = (uint32_t)m->n;
+    const uint32_t me = (uint32_t)m->rank;
+    export_sizes(c, G, nullptr, nullptr);
+    // per-destination (records, heap bytes) -> all-to-all -> per-source
+    std::vector<uint64_t> sc(2ull * G), rc(2ull * G);
+    for (uint32_t o = 0; o < G; ++o) {
+        sc[2 * o] = c->exp_rec[o];
+        sc[2 * o + 1] = c->exp_heap[o];
+    }
+    uint64_t *d_c = pget<uint64_t>(p, 4ull * G);
+    HIPCHK(hipMemcpyAsync(d_c, sc.data(), 16ull * G, hipMemcpyHostToDevice, s));
+    NCCLCHK(ncclAllToAll(d_c, d_c + 2 * G, 2, ncclUint64, m->comm, s));
+    HIPCHK(hipMemcpyAsync(rc.data(), d_c + 2 * G, 16ull * G, hipMemcpyDeviceToHost, s));
+    sync(c);
+    p.put(d_c);
+    std::vector<uint64_t> sro(G + 1, 0), sho(G + 1, 0), rro(G + 1, 0), rho(G + 1, 0), seg_rec(G), seg_heap(G);
+    for (uint32_t o = 0; o < G; ++o) {
+        sro[o + 1] = sro[o] + sc[2 * o];
+        sho[o + 1] = sho[o] + sc[2 * o + 1];
+        rro[o + 1] = rro[o] + rc[2 * o];
+        rho[o + 1] = rho[o] + rc[2 * o + 1];
+        seg_rec[o] = rc[2 * o];
+        seg_heap[o] = rc[2 * o + 1];
+    }
+    uint8_t *srec = pget<uint8_t>(p, sro[G] * MRG_XREC_BYTES + 16), *sheap = pget<uint8_t>(p, sho[G] + 16);
+    uint8_t *rrec = pget<uint8_t>(p, rro[G] * MRG_XREC_BYTES + 16), *rheap = pget<uint8_t>(p, rho[G] + 16);
+    export_pack(c, srec, sheap);
+    const uint64_t X = MRG_XREC_BYTES;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, s));
+    // own slice: a device copy; peers: one send/recv group (each peer pair has its own xGMI link)
+    if (sc[2 * me]) HIPCHK(hipMemcpyAsync(rrec + rro[me] * X, srec + sro[me] * X, sc[2 * me] * X, hipMemcpyDeviceToDevice, s));
+    if (sc[2 * me + 1]) HIPCHK(hipMemcpyAsync(rheap + rho[me], sheap + sho[me], sc[2 * me + 1], hipMemcpyDeviceToDevice, s));
+    uint64_t sent = 0, recv = 0;
+    NCCLCHK(ncclGroupStart());
+    for (uint32_t o = 0; o < G; ++o) {
+        if (o == me) continue;
+        if (sc[2 * o]) NCCLCHK(ncclSend(srec + sro[o] * X, sc[2 * o] * X, ncclUint8, (int)o, m->comm, s));
+        if (sc[2 * o + 1]) NCCLCHK(ncclSend(sheap + sho[o], sc[2 * o + 1], ncclUint8, (int)o, m->comm, s));
+        if (rc[2 * o]) NCCLCHK(ncclRecv(rrec + rro[o] * X, rc[2 * o] * X, ncclUint8, (int)o, m->comm, s));
+        if (rc[2 * o + 1]) NCCLCHK(ncclRecv(rheap + rho[o], rc[2 * o + 1], ncclUint8, (int)o, m->comm, s));
+        sent += sc[2 * o] * X + sc[2 * o + 1];
+        recv += rc[2 * o] * X + rc[2 * o + 1];
+    }
+    NCCLCHK(ncclGroupEnd());
+    HIPCHK(hipEventRecord(e1, s));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    p.put(srec);
+    p.put(sheap);
+    const mrg_stats keep = c->st;
+    job_import(c, rrec, rro[G], rheap, rho[G], seg_rec.data(), seg_heap.data(), G);
+    p.put(rrec);
+    p.put(rheap);
+    // the import's aggregation time is the reduce side's; the map-side stats stay those of the map
+    const double agg_import = c->st.ms_aggregate;
+    c->st = keep;
+    c->st.ms_aggregate += agg_import;
+    c->st.distinct_keys = c->keys.n;
+    c->st.ms_exchange = ms;
+    c->st.exchange_sent = sent;
+    c->st.exchange_recv = recv;
+}
+
 void check_names(const char *const *names, uint32_t n) {
     for (uint32_t i = 0; i < n; ++i) {
         if (!names[i]) raise(MRG_EINVAL, "null document name %u", i);
@@ -922,6 +1040,7 @@ void text_map(mrg_ctx *c, const uint8_t *h, uint64_t n, uint32_t R, std::vector<
         uint32_t *idx = pget<uint32_t>(p, T);
         void *stmp2 = p.get(mrg_sort_tmp_bytes(T));
         mrg_launch_text_keys(tok, T, part, idx, s);
+        check_sort_n(T, "text partition sort");
         mrg_radix_sort_u64(part, idx, kv, T, stmp2, s);  // stable: input order inside a partition
         uint64_t *L = pget<uint64_t>(p, T + 1), *O = pget<uint64_t>(p, T + 1);
         uint64_t *stmp3 = pget<uint64_t>(p, mrg_scan_tmp_elems(T + 1));
@@ -1107,7 +1226,9 @@ int mrg_job_set_input(mrg_ctx *c, const uint8_t *d_bytes, const uint64_t *h_doc_
                       const uint32_t *h_doc_ids) {
     return guard([&] {
         need_job(c);
-        if (n_docs && (!d_bytes || !h_doc_off)) raise(MRG_EINVAL, "null input");
+        if (!h_doc_off) raise(MRG_EINVAL, "null document offsets (h_doc_off needs n_docs + 1 entries)");
+        if (n_docs && !d_bytes) raise(MRG_EINVAL, "null input");
+        if (n_docs == 0xFFFFFFFFu) raise(MRG_EINVAL, "n_docs out of range");
         if ((uintptr_t)d_bytes & 15u) raise(MRG_EINVAL, "input buffer must be 16-byte aligned");
         for (uint32_t i = 0; i < n_docs; ++i)
             if (h_doc_off[i + 1] < h_doc_off[i]) raise(MRG_EINVAL, "document offsets must be non-decreasing");
@@ -1321,71 +1442,220 @@ int mrg_reduce(mrg_ctx *c, int app, uint32_t r, const mrg_parts *const *in, size
     });
 }
 
-int mrg_run_job(const char *const *files, size_t n_files, uint32_t n_reduce, int app, const char *out_dir,
-                uint32_t flags, int device) {
-    mrg_ctx *c = nullptr;
-    int rc = mrg_open(device, &c);
-    if (rc) return rc;
-    rc = guard([&] {
-        std::vector<uint64_t> off(1, 0);
-        std::vector<std::vector<uint8_t>> data(n_files);
-        for (size_t i = 0; i < n_files; ++i) {
-            FILE *f = fopen(files[i], "rb");   // worker.rs:73 File::open(..).unwrap()
-            if (!f) raise(MRG_EIO, "cannot open %s", files[i]);
-            fseek(f, 0, SEEK_END);
-            const long sz = ftell(f);
-            fseek(f, 0, SEEK_SET);
-            data[i].resize((size_t)sz);
-            const size_t got = sz ? fread(data[i].data(), 1, (size_t)sz, f) : 0;
-            fclose(f);
-            if (got != (size_t)sz) raise(MRG_EIO, "short read on %s", files[i]);
-            off.push_back(off.back() + (uint64_t)sz);
+int mrg_comm_get_id(uint8_t id[MRG_COMM_ID_BYTES]) {
+    return guard([&] {
+        if (!id) raise(MRG_EINVAL, "null id");
+        static_assert(sizeof(ncclUniqueId) == MRG_COMM_ID_BYTES, "RCCL unique id size");
+        ncclUniqueId u;
+        NCCLCHK(ncclGetUniqueId(&u));
+        memcpy(id, &u, sizeof u);
+    });
+}
+
+int mrg_comm_init(mrg_ctx *c, const uint8_t id[MRG_COMM_ID_BYTES], int n_ranks, int rank, mrg_comm **out) {
+    return guard([&] {
+        if (!c || !id || !out) raise(MRG_EINVAL, "null argument");
+        if (n_ranks < 1 || rank < 0 || rank >= n_ranks) raise(MRG_EINVAL, "rank %d of %d", rank, n_ranks);
+        HIPCHK(hipSetDevice(c->device));
+        ncclUniqueId u;
+        memcpy(&u, id, sizeof u);
+        mrg_comm *m = new mrg_comm();
+        const ncclResult_t r = ncclCommInitRank(&m->comm, n_ranks, u, rank);
+        if (r != ncclSuccess) {
+            delete m;
+            raise(MRG_ECOMM, "ncclCommInitRank(%d of %d): %s", rank, n_ranks, ncclGetErrorString(r));
         }
-        job_begin(c, app, n_reduce, flags);
+        m->n = n_ranks;
+        m->rank = rank;
+        m->device = c->device;
+        *out = m;
+    });
+}
+
+int mrg_comm_destroy(mrg_comm *m) {
+    return guard([&] {
+        if (!m) return;
+        if (m->comm) {
+            (void)hipSetDevice(m->device);
+            const ncclResult_t r = ncclCommDestroy(m->comm);
+            m->comm = nullptr;
+            delete m;
+            if (r != ncclSuccess) raise(MRG_ECOMM, "ncclCommDestroy: %s", ncclGetErrorString(r));
+            return;
+        }
+        delete m;
+    });
+}
+
+int mrg_job_shuffle(mrg_ctx *c, mrg_comm *m) {
+    return guard([&] { job_shuffle(c, m); });
+}
+
+}  // extern "C"
+
+namespace {
+
+void read_file(const char *path, std::vector<uint8_t> &data) {
+    FILE *f = fopen(path, "rb");  // worker.rs:73 File::open(..).unwrap()
+    if (!f) raise(MRG_EIO, "cannot open %s", path);
+    fseek(f, 0, SEEK_END);
+    const long sz = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    data.resize(sz > 0 ? (size_t)sz : 0);
+    const size_t got = sz > 0 ? fread(data.data(), 1, (size_t)sz, f) : 0;
+    fclose(f);
+    if (sz < 0 || got != (size_t)sz) raise(MRG_EIO, "short read on %s", path);
+}
+
+void write_file(const std::string &path, const uint8_t *p, uint64_t n) {
+    FILE *f = fopen(path.c_str(), "wb");  // worker.rs:167-168 File::create("mr-{r}.txt")
+    if (!f) raise(MRG_EIO, "cannot create %s", path.c_str());
+    const size_t w = n ? fwrite(p, 1, n, f) : 0;
+    const int cl = fclose(f);
+    if (w != n || cl != 0) raise(MRG_EIO, "short write on %s", path.c_str());
+}
+
+// k-way merge of G byte-sorted line runs (each GPU's final.txt lines): LC_ALL=C `sort` order
+std::vector<uint8_t> merge_sorted_lines(const std::vector<std::vector<uint8_t>> &runs) {
+    struct Cur { const uint8_t *p, *e; };
+    std::vector<Cur> cur;
+    uint64_t total = 0;
+    for (auto &r : runs) {
+        cur.push_back({r.data(), r.data() + r.size()});
+        total += r.size();
+    }
+    auto line_end = [](const Cur &c) { return (const uint8_t *)memchr(c.p, '\n', (size_t)(c.e - c.p)); };
+    std::vector<uint8_t> out;
+    out.reserve(total);
+    for (;;) {
+        int best = -1;
+        const uint8_t *be = nullptr;
+        for (int i = 0; i < (int)cur.size(); ++i) {
+            if (cur[i].p >= cur[i].e) continue;
+            const uint8_t *e = line_end(cur[i]);
+            if (!e) e = cur[i].e;
+            if (best < 0) { best = i; be = e; continue; }
+            const size_t la = (size_t)(e - cur[i].p), lb = (size_t)(be - cur[best].p);
+            const int cm = memcmp(cur[i].p, cur[best].p, std::min(la, lb));
+            if (cm < 0 || (cm == 0 && la < lb)) { best = i; be = e; }
+        }
+        if (best < 0) break;
+        const uint8_t *stop = be < cur[best].e ? be + 1 : be;
+        out.insert(out.end(), cur[best].p, stop);
+        cur[best].p = stop;
+    }
+    return out;
+}
+
+// One GPU of mrg_run_job: rank g of G (GPU g), one host thread.
+void run_rank(int g, int G, const ncclUniqueId *uid, const char *const *files, size_t n_files, uint32_t R, int app,
+              const char *out_dir, uint32_t flags, std::vector<uint8_t> &final_out) {
+    mrg_ctx *c = nullptr;
+    if (mrg_open(g, &c) != MRG_OK) raise(MRG_EHIP, "GPU %d: %s", g, mrg_last_error());
+    struct Closer { mrg_ctx *c; mrg_comm *m; ~Closer() { mrg_comm_destroy(m); mrg_close(c); } } closer{c, nullptr};
+    if (G > 1 || uid) {
+        if (mrg_comm_init(c, (const uint8_t *)uid, G, g, &closer.m) != MRG_OK) raise(MRG_ECOMM, "%s", mrg_last_error());
+    }
+    // map shard: files m with m % G == g (static plan for coordinator.rs:137-176)
+    int status = MRG_OK;
+    std::string err;
+    uint8_t *d = nullptr;
+    try {
+        job_begin(c, app, R, flags);
         std::vector<const char *> nm(files, files + n_files);
         check_names(nm.data(), (uint32_t)n_files);
         c->names.assign(files, files + n_files);
-        uint8_t *d = pget<uint8_t>(c->pool, off.back() + 64);
-        for (size_t i = 0; i < n_files; ++i)
+        std::vector<uint64_t> off(1, 0);
+        std::vector<uint32_t> ids;
+        std::vector<std::vector<uint8_t>> data;
+        for (size_t m = (size_t)g; m < n_files; m += (size_t)G) {
+            data.emplace_back();
+            read_file(files[m], data.back());
+            off.push_back(off.back() + data.back().size());
+            ids.push_back((uint32_t)m);
+        }
+        d = pget<uint8_t>(c->pool, off.back() + 64);
+        for (size_t i = 0; i < data.size(); ++i)
             if (!data[i].empty())
                 HIPCHK(hipMemcpyAsync(d + off[i], data[i].data(), data[i].size(), hipMemcpyHostToDevice, c->stream));
         sync(c);
+        data.clear();
         c->d_in = d;
         c->doc_off = off;
+        c->doc_ids = ids;
         job_map(c);
-        job_reduce(c);
-        std::vector<uint8_t> out(c->out_bytes);
-        if (c->out_bytes)
-            HIPCHK(hipMemcpyAsync(out.data(), c->d_out, c->out_bytes, hipMemcpyDeviceToHost, c->stream));
+    } catch (const MrgError &e) {
+        status = e.code;
+        err = e.msg;
+    }
+    if (closer.m) {  // every rank learns whether any map failed before entering the exchange
+        int *flag = pget<int>(c->pool, 1);
+        int h = status ? 1 : 0;
+        HIPCHK(hipMemcpyAsync(flag, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
+        NCCLCHK(ncclAllReduce(flag, flag, 1, ncclInt, ncclMax, closer.m->comm, c->stream));
+        HIPCHK(hipMemcpyAsync(&h, flag, sizeof h, hipMemcpyDeviceToHost, c->stream));
         sync(c);
-        for (uint32_t r = 0; r < n_reduce; ++r) {   // worker.rs:167-168 File::create("mr-{r}.txt")
-            const std::string path = std::string(out_dir) + "/mr-" + std::to_string(r) + ".txt";
-            FILE *f = fopen(path.c_str(), "wb");
-            if (!f) raise(MRG_EIO, "cannot create %s", path.c_str());
-            const uint64_t a = c->part_off[r], b = c->part_off[r + 1];
-            const size_t w = b > a ? fwrite(out.data() + a, 1, b - a, f) : 0;
-            fclose(f);
-            if (w != b - a) raise(MRG_EIO, "short write on %s", path.c_str());
+        c->pool.put(flag);
+        if (h && !status) raise(MRG_ECOMM, "another GPU of the job failed");
+    }
+    if (status) throw MrgError{status, err};
+    if (closer.m) job_shuffle(c, closer.m);
+    job_reduce(c);
+    std::vector<uint8_t> out(c->out_bytes);
+    if (c->out_bytes) HIPCHK(hipMemcpyAsync(out.data(), c->d_out, c->out_bytes, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    for (uint32_t r = (uint32_t)g; r < R; r += (uint32_t)G) {  // reduce tasks of this GPU (coordinator.rs:178-215)
+        const uint64_t a = c->part_off[r], b = c->part_off[r + 1];
+        write_file(std::string(out_dir) + "/mr-" + std::to_string(r) + ".txt", out.data() + a, b - a);
+    }
+    if (flags & MRG_FLAG_FINAL_TXT) {  // run.sh:16-20 generate_output: this GPU's lines, sorted on the device
+        job_final(c);
+        final_out.resize(c->final_bytes);
+        if (c->final_bytes)
+            HIPCHK(hipMemcpyAsync(final_out.data(), c->d_final, c->final_bytes, hipMemcpyDeviceToHost, c->stream));
+        sync(c);
+    }
+    c->pool.put(d);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mrg_run_job(const char *const *files, size_t n_files, uint32_t n_reduce, int app, const char *out_dir,
+                uint32_t flags, int n_gpus) {
+    return guard([&] {
+        if ((n_files && !files) || !out_dir) raise(MRG_EINVAL, "null argument");
+        if (n_reduce == 0) raise(MRG_EINVAL, "n_reduce must be > 0");
+        int ndev = 0;
+        HIPCHK(hipGetDeviceCount(&ndev));
+        if (n_gpus < 1 || n_gpus > ndev) raise(MRG_EINVAL, "n_gpus %d: %d devices visible", n_gpus, ndev);
+        const int G = n_gpus;
+        std::vector<std::vector<uint8_t>> fin(G);
+        if (G == 1 && !env_u64("MRG_TEST_FORCE_COMM", 0)) {  // one GPU: no communicator needed
+            run_rank(0, 1, nullptr, files, n_files, n_reduce, app, out_dir, flags, fin[0]);
+        } else {
+            ncclUniqueId uid;
+            NCCLCHK(ncclGetUniqueId(&uid));
+            std::vector<int> rc(G, MRG_OK);
+            std::vector<std::string> msg(G);
+            std::vector<std::thread> th;
+            for (int g = 0; g < G; ++g)
+                th.emplace_back([&, g] {
+                    rc[g] = guard([&] { run_rank(g, G, &uid, files, n_files, n_reduce, app, out_dir, flags, fin[g]); });
+                    if (rc[g]) msg[g] = g_err;
+                });
+            for (auto &t : th) t.join();
+            for (int g = 0; g < G; ++g)  // the first rank's own failure, not the others' ECOMM echo of it
+                if (rc[g] && rc[g] != MRG_ECOMM) raise(rc[g], "GPU %d: %s", g, msg[g].c_str());
+            for (int g = 0; g < G; ++g)
+                if (rc[g]) raise(rc[g], "GPU %d: %s", g, msg[g].c_str());
         }
-        if (flags & MRG_FLAG_FINAL_TXT) {  // run.sh:16-20 generate_output, on the device
-            job_final(c);
-            std::vector<uint8_t> fin(c->final_bytes);
-            if (c->final_bytes)
-                HIPCHK(hipMemcpyAsync(fin.data(), c->d_final, c->final_bytes, hipMemcpyDeviceToHost, c->stream));
-            sync(c);
-            const std::string path = std::string(out_dir) + "/final.txt";
-            FILE *f = fopen(path.c_str(), "wb");
-            if (!f) raise(MRG_EIO, "cannot create %s", path.c_str());
-            const size_t w = fin.empty() ? 0 : fwrite(fin.data(), 1, fin.size(), f);
-            fclose(f);
-            if (w != fin.size()) raise(MRG_EIO, "short write on %s", path.c_str());
+        if (flags & MRG_FLAG_FINAL_TXT) {
+            const std::vector<uint8_t> all = G == 1 ? fin[0] : merge_sorted_lines(fin);
+            write_file(std::string(out_dir) + "/final.txt", all.data(), all.size());
         }
-        c->pool.put(d);
     });
-    std::string err = g_err;
-    mrg_close(c);
-    g_err = err;
-    return rc;
 }
 
 void mrg_free(void *p) { free(p); }

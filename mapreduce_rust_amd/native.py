@@ -15,8 +15,9 @@ FLAG_NO_COMPAT_DROP_LAST = 0x1
 FLAG_FINAL_TXT = 0x2
 XREC_BYTES = 40
 
-OK, EINVAL, EUTF8, EHIP, ENOMEM, EIO = 0, -1, -2, -3, -4, -5
-_CODES = {EINVAL: "EINVAL", EUTF8: "EUTF8", EHIP: "EHIP", ENOMEM: "ENOMEM", EIO: "EIO"}
+OK, EINVAL, EUTF8, EHIP, ENOMEM, EIO, ECOMM = 0, -1, -2, -3, -4, -5, -6
+_CODES = {EINVAL: "EINVAL", EUTF8: "EUTF8", EHIP: "EHIP", ENOMEM: "ENOMEM", EIO: "EIO", ECOMM: "ECOMM"}
+COMM_ID_BYTES = 128
 
 
 def debug_hash_bits(n):
@@ -38,11 +39,12 @@ class Stats(C.Structure):
     _fields_ = [("input_bytes", C.c_uint64), ("tokens", C.c_uint64), ("long_tokens", C.c_uint64),
                 ("map_records", C.c_uint64), ("distinct_keys", C.c_uint64), ("output_bytes", C.c_uint64),
                 ("ms_map", C.c_double), ("ms_aggregate", C.c_double), ("ms_sort", C.c_double),
-                ("ms_format", C.c_double), ("map_launches", C.c_uint32), ("reserved", C.c_uint32),
-                ("overflow_keys", C.c_uint64)]
+                ("ms_format", C.c_double), ("map_launches", C.c_uint32), ("agg_launches", C.c_uint32),
+                ("overflow_keys", C.c_uint64), ("ms_exchange", C.c_double), ("exchange_sent", C.c_uint64),
+                ("exchange_recv", C.c_uint64), ("map_spill", C.c_uint64)]
 
     def as_dict(self):
-        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+        return {f: getattr(self, f) for f, _ in self._fields_}
 
 
 _lib = None
@@ -82,6 +84,10 @@ _SIGS = {
                                   C.POINTER(C.c_size_t)]),
     "mrg_run_job": (C.c_int, [C.POINTER(C.c_char_p), C.c_size_t, C.c_uint32, C.c_int, C.c_char_p, C.c_uint32,
                               C.c_int]),
+    "mrg_comm_get_id": (C.c_int, [_vp]),
+    "mrg_comm_init": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.POINTER(_vp)]),
+    "mrg_comm_destroy": (C.c_int, [_vp]),
+    "mrg_job_shuffle": (C.c_int, [_vp, _vp]),
     "mrg_free": (None, [_vp]),
     "mrg_gen_zipf": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_double]),
     "mrg_gen_unique": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64]),
@@ -194,6 +200,8 @@ class Context:
         _check(load().mrg_job_set_doc_names(self.h, arr, len(names)))
 
     def set_input(self, dev_ptr, doc_off, doc_ids=None):
+        if len(doc_off) < 1:
+            raise ValueError("doc_off needs n_docs + 1 entries (at least [0])")
         n = len(doc_off) - 1
         off = _u64arr(doc_off)
         ids = (C.c_uint32 * max(n, 1))(*doc_ids) if doc_ids is not None else None
@@ -217,6 +225,10 @@ class Context:
         else:
             _check(load().mrg_job_import(self.h, d_rec, n_rec, d_heap, heap_bytes, _u64arr(seg_recs),
                                          _u64arr(seg_heap), len(seg_recs)))
+
+    def shuffle(self, comm):
+        """mrg_job_shuffle: the exchange over RCCL (collective over comm's ranks)."""
+        _check(load().mrg_job_shuffle(self.h, comm.h))
 
     def reduce(self):
         n = C.c_uint64()
@@ -295,6 +307,31 @@ class Context:
         _check(load().mrg_gen_unique(self.h, dev_ptr, n_bytes, seed, file_index))
 
 
-def run_job(files, n_reduce, app=APP_WC, out_dir=".", flags=0, device=0):
+def run_job(files, n_reduce, app=APP_WC, out_dir=".", flags=0, n_gpus=1):
     arr = (C.c_char_p * max(len(files), 1))(*[f.encode() for f in files])
-    _check(load().mrg_run_job(arr, len(files), n_reduce, app, out_dir.encode(), flags, device))
+    _check(load().mrg_run_job(arr, len(files), n_reduce, app, out_dir.encode(), flags, n_gpus))
+
+
+def comm_id():
+    """A fresh RCCL communicator id (bytes) for Comm(); made by one rank, shared out of band."""
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    _check(load().mrg_comm_get_id(buf))
+    return buf.raw
+
+
+class Comm:
+    """mrg_comm: this rank's membership of an RCCL communicator (one per GPU / context)."""
+
+    def __init__(self, ctx, uid, n_ranks, rank):
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError("communicator id must be %d bytes" % COMM_ID_BYTES)
+        h = _vp()
+        _check(load().mrg_comm_init(ctx.h, uid, n_ranks, rank, C.byref(h)))
+        self.h = h
+        self.n_ranks = n_ranks
+        self.rank = rank
+
+    def close(self):
+        if self.h:
+            _check(load().mrg_comm_destroy(self.h))
+            self.h = None

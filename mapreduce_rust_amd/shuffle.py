@@ -1,16 +1,24 @@
-"""Multi-GPU static plan and the shuffle exchange (torch.distributed: RCCL on GPU, gloo on CPU).
+"""Multi-GPU static plan and the shuffle exchange.
 
 The reference coordinator hands out map tasks (input files) and reduce tasks (partitions) on demand
 (src/mr/coordinator.rs:137-215) and the shuffle goes through mr-{m}-{r}.txt files in a shared CWD
 (src/mr/worker.rs:117-140, 79-109).  Here the plan is static: rank g maps its shard of the input
 files, and owns every partition r with r % G == g.  After the map each rank packs its per-key
 records by owner (mrg_job_export), one all-to-all of the per-owner counts tells every rank how much
-it receives, and two all-to-all(v)s move the 40-byte exchange records and the long-key heap bytes.
-The receiving rank re-aggregates (mrg_job_import: the same key can arrive from every rank) and
-reduces its partitions.  There is exactly one data-path collective, the exchange itself.
+it receives, and the 40-byte exchange records and the long-key heap bytes follow.  The receiving
+rank re-aggregates (mrg_job_import: the same key can arrive from every rank) and reduces its
+partitions.  There is exactly one data-path collective, the exchange itself.
+
+Two transports of the same records:
+  * library_comm() + Context.shuffle(): the product path, RCCL called from libmrgpu.so
+    (mrg_job_shuffle: counts all-to-all, then grouped send/recv over xGMI on the context's stream);
+  * shuffle(): export -> torch.distributed all_to_all_single -> import, used with the gloo backend
+    (host staged) to rehearse N ranks on one GPU and in the CPU tests.
 """
 import torch
 import torch.distributed as dist
+
+from . import native
 
 XREC = 40
 
@@ -70,12 +78,32 @@ def alltoall_exchange(send_rec, send_heap, rec_counts, heap_counts, group=None):
     return recv_rec, recv_heap, r_rec, r_heap
 
 
+def library_comm(ctx, group=None):
+    """The library's RCCL communicator over the ranks of a torch.distributed group, one rank per GPU:
+    rank 0 makes the id (mrg_comm_get_id), a broadcast over the group hands it to the others, every
+    rank joins (mrg_comm_init, collective).  Use with ctx.shuffle(comm)."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    obj = [native.comm_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return native.Comm(ctx, obj[0], world, rank)
+
+
 def shuffle(ctx, world, device, group=None):
-    """The exchange step of a device-resident job on every rank (after ctx.map())."""
+    """The exchange step of a device-resident job on every rank (after ctx.map()), through
+    torch.distributed.  The context's kernels run on its own stream, torch's buffers and collectives
+    on torch's current stream: the current stream is drained before the export writes into torch
+    buffers and before the import reads what the collectives wrote (the export itself returns only
+    after its kernels are done)."""
+    dev = torch.device(device)
+    cuda = dev.type == "cuda"
     rec, heap = ctx.export_sizes(world)
-    send_rec = torch.empty(max(sum(rec), 1) * XREC, dtype=torch.uint8, device=device)
-    send_heap = torch.empty(max(sum(heap), 1), dtype=torch.uint8, device=device)
+    send_rec = torch.empty(max(sum(rec), 1) * XREC, dtype=torch.uint8, device=dev)
+    send_heap = torch.empty(max(sum(heap), 1), dtype=torch.uint8, device=dev)
+    if cuda:
+        torch.cuda.current_stream(dev).synchronize()
     ctx.export(send_rec.data_ptr(), send_heap.data_ptr())
     recv_rec, recv_heap, r_rec, r_heap = alltoall_exchange(send_rec, send_heap, rec, heap, group)
+    if cuda:
+        torch.cuda.current_stream(dev).synchronize()
     ctx.import_(recv_rec.data_ptr(), sum(r_rec), recv_heap.data_ptr(), sum(r_heap), r_rec, r_heap)
     return sum(r_rec), sum(r_heap)

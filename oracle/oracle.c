@@ -23,10 +23,16 @@
  *   ORACLE_FAITHFUL : the reference's structure (per-token write(2) + log line, files, read-back,
  *                     stable sort of every record, adjacent grouping) -- the "reference CPU path"
  *   ORACLE_FAST     : in-memory hash count + sort of distinct keys (a checker at larger sizes)
+ * and two multi-threaded forms of them:
+ *   oracle_wc_workers : FAITHFUL with W worker threads that pull map task ids, then reduce task ids,
+ *                       like W `mrworker` processes under the coordinator (mrworker.rs:43-149,
+ *                       coordinator.rs:137-215) -- the CPU baseline at W = host cores
+ *   oracle_wc_mt      : FAST over whitespace-aligned chunks on T threads (the full-size checker)
  */
 #define _GNU_SOURCE
 #include <errno.h>
 #include <fcntl.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -167,10 +173,25 @@ static void by_putu64(bytes_t *b, uint64_t v) {
  * Restatement: delete X codepoints, split on S; a run of W/X with no W yields nothing. */
 typedef void (*tok_cb)(void *ud, const uint8_t *key, size_t len);
 
+static int8_t g_ascii_cls[128];
+__attribute__((constructor)) static void init_ascii_cls(void) {
+    for (uint32_t c = 0; c < 128; ++c) g_ascii_cls[c] = (int8_t)oracle_class(c);
+}
+
 static int tokenize(const uint8_t *s, size_t n, tok_cb cb, void *ud, bytes_t *scratch) {
     scratch->n = 0;
     size_t i = 0;
     while (i < n) {
+        if (s[i] < 0x80) {  /* ASCII: the class table above (same classes, no decode / search) */
+            int c = g_ascii_cls[s[i]];
+            if (c == 2) {
+                if (scratch->n) { cb(ud, scratch->p, scratch->n); scratch->n = 0; }
+            } else if (c == 1) {
+                by_putc(scratch, s[i]);
+            }
+            ++i;
+            continue;
+        }
         uint32_t cp;
         int l = utf8_next(s, n, i, &cp);
         if (!l) return ORACLE_EUTF8;
@@ -372,89 +393,103 @@ static int read_all(const char *path, bytes_t *b) {
     return ORACLE_OK;
 }
 
+/* One map task (Worker::map, worker.rs:142-155): tokenize file m, one write(2) of "k 1\n" per token to
+ * dir/mr-{m}-{r}.txt (r = SipHash % R) and one log line per token. */
+static int faithful_map_task(const uint8_t *file, size_t len, int m, uint32_t R, const char *dir, int logfd,
+                             bytes_t *scratch) {
+    char path[4096];
+    int rc = ORACLE_OK;
+    int *fds = (int *)malloc(sizeof(int) * R);
+    for (uint32_t r = 0; r < R; ++r) {                                       /* :120-125 */
+        snprintf(path, sizeof path, "%s/mr-%d-%u.txt", dir, m, r);
+        fds[r] = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        if (fds[r] < 0) rc = ORACLE_EIO;
+    }
+    if (rc == ORACLE_OK) {
+        faithful_ud u = {fds, R, logfd, m, 0};
+        rc = tokenize(file, len, cb_faithful, &u, scratch);
+        if (u.err && rc == ORACLE_OK) rc = ORACLE_EIO;
+    }
+    for (uint32_t r = 0; r < R; ++r) if (fds[r] >= 0) close(fds[r]);
+    free(fds);
+    return rc;
+}
+
+/* One reduce task (Worker::reduce, worker.rs:157-193): read mr-{m}-{r}.txt for every m, parse, stable
+ * sort, group, write dir/mr-{r}.txt; its bytes are also appended to *out. */
+static int faithful_reduce_task(int n_files, uint32_t r, const char *dir, bytes_t *out) {
+    char path[4096];
+    int rc = ORACLE_OK;
+    bytes_t all = {0}, content = {0};
+    for (int m = 0; m < n_files && rc == ORACLE_OK; ++m) {                   /* read_file_to_mem_reduce :79-109 */
+        snprintf(path, sizeof path, "%s/mr-%d-%u.txt", dir, m, r);
+        rc = read_all(path, &content);
+        if (rc == ORACLE_OK) by_put(&all, content.p, content.n);
+    }
+    size_t nkv = 0, cap = 1024;
+    kv_t *kv = (kv_t *)malloc(sizeof(kv_t) * cap);
+    size_t i = 0;
+    while (rc == ORACLE_OK && i < all.n) {
+        size_t e = i;
+        while (e < all.n && all.p[e] != '\n') ++e;
+        if (e > i) {
+            size_t sp = i;
+            while (sp < e && all.p[sp] != ' ') ++sp;
+            size_t sp2 = sp + 1;
+            while (sp2 < e && all.p[sp2] != ' ') ++sp2;
+            if (sp >= e || sp2 != e) { rc = ORACLE_EARG; break; }             /* assert!(len == 2) */
+            if (nkv == cap) { cap *= 2; kv = (kv_t *)realloc(kv, sizeof(kv_t) * cap); }
+            kv[nkv].k = all.p + i; kv[nkv].kl = (uint32_t)(sp - i);
+            kv[nkv].v = all.p + sp + 1; kv[nkv].vl = (uint32_t)(e - sp - 1);
+            ++nkv;
+        }
+        i = e + 1;
+    }
+    kv_t *tmp = (kv_t *)malloc(sizeof(kv_t) * (nkv ? nkv : 1));
+    merge_sort_kv(kv, tmp, nkv);                                             /* :162-164 */
+    free(tmp);
+    int ofd = -1;
+    if (rc == ORACLE_OK) {
+        snprintf(path, sizeof path, "%s/mr-%u.txt", dir, r);
+        ofd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        if (ofd < 0) rc = ORACLE_EIO;
+    }
+    const uint8_t *prev = NULL;
+    uint32_t prevl = 0;
+    uint64_t nvals = 0;
+    for (size_t t = 0; t < nkv && rc == ORACLE_OK; ++t) {                    /* :169-184 */
+        if (!prev) { prev = kv[t].k; prevl = kv[t].kl; }
+        if (kv[t].kl != prevl || memcmp(kv[t].k, prev, prevl)) {
+            size_t before = out->n;
+            by_put(out, prev, prevl);
+            by_putc(out, ' ');
+            by_putu64(out, nvals);                                           /* wc::reduce */
+            by_putc(out, '\n');
+            if (write(ofd, out->p + before, out->n - before) != (ssize_t)(out->n - before)) rc = ORACLE_EIO;
+            nvals = 0;
+            prev = kv[t].k; prevl = kv[t].kl;
+        }
+        ++nvals;
+    }
+    /* the final group is never written (no flush after the loop before :185) */
+    if (ofd >= 0) close(ofd);
+    free(kv); free(all.p); free(content.p);
+    return rc;
+}
+
 /* The reference job with its own structure, in directory `dir` (intermediates + outputs written
  * there as mr-{m}-{r}.txt / mr-{r}.txt).  Output bytes are also returned concatenated. */
 static int wc_faithful(const uint8_t *const *files, const size_t *lens, int n_files, uint32_t R,
                        const char *dir, bytes_t *out, size_t *part_off) {
-    char path[4096];
     int logfd = open("/dev/null", O_WRONLY);
     bytes_t scratch = {0};
     int rc = ORACLE_OK;
-    for (int m = 0; m < n_files && rc == ORACLE_OK; ++m) {
-        int *fds = (int *)malloc(sizeof(int) * R);
-        for (uint32_t r = 0; r < R; ++r) {                                   /* :120-125 */
-            snprintf(path, sizeof path, "%s/mr-%d-%u.txt", dir, m, r);
-            fds[r] = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-            if (fds[r] < 0) rc = ORACLE_EIO;
-        }
-        if (rc == ORACLE_OK) {
-            faithful_ud u = {fds, R, logfd, m, 0};
-            rc = tokenize(files[m], lens[m], cb_faithful, &u, &scratch);
-            if (u.err && rc == ORACLE_OK) rc = ORACLE_EIO;
-        }
-        for (uint32_t r = 0; r < R; ++r) if (fds[r] >= 0) close(fds[r]);
-        free(fds);
-    }
-    bytes_t content = {0};
+    for (int m = 0; m < n_files && rc == ORACLE_OK; ++m) rc = faithful_map_task(files[m], lens[m], m, R, dir, logfd, &scratch);
     for (uint32_t r = 0; r < R && rc == ORACLE_OK; ++r) {
-        /* read_file_to_mem_reduce :79-109 */
-        bytes_t all = {0};
-        size_t *starts = (size_t *)malloc(sizeof(size_t) * (size_t)(n_files + 1));
-        for (int m = 0; m < n_files && rc == ORACLE_OK; ++m) {
-            snprintf(path, sizeof path, "%s/mr-%d-%u.txt", dir, m, r);
-            starts[m] = all.n;
-            rc = read_all(path, &content);
-            if (rc == ORACLE_OK) by_put(&all, content.p, content.n);
-        }
-        size_t nkv = 0, cap = 1024;
-        kv_t *kv = (kv_t *)malloc(sizeof(kv_t) * cap);
-        size_t i = 0;
-        while (rc == ORACLE_OK && i < all.n) {
-            size_t e = i;
-            while (e < all.n && all.p[e] != '\n') ++e;
-            if (e > i) {
-                size_t sp = i;
-                while (sp < e && all.p[sp] != ' ') ++sp;
-                size_t sp2 = sp + 1;
-                while (sp2 < e && all.p[sp2] != ' ') ++sp2;
-                if (sp >= e || sp2 != e) { rc = ORACLE_EARG; break; }         /* assert!(len == 2) */
-                if (nkv == cap) { cap *= 2; kv = (kv_t *)realloc(kv, sizeof(kv_t) * cap); }
-                kv[nkv].k = all.p + i; kv[nkv].kl = (uint32_t)(sp - i);
-                kv[nkv].v = all.p + sp + 1; kv[nkv].vl = (uint32_t)(e - sp - 1);
-                ++nkv;
-            }
-            i = e + 1;
-        }
-        kv_t *tmp = (kv_t *)malloc(sizeof(kv_t) * (nkv ? nkv : 1));
-        merge_sort_kv(kv, tmp, nkv);                                         /* :162-164 */
-        free(tmp);
-        snprintf(path, sizeof path, "%s/mr-%u.txt", dir, r);
-        int ofd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-        if (ofd < 0) rc = ORACLE_EIO;
         part_off[r] = out->n;
-        const uint8_t *prev = NULL;
-        uint32_t prevl = 0;
-        uint64_t nvals = 0;
-        for (size_t t = 0; t < nkv && rc == ORACLE_OK; ++t) {                /* :169-184 */
-            if (!prev) { prev = kv[t].k; prevl = kv[t].kl; }
-            if (kv[t].kl != prevl || memcmp(kv[t].k, prev, prevl)) {
-                size_t before = out->n;
-                by_put(out, prev, prevl);
-                by_putc(out, ' ');
-                by_putu64(out, nvals);                                       /* wc::reduce */
-                by_putc(out, '\n');
-                if (write(ofd, out->p + before, out->n - before) != (ssize_t)(out->n - before)) rc = ORACLE_EIO;
-                nvals = 0;
-                prev = kv[t].k; prevl = kv[t].kl;
-            }
-            ++nvals;
-        }
-        /* the final group is never written (no flush after the loop before :185) */
-        if (ofd >= 0) close(ofd);
-        free(kv); free(all.p); free(starts);
+        rc = faithful_reduce_task(n_files, r, dir, out);
     }
     part_off[R] = out->n;
-    free(content.p);
     free(scratch.p);
     close(logfd);
     return rc;
@@ -612,6 +647,249 @@ int oracle_indexer(const uint8_t *const *files, const size_t *lens, const char *
     }
     map_free(&words); map_free(&pairs);
     if (rc) { free(o.p); return rc; }
+    *out = o.p ? o.p : (uint8_t *)malloc(1);
+    *out_len = o.n;
+    return ORACLE_OK;
+}
+
+/* ------------------------------------------------------------------ W worker threads (FAITHFUL) */
+
+/* The reference's process structure (mrworker.rs:43-149): W workers pull map task ids from the
+ * coordinator (coordinator.rs:137-176), then -- after every map task is done -- reduce task ids
+ * (:178-215).  Threads here, processes there; each task is the single-threaded FAITHFUL task. */
+typedef struct {
+    const uint8_t *const *files; const size_t *lens; int n_files; uint32_t R; const char *dir;
+    int next_map, next_reduce, rc; bytes_t *outs; pthread_mutex_t mu; pthread_barrier_t maps_done;
+} workers_t;
+
+static int take(workers_t *w, int *next, int limit) {
+    pthread_mutex_lock(&w->mu);
+    int t = (w->rc == ORACLE_OK && *next < limit) ? (*next)++ : -1;
+    pthread_mutex_unlock(&w->mu);
+    return t;
+}
+static void fail(workers_t *w, int rc) {
+    pthread_mutex_lock(&w->mu);
+    if (w->rc == ORACLE_OK) w->rc = rc;
+    pthread_mutex_unlock(&w->mu);
+}
+
+static void *worker_main(void *arg) {
+    workers_t *w = (workers_t *)arg;
+    int logfd = open("/dev/null", O_WRONLY);
+    bytes_t scratch = {0};
+    for (int m; (m = take(w, &w->next_map, w->n_files)) >= 0;) {
+        int rc = faithful_map_task(w->files[m], w->lens[m], m, w->R, w->dir, logfd, &scratch);
+        if (rc) fail(w, rc);
+    }
+    pthread_barrier_wait(&w->maps_done);   /* the coordinator's phase barrier (map_finish) */
+    for (int r; (r = take(w, &w->next_reduce, (int)w->R)) >= 0;) {
+        int rc = faithful_reduce_task(w->n_files, (uint32_t)r, w->dir, &w->outs[r]);
+        if (rc) fail(w, rc);
+    }
+    free(scratch.p);
+    close(logfd);
+    return NULL;
+}
+
+int oracle_wc_workers(const uint8_t *const *files, const size_t *lens, int n_files, uint32_t R, int W,
+                      const char *dir, uint8_t **out, size_t *out_len, size_t *part_off) {
+    if (R == 0 || n_files < 0 || W < 1 || !dir) return ORACLE_EARG;
+    workers_t w;
+    memset(&w, 0, sizeof w);
+    w.files = files; w.lens = lens; w.n_files = n_files; w.R = R; w.dir = dir; w.rc = ORACLE_OK;
+    w.outs = (bytes_t *)calloc(R, sizeof(bytes_t));
+    pthread_mutex_init(&w.mu, NULL);
+    pthread_barrier_init(&w.maps_done, NULL, (unsigned)W);
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)W);
+    for (int i = 0; i < W; ++i) pthread_create(&th[i], NULL, worker_main, &w);
+    for (int i = 0; i < W; ++i) pthread_join(th[i], NULL);
+    free(th);
+    pthread_barrier_destroy(&w.maps_done);
+    pthread_mutex_destroy(&w.mu);
+    bytes_t o = {0};
+    for (uint32_t r = 0; r < R; ++r) {
+        part_off[r] = o.n;
+        if (w.outs[r].n) by_put(&o, w.outs[r].p, w.outs[r].n);
+        free(w.outs[r].p);
+    }
+    part_off[R] = o.n;
+    free(w.outs);
+    if (w.rc) { free(o.p); return w.rc; }
+    *out = o.p ? o.p : (uint8_t *)malloc(1);
+    *out_len = o.n;
+    return ORACLE_OK;
+}
+
+/* ------------------------------------------------------------------ FAST on T threads */
+
+/* The input is cut into chunks at ASCII White_Space bytes (a token never spans one; UTF-8 never
+ * has a byte < 0x80 inside a multi-byte sequence), each thread counts its chunks into NSUB sub-maps
+ * chosen by the key's FNV hash, then sub-map p of every thread is merged by one thread, partitioned
+ * by SipHash % R, and every partition is sorted and written by one thread.  Output = oracle_wc FAST. */
+#define MT_NSUB 64
+typedef struct { const uint8_t *p; size_t n; } chunk_t;
+typedef struct { const uint8_t *k; uint32_t len; uint32_t part; uint64_t val; } kent_t;
+
+typedef struct {
+    chunk_t *chunks; size_t n_chunks; int T; uint32_t R;
+    map_t *sub;              /* [T][NSUB] */
+    kent_t **ents; size_t *n_ents;   /* per sub-map after the merge */
+    size_t **pcount;         /* [NSUB][R] entries of sub p in partition r */
+    bytes_t *outs;           /* per partition */
+    int next, rc; pthread_mutex_t mu; pthread_barrier_t bar;
+} mt_t;
+
+typedef struct { mt_t *g; int t; } mt_arg;
+typedef struct { map_t *sub; } mt_ud;
+
+static void cb_count_mt(void *ud, const uint8_t *k, size_t len) {
+    mt_ud *u = (mt_ud *)ud;
+    uint64_t h = fnv1a(k, len);
+    int added;
+    slot_t *s = map_find_or_add(&u->sub[h >> 58], k, len, &added);
+    s->val++;
+}
+
+static int mt_take(mt_t *g, int limit) {
+    pthread_mutex_lock(&g->mu);
+    int t = g->next < limit ? g->next++ : -1;
+    pthread_mutex_unlock(&g->mu);
+    return t;
+}
+
+static int cmp_kent(const void *x, const void *y) {
+    const kent_t *a = (const kent_t *)x, *b = (const kent_t *)y;
+    return cmp_bytes(a->k, a->len, b->k, b->len);
+}
+
+#include <time.h>
+static double now_s(void) { struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); return ts.tv_sec + 1e-9 * ts.tv_nsec; }
+static void *mt_main(void *arg) {
+    mt_arg *a = (mt_arg *)arg;
+    const int dbg = getenv("ORACLE_MT_DEBUG") != NULL;
+    double t0 = now_s();
+    mt_t *g = a->g;
+    const int t = a->t;
+    map_t *mine = &g->sub[(size_t)t * MT_NSUB];
+    bytes_t scratch = {0};
+    mt_ud u = {mine};
+    for (int c; (c = mt_take(g, (int)g->n_chunks)) >= 0;) {
+        int rc = tokenize(g->chunks[c].p, g->chunks[c].n, cb_count_mt, &u, &scratch);
+        if (rc) { pthread_mutex_lock(&g->mu); g->rc = rc; pthread_mutex_unlock(&g->mu); }
+    }
+    free(scratch.p);
+    if (dbg) fprintf(stderr, "t%d count %.3f\n", t, now_s() - t0);
+    if (pthread_barrier_wait(&g->bar) == PTHREAD_BARRIER_SERIAL_THREAD) g->next = 0;
+    pthread_barrier_wait(&g->bar);
+    if (dbg && t == 0) fprintf(stderr, "barrier1 %.3f\n", now_s() - t0);
+    /* merge sub-map p of every thread into thread 0's, then list its entries with their partition */
+    for (int p; (p = mt_take(g, MT_NSUB)) >= 0;) {
+        map_t *dst = &g->sub[p];
+        for (int o = 1; o < g->T; ++o) {
+            map_t *src = &g->sub[(size_t)o * MT_NSUB + p];
+            for (size_t i = 0; i < src->cap; ++i) {
+                if (!src->s[i].h) continue;
+                int added;
+                slot_t *d = map_find_or_add(dst, src->keys.p + src->s[i].off, src->s[i].len, &added);
+                d->val += src->s[i].val;
+            }
+            map_free(src);
+            memset(src, 0, sizeof *src);
+        }
+        kent_t *e = (kent_t *)malloc(sizeof(kent_t) * (dst->n ? dst->n : 1));
+        size_t k = 0;
+        g->pcount[p] = (size_t *)calloc(g->R, sizeof(size_t));
+        for (size_t i = 0; i < dst->cap; ++i) {
+            if (!dst->s[i].h) continue;
+            e[k].k = dst->keys.p + dst->s[i].off;
+            e[k].len = dst->s[i].len;
+            e[k].val = dst->s[i].val;
+            e[k].part = (uint32_t)(oracle_key_hash(e[k].k, e[k].len) % g->R);
+            g->pcount[p][e[k].part]++;
+            ++k;
+        }
+        g->ents[p] = e;
+        g->n_ents[p] = k;
+    }
+    if (pthread_barrier_wait(&g->bar) == PTHREAD_BARRIER_SERIAL_THREAD) g->next = 0;
+    pthread_barrier_wait(&g->bar);
+    if (dbg && t == 0) fprintf(stderr, "barrier2 %.3f\n", now_s() - t0);
+    /* partition r: gather, sort by key bytes, format, drop the last group */
+    for (int r; (r = mt_take(g, (int)g->R)) >= 0;) {
+        size_t n = 0;
+        for (int p = 0; p < MT_NSUB; ++p) n += g->pcount[p][r];
+        kent_t *e = (kent_t *)malloc(sizeof(kent_t) * (n ? n : 1));
+        size_t k = 0;
+        for (int p = 0; p < MT_NSUB; ++p)
+            for (size_t i = 0; i < g->n_ents[p]; ++i)
+                if (g->ents[p][i].part == (uint32_t)r) e[k++] = g->ents[p][i];
+        qsort(e, k, sizeof(kent_t), cmp_kent);
+        bytes_t *o = &g->outs[r];
+        for (size_t i = 0; i + 1 < k; ++i) {   /* worker.rs:169-184: the last group is never written */
+            by_put(o, e[i].k, e[i].len);
+            by_putc(o, ' ');
+            by_putu64(o, e[i].val);
+            by_putc(o, '\n');
+        }
+        free(e);
+    }
+    return NULL;
+}
+
+int oracle_wc_mt(const uint8_t *const *files, const size_t *lens, int n_files, uint32_t R, int T,
+                 uint8_t **out, size_t *out_len, size_t *part_off) {
+    if (R == 0 || n_files < 0 || T < 1) return ORACLE_EARG;
+    size_t total = 0;
+    for (int f = 0; f < n_files; ++f) total += lens[f];
+    const size_t target = total / ((size_t)T * 8) + (1u << 20);
+    size_t cap = 16, nc = 0;
+    chunk_t *ch = (chunk_t *)malloc(sizeof(chunk_t) * cap);
+    for (int f = 0; f < n_files; ++f) {
+        const uint8_t *s = files[f];
+        size_t a = 0;
+        while (a < lens[f]) {
+            size_t b = a + target < lens[f] ? a + target : lens[f];
+            while (b < lens[f] && !(s[b] == ' ' || (s[b] >= 0x09 && s[b] <= 0x0D))) ++b;
+            if (nc == cap) { cap *= 2; ch = (chunk_t *)realloc(ch, sizeof(chunk_t) * cap); }
+            ch[nc].p = s + a;
+            ch[nc].n = b - a;
+            ++nc;
+            a = b;
+        }
+    }
+    mt_t g;
+    memset(&g, 0, sizeof g);
+    g.chunks = ch; g.n_chunks = nc; g.T = T; g.R = R;
+    g.sub = (map_t *)calloc((size_t)T * MT_NSUB, sizeof(map_t));
+    for (size_t i = 0; i < (size_t)T * MT_NSUB; ++i) map_init(&g.sub[i], 1 << 10);
+    g.ents = (kent_t **)calloc(MT_NSUB, sizeof(kent_t *));
+    g.n_ents = (size_t *)calloc(MT_NSUB, sizeof(size_t));
+    g.pcount = (size_t **)calloc(MT_NSUB, sizeof(size_t *));
+    g.outs = (bytes_t *)calloc(R, sizeof(bytes_t));
+    pthread_mutex_init(&g.mu, NULL);
+    pthread_barrier_init(&g.bar, NULL, (unsigned)T);
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)T);
+    mt_arg *args = (mt_arg *)malloc(sizeof(mt_arg) * (size_t)T);
+    for (int t = 0; t < T; ++t) {
+        args[t].g = &g;
+        args[t].t = t;
+        pthread_create(&th[t], NULL, mt_main, &args[t]);
+    }
+    for (int t = 0; t < T; ++t) pthread_join(th[t], NULL);
+    bytes_t o = {0};
+    for (uint32_t r = 0; r < R; ++r) {
+        part_off[r] = o.n;
+        if (g.outs[r].n) by_put(&o, g.outs[r].p, g.outs[r].n);
+        free(g.outs[r].p);
+    }
+    part_off[R] = o.n;
+    for (size_t i = 0; i < (size_t)T * MT_NSUB; ++i) map_free(&g.sub[i]);
+    for (int p = 0; p < MT_NSUB; ++p) { free(g.ents[p]); free(g.pcount[p]); }
+    free(g.sub); free(g.ents); free(g.n_ents); free(g.pcount); free(g.outs); free(th); free(args); free(ch);
+    pthread_barrier_destroy(&g.bar);
+    pthread_mutex_destroy(&g.mu);
+    if (g.rc) { free(o.p); return g.rc; }
     *out = o.p ? o.p : (uint8_t *)malloc(1);
     *out_len = o.n;
     return ORACLE_OK;

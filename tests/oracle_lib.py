@@ -39,6 +39,13 @@ def lib():
                                      ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.c_uint32,
                                      ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t),
                                      ctypes.POINTER(ctypes.c_size_t)]
+        L.oracle_wc_workers.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                                         ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_char_p,
+                                         ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t),
+                                         ctypes.POINTER(ctypes.c_size_t)]
+        L.oracle_wc_mt.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
+                                   ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(u8p),
+                                   ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
         L.oracle_free.argtypes = [ctypes.c_void_p]
         _lib = L
     return _lib
@@ -118,3 +125,37 @@ def indexer(files, docs, n_reduce):
         raise OracleError(rc)
     buf = _take(out, olen.value)
     return _split(buf, list(offs), n_reduce)
+
+
+def wc_workers(files, n_reduce, workers, workdir=None):
+    """The reference structure (FAITHFUL tasks) on `workers` threads pulling map, then reduce tasks."""
+    L = lib()
+    n = len(files)
+    arr = (ctypes.c_char_p * max(n, 1))(*files)
+    lens = (ctypes.c_size_t * max(n, 1))(*[len(f) for f in files])
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    offs = (ctypes.c_size_t * (n_reduce + 1))()
+    with tempfile.TemporaryDirectory(prefix="oracle_wk_", dir=workdir) as d:
+        rc = L.oracle_wc_workers(arr, lens, n, n_reduce, workers, d.encode(), ctypes.byref(out), ctypes.byref(olen),
+                                 offs)
+    if rc:
+        raise OracleError(rc)
+    return _split(_take(out, olen.value), list(offs), n_reduce)
+
+
+def wc_mt(buffers, n_reduce, threads=8):
+    """FAST mode on `threads` threads.  buffers: bytes / bytearray / numpy uint8 arrays (not copied)."""
+    import numpy as np
+    L = lib()
+    arrs = [np.frombuffer(b, dtype=np.uint8) if not isinstance(b, np.ndarray) else b for b in buffers]
+    n = len(arrs)
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+    lens = (ctypes.c_size_t * max(n, 1))(*[a.size for a in arrs])
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    offs = (ctypes.c_size_t * (n_reduce + 1))()
+    rc = L.oracle_wc_mt(ptrs, lens, n, n_reduce, threads, ctypes.byref(out), ctypes.byref(olen), offs)
+    if rc:
+        raise OracleError(rc)
+    return _split(_take(out, olen.value), list(offs), n_reduce)

@@ -142,13 +142,17 @@ def test_document_offsets_and_tile_edges(ctx):
 
 @pytest.mark.parametrize("bits", [1, 4, 12, 20])
 def test_forced_hash_collisions(ctx, corpus, bits):
-    """Truncated internal hashes: output must be identical (collision-safe tie-breaks)."""
+    """Truncated internal hashes (every key in a few buckets and fingerprint runs): the output must
+    still equal the oracle's (collision-safe tie-breaks, the bucket aggregation's HBM overflow)."""
     import mapreduce_rust_amd as M
+    import oracle_lib as O
     from gpu_util import run_wc
     docs = corpus[:2] + [("".join("longprefix_shared_%05d " % (i % 700) for i in range(6000))).encode()]
-    base = run_wc(ctx, docs, 10)
+    exp = O.wc(docs, 10, O.FAST)
     got = run_wc(ctx, docs, 10, flags=M.debug_hash_bits(bits))
-    assert got == base
+    assert got == exp
+    if bits <= 4:
+        assert ctx.stats()["overflow_keys"] > 0   # keys past a bucket's LDS table: the exact HBM path ran
 
 
 def test_empty_inputs(ctx):

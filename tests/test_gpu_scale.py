@@ -1,0 +1,293 @@
+"""GPU parity at full size, on the capacity-overflow paths, and across ranks (all through the C ABI).
+
+* C3 at its full 10 GiB (BASELINE.json configs[2]) and a 1 GiB slice of C5 (configs[4]) against the
+  multi-threaded C oracle (tests/oracle_lib.wc_mt, FAST mode, run on the host over the same bytes).
+* The map's tail-region spill, grow-and-rerun and the aggregation's overflow regrow forced by the
+  test knobs MRG_TEST_TAIL_CAP / MRG_TEST_OVF_CAP / MRG_TEST_AGG_OCAP, against the oracle.
+* The exchange: the library's RCCL shuffle (mrg_job_shuffle) in a one-rank communicator, the
+  mrgpu CLI and mrg_run_job (GPU threads + communicator), a plain-C FFI host (worker_harness.c) and
+  two processes on the one GPU exchanging the library's export records over gloo.
+Reference for the path: src/mr/worker.rs:65-193, src/app/wc.rs:6-17, src/run.sh:16-20.
+"""
+import gzip
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+GOLDEN = json.load(open(os.path.join(HERE, "golden", "golden.json")))
+MIB = 1 << 20
+THREADS = min(16, os.cpu_count() or 4)   # the GPU box's CPU share is 16
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import mapreduce_rust_amd as M
+    c = M.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    return [gzip.open(os.path.join(HERE, "golden", "corpus", f"gut-{m}.txt.gz")).read() for m in range(6)]
+
+
+def _generate(ctx, kind, n_files, file_bytes, seed):
+    import torch
+    buf = torch.empty(n_files * file_bytes + 64, dtype=torch.uint8, device="cuda:0")
+    for i in range(n_files):
+        p = buf.data_ptr() + i * file_bytes
+        if kind == "zipf":
+            ctx.gen_zipf(p, file_bytes, seed, i, 1 << 20, 1.1)
+        else:
+            ctx.gen_unique(p, file_bytes, seed, i)
+    torch.cuda.synchronize()
+    return buf
+
+
+def _host_files(buf, n_files, file_bytes):
+    """D2H of the generated input, one numpy view per file (no second host copy)."""
+    import torch
+    host = np.empty(n_files * file_bytes, dtype=np.uint8)
+    torch.from_numpy(host).copy_(buf[:n_files * file_bytes])
+    return [host[i * file_bytes:(i + 1) * file_bytes] for i in range(n_files)]
+
+
+def _run_job(ctx, buf, n_files, file_bytes, R):
+    import mapreduce_rust_amd as M
+    ctx.job_begin(M.APP_WC, R)
+    ctx.set_input(buf.data_ptr(), [i * file_bytes for i in range(n_files + 1)])
+    ctx.map()
+    ctx.reduce()
+    return ctx.outputs()
+
+
+def test_c3_full_size_vs_oracle(ctx):
+    """configs[2]: 40 x 256 MiB of Zipf(1.1) text over 2^20 words, nReduce 64 -- every mr-{r}.txt
+    byte-identical to the oracle's on the same 10 GiB."""
+    import oracle_lib as O
+    nf, fb = 40, 256 * MIB
+    buf = _generate(ctx, "zipf", nf, fb, 0x5EED2026)
+    got = _run_job(ctx, buf, nf, fb, 64)
+    st = ctx.stats()
+    files = _host_files(buf, nf, fb)
+    del buf
+    exp = O.wc_mt(files, 64, threads=THREADS)
+    assert st["distinct_keys"] == 1 << 20
+    assert [sha(g) for g in got] == [sha(e) for e in exp]
+
+
+def test_c5_slice_vs_oracle(ctx):
+    """configs[4] (1e9 near-unique keys), a 1 GiB slice: 4 x 256 MiB, ~8e7 distinct 12-byte keys,
+    taken by the wide (sort-based) aggregation; byte-identical to the oracle."""
+    import oracle_lib as O
+    nf, fb = 4, 256 * MIB
+    buf = _generate(ctx, "unique", nf, fb, 0xC5C5)
+    got = _run_job(ctx, buf, nf, fb, 64)
+    st = ctx.stats()
+    files = _host_files(buf, nf, fb)
+    del buf
+    assert st["distinct_keys"] > 70_000_000
+    exp = O.wc_mt(files, 64, threads=THREADS)
+    assert len(got) == len(exp)
+    for r in range(64):
+        assert got[r] == exp[r], r
+
+
+@pytest.fixture
+def knobs():
+    keys = ["MRG_TEST_TAIL_CAP", "MRG_TEST_OVF_CAP", "MRG_TEST_AGG_OCAP", "MRG_WIDE"]
+    saved = {k: os.environ.get(k) for k in keys}
+
+    def set_(**kw):
+        for k in keys:
+            os.environ.pop(k, None)
+        for k, v in kw.items():
+            os.environ[k] = str(v)
+    yield set_
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+
+
+@pytest.mark.parametrize("wide", ["0", "1"])
+def test_map_spill_and_rerun_vs_oracle(ctx, corpus, knobs, wide):
+    """Tail regions of 1 record: (a) records spill into the per-bucket overflow lists (one launch);
+    (b) the lists are 16 records too: a launch overflows, regions grow to the measured demand and the
+    map reruns.  Both aggregation paths (bucketed / wide) must still equal the oracle."""
+    import torch
+    import oracle_lib as O
+    from gpu_util import run_wc
+    n = 16 * MIB
+    t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
+    ctx.gen_zipf(t.data_ptr(), n, 0x5EED2026, 7, 1 << 16, 1.1)
+    docs = corpus[:3] + [t[:n].cpu().numpy().tobytes()]
+    exp = O.wc(docs, 10, O.FAST)
+    knobs(MRG_TEST_TAIL_CAP=1, MRG_TEST_OVF_CAP=1 << 22, MRG_WIDE=wide)
+    assert run_wc(ctx, docs, 10) == exp
+    st = ctx.stats()
+    assert st["map_launches"] == 1 and st["map_spill"] > 100_000, st
+    knobs(MRG_TEST_TAIL_CAP=1, MRG_TEST_OVF_CAP=16, MRG_WIDE=wide)
+    assert run_wc(ctx, docs, 10) == exp
+    st = ctx.stats()
+    assert st["map_launches"] >= 2, st
+
+
+def test_aggregation_overflow_regrow_vs_oracle(ctx, corpus, knobs):
+    """Every key in one bucket (4-bit internal hashes), the HBM overflow list of the bucket
+    aggregation started at 1000 records: it overflows, is regrown and the aggregation reruns."""
+    import mapreduce_rust_amd as M
+    import oracle_lib as O
+    from gpu_util import run_wc
+    knobs(MRG_TEST_AGG_OCAP=1000, MRG_WIDE=0)
+    got = run_wc(ctx, corpus, 10, flags=M.debug_hash_bits(4))
+    st = ctx.stats()
+    assert st["agg_launches"] >= 2 and st["overflow_keys"] > 1000, st
+    assert got == O.wc(corpus, 10, O.FAST)
+
+
+def test_library_shuffle_single_rank(ctx, corpus):
+    """mrg_job_shuffle (RCCL inside libmrgpu.so) in a one-rank communicator: the counts all-to-all,
+    the own-slice copy and the import run; output = golden, no peer bytes."""
+    import mapreduce_rust_amd as M
+    from gpu_util import to_device
+    comm = M.Comm(ctx, M.comm_id(), 1, 0)
+    try:
+        for R in (10, 64):
+            t, off = to_device(corpus)
+            ctx.set_timing(True)
+            ctx.job_begin(M.APP_WC, R)
+            ctx.set_input(t.data_ptr(), off)
+            ctx.map()
+            ctx.shuffle(comm)
+            ctx.reduce()
+            outs = ctx.outputs()
+            st = ctx.stats()
+            ctx.set_timing(False)
+            assert [sha(o) for o in outs] == [GOLDEN["wc"][str(R)][f"mr-{r}.txt"] for r in range(R)]
+            assert st["exchange_sent"] == 0 and st["exchange_recv"] == 0 and st["ms_exchange"] >= 0.0
+            assert st["tokens"] == sum(GOLDEN["corpus"]["tokens"])
+    finally:
+        comm.close()
+
+
+def _data_dir(tmp_path, corpus, extra=None):
+    d = tmp_path / "data"
+    d.mkdir()
+    for m, c in enumerate(corpus + (extra or [])):
+        (d / f"gut-{m}.txt").write_bytes(c)
+
+
+def _cli(tmp_path, *args, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run([os.path.join(ROOT, "mapreduce_rust_amd", "lib", "mrgpu")] + [str(a) for a in args],
+                          cwd=tmp_path, env=e, capture_output=True, text=True, timeout=120)
+
+
+@pytest.mark.parametrize("force_comm", ["0", "1"])
+def test_mrgpu_cli_binary(tmp_path, corpus, force_comm):
+    """The mrgpu binary (no Python on the data path): `mrgpu 6 10 --gpus 1 --final` in a directory
+    holding data/gut-{m}.txt writes the golden mr-{r}.txt and final.txt.  force_comm=1 runs the
+    multi-GPU plan's code (GPU thread + RCCL communicator + mrg_job_shuffle) with one GPU."""
+    _data_dir(tmp_path, corpus)
+    p = _cli(tmp_path, 6, 10, "--gpus", 1, "--final", env={"MRG_TEST_FORCE_COMM": force_comm})
+    assert p.returncode == 0, p.stderr
+    for r in range(10):
+        assert sha((tmp_path / f"mr-{r}.txt").read_bytes()) == GOLDEN["wc"]["10"][f"mr-{r}.txt"], r
+    assert sha((tmp_path / "final.txt").read_bytes()) == GOLDEN["wc"]["10"]["final.txt"]
+
+
+def test_mrgpu_cli_indexer_and_errors(tmp_path, corpus):
+    _data_dir(tmp_path, corpus, extra=[b"fine words \xe2\x82 broken"])
+    p = _cli(tmp_path, 6, 10, "--app", "indexer", env={"MRG_TEST_FORCE_COMM": "1"})
+    assert p.returncode == 0, p.stderr
+    for r in range(10):
+        assert sha((tmp_path / f"mr-{r}.txt").read_bytes()) == GOLDEN["indexer"]["10"][f"mr-{r}.txt"], r
+    p = _cli(tmp_path, 7, 10, env={"MRG_TEST_FORCE_COMM": "1"})   # file 6 is not UTF-8 (worker.rs:75 panics)
+    assert p.returncode == 1 and "UTF-8" in p.stderr, p.stderr
+    p = _cli(tmp_path, 8, 10)                                       # data/gut-7.txt is missing
+    assert p.returncode == 1 and "gut-7" in p.stderr, p.stderr
+    p = _cli(tmp_path, 6, 10, "--gpus", 64)
+    assert p.returncode == 1 and "n_gpus" in p.stderr, p.stderr
+
+
+def test_ffi_c_host_worker_calls(tmp_path, corpus):
+    """A plain-C host making the calls Worker::map / Worker::reduce would make through an FFI crate
+    (mrg_map per file, then mrg_reduce per partition; worker.rs:142-193): golden mr-{r}.txt."""
+    _data_dir(tmp_path, corpus)
+    exe = os.path.join(HERE, "ffi", "build", "worker_harness")
+    for R in (10, 3):
+        p = subprocess.run([exe, "6", str(R)], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0, p.stderr
+        for r in range(R):
+            assert sha((tmp_path / f"mr-{r}.txt").read_bytes()) == GOLDEN["wc"][str(R)][f"mr-{r}.txt"], (R, r)
+    p = subprocess.run([exe, "6", "10", "--indexer"], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    for r in range(10):
+        assert sha((tmp_path / f"mr-{r}.txt").read_bytes()) == GOLDEN["indexer"]["10"][f"mr-{r}.txt"], r
+
+
+def _rank_main(rank, world, init_file, out_dir):
+    """One rank of a 2-process job on the one GPU: the library's map, export and import, the records
+    moved by torch.distributed gloo (host staged: RCCL does not put two ranks on one device)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, HERE)
+    import torch
+    import torch.distributed as dist
+    import mapreduce_rust_amd as M
+    from mapreduce_rust_amd import shuffle as S
+    from gpu_util import to_device
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    corpus = [gzip.open(os.path.join(HERE, "golden", "corpus", f"gut-{m}.txt.gz")).read() for m in range(6)]
+    res = {}
+    with M.Context(0) as c:
+        for R in (10, 64):
+            mine = S.shard_files(len(corpus), rank, world)
+            t, off = to_device([corpus[m] for m in mine])
+            c.job_begin(M.APP_WC, R)
+            c.set_input(t.data_ptr(), off, mine)
+            c.map()
+            n_rec, _ = S.shuffle(c, world, "cuda:0")
+            c.reduce()
+            outs = c.outputs()
+            res[str(R)] = {str(r): sha(outs[r]) for r in range(R) if r % world == rank}
+            res[str(R) + "_empty"] = all(outs[r] == b"" for r in range(R) if r % world != rank)
+            res[str(R) + "_n_rec"] = n_rec
+    with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+def test_two_ranks_library_exchange(tmp_path):
+    """C4's structure at world size 2: each rank maps its files (m % 2), mrg_job_export ->
+    all-to-all -> mrg_job_import, reduces the partitions it owns (r % 2); the union is golden."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_rank_main, args=(2, str(tmp_path / "init"), str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    merged = {"10": {}, "64": {}}
+    for rk in range(2):
+        res = json.load(open(tmp_path / f"rank{rk}.json"))
+        for R in ("10", "64"):
+            merged[R].update(res[R])
+            assert res[R + "_empty"] and res[R + "_n_rec"] > 0
+    for R in ("10", "64"):
+        assert sorted(int(r) for r in merged[R]) == list(range(int(R)))
+        for r in range(int(R)):
+            assert merged[R][str(r)] == GOLDEN["wc"][R][f"mr-{r}.txt"], (R, r)
