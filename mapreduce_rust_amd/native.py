@@ -25,6 +25,19 @@ def debug_hash_bits(n):
     return (n & 0xFF) << 8
 
 
+def kernel_source_sha():
+    """sha256 over the sources libmrgpu.so is built from (kernels, headers, host layer): keys the
+    committed PMC traffic figure (profiles/map_traffic.json) to the code it was measured on."""
+    import hashlib
+    d = os.path.join(_HERE, "csrc")
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".h", ".inc", ".cpp")) and f != "mrgpu_cli.cpp":
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
 def lib_path():
     return os.environ.get("MRG_LIB", os.path.join(_HERE, "lib", "libmrgpu.so"))
 

@@ -51,3 +51,23 @@ def test_record_layout_constant():
     assert "#define MRG_XREC_BYTES 40" in src
     from mapreduce_rust_amd import native, shuffle
     assert native.XREC_BYTES == shuffle.XREC == 40
+
+
+def test_rust_ffi_crate_declares_the_header():
+    """mrgpu-sys/src/lib.rs (not compiled here: no Rust toolchain) declares every entry point of
+    include/mrgpu.h with the same number of parameters, and mrg_stats with the same fields."""
+    hdr = open(os.path.join(ROOT, "include", "mrgpu.h")).read()
+    rs = open(os.path.join(ROOT, "mrgpu-sys", "src", "lib.rs")).read()
+    decl_c = {m.group(1): m.group(2) for m in re.finditer(r"^\s*(?:int|void|const char \*)\s*(mrg_\w+)\s*\(([^)]*)\)",
+                                                         hdr, re.M)}
+    decl_rs = {m.group(1): m.group(2) for m in re.finditer(r"pub fn (mrg_\w+)\(([^)]*)\)", rs, re.S)}
+    assert sorted(decl_c) == sorted(k for k in decl_rs if k in decl_c) == header_functions()
+
+    def arity(args):
+        a = args.strip()
+        return 0 if a in ("", "void") else a.count(",") + 1
+    for f, args in decl_c.items():
+        assert arity(args) == arity(decl_rs[f]), f
+    stats_c = re.findall(r"^\s+(?:uint64_t|uint32_t|double)\s+(\w+);", hdr.split("} mrg_stats;")[0], re.M)
+    stats_rs = re.findall(r"pub (\w+): (?:u64|u32|f64),", rs.split("pub struct mrg_stats")[1].split("}")[0])
+    assert stats_c == stats_rs

@@ -53,7 +53,10 @@ def main():
             raise SystemExit("need FETCH_SIZE and WRITE_SIZE rows for k_map")
         f, w = km[0]["FETCH_SIZE"], km[0]["WRITE_SIZE"]
         hbm = int((2 * f + w) * 1024)
-        doc = {"input_bytes": a.traffic, "hbm_bytes_per_launch": hbm,
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from mapreduce_rust_amd.native import kernel_source_sha
+        doc = {"input_bytes": a.traffic, "hbm_bytes_per_launch": hbm, "kernel_src_sha": kernel_source_sha(),
                "fetch_size_kib": f, "write_size_kib": w,
                "rule": "2 x FETCH_SIZE + WRITE_SIZE (KiB); gfx950 FETCH_SIZE halves 128-B streaming reads"}
         json.dump(doc, open(a.out, "w"), indent=1)
