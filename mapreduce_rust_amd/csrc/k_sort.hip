@@ -265,6 +265,10 @@ void mrg_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, 
     scan_rec<uint64_t>(in, out, n, tmp, s);
 }
 
+void mrg_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *tmp, hipStream_t s) {
+    scan_rec<uint32_t>(in, out, n, tmp, s);
+}
+
 uint64_t mrg_sort_tmp_bytes(uint64_t n) {
     const uint64_t ntiles = (n + TILE - 1) / TILE;
     return sizeof(unsigned long long) * 24 * 256 + sizeof(uint32_t) * (256 * ntiles + scan_tmp(256 * ntiles)) + 256;

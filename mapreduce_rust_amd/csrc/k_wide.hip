@@ -1,0 +1,1046 @@
+// k_wide.hip -- high-cardinality ("wide") aggregation and formatting for gfx950 (BASELINE config C5).
+//
+// When most tokens miss the map kernel's LDS combine (near-unique keys), the reduce side of the
+// reference -- sort every record by key (src/mr/worker.rs:162-164), group adjacent equal keys, call
+// wc::reduce and write "{key} {count}\n" per group (worker.rs:165-184, src/app/wc.rs:15-17) -- is
+// done by a two-level sample sort that moves each record three times instead of once per radix
+// digit:
+//   L1  records (16-byte packed keys) -> R x B1r buckets: partition r = SipHash-1-3(key) % R
+//       (worker.rs:111-115, 129), then quantile splitters of a global sample (per-tile histogram,
+//       scan, scatter);
+//   L2  one workgroup per L1 bucket: quantile splitters of an 8 Ki sample of the bucket sorted in LDS,
+//       histogram, scatter into leaves of ~1 Ki records;
+//   leaf one workgroup per L1 bucket walks its leaves: an LDS hash table sums the leaf's records
+//       (count 1) and the map tables' flushed counts (the "weighted" keys, pre-aggregated and sorted),
+//       an LDS LSD radix sort over the key bytes that vary inside the leaf orders the distinct keys,
+//       which are written in place with their counts, plus the leaf's line bytes;
+//   write after a scan of the leaf byte totals (and the last-group drop of worker.rs:169-184 applied
+//       to the last non-empty leaf of each partition), one workgroup per L1 bucket formats its
+//       leaves' lines through LDS and stores them as whole dwords.
+// Leaves whose distinct keys do not fit the LDS table (sample outliers, adversarial key sets) are
+// listed and finished by a global radix sort of their records (mrgpu.cpp).
+// Order within a leaf: (k0, k1) unsigned = key bytes (mrg_device.h), one partition per L1 bucket.
+#include "mrg_device.h"
+#include "mrg_internal.h"
+
+namespace {
+
+#define GASW __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ GASW T *gw(T *p) {
+    return (GASW T *)p;
+}
+
+constexpr int W_WG = 1024;
+constexpr int W_NW = W_WG / 64;
+constexpr uint32_t W_S2 = 8192;       // L2 samples per L1 bucket (sorted in LDS)
+constexpr uint32_t W_SLOTS = 4096;    // leaf LDS table slots
+constexpr uint32_t W_MAXD = 3072;     // distinct keys a leaf may hold (75 % load)
+constexpr uint32_t W_SEGLDS = 2048;   // segment offsets cached in LDS per L1 tile
+
+__device__ __forceinline__ bool key_lt(uint64_t a0, uint64_t a1, uint64_t b0, uint64_t b1) {
+    return a0 < b0 || (a0 == b0 && a1 < b1);
+}
+
+// ---------------------------------------------------------------- the map's records (count 1)
+// main segments: the tail regions (bucket-major, map workgroup minor), then the per-bucket
+// overflow lists -- the order of mrg_launch_wmain_counts
+__device__ __forceinline__ void main_rec(const BucketArgs &A, uint64_t s, uint64_t i, uint64_t &k0, uint64_t &k1) {
+    const uint64_t nt = (uint64_t)A.nreg * MRG_NBUCKET;
+    const GASW uint64_t *p;
+    if (s < nt) {
+        const uint32_t b = (uint32_t)(s / A.nreg), w = (uint32_t)(s % A.nreg);
+        p = gw(A.pool) + 2 * (A.rbase[b] + (uint64_t)w * A.bcap[b] + i);
+    } else {
+        p = gw(A.movf) + 2 * ((s - nt) * A.mocap + i);
+    }
+    const uint64_t a = p[0], b = p[1];
+    k0 = a;
+    k1 = b;
+}
+
+// s in [lo, hi) with off[s] <= i < off[s + 1]  (off non-decreasing; empty segments are skipped)
+template <class OFF>
+__device__ __forceinline__ uint64_t seg_find(const OFF &off, uint64_t lo, uint64_t hi, uint64_t i) {
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (off(mid) <= i) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint32_t part_of(uint64_t k0, uint64_t k1, uint32_t R) {
+    return (uint32_t)(mrg_siphash_short(k0, k1, mrg_short_len(k0, k1)) % (uint64_t)R);
+}
+
+// number of splitters <= key among sp[0 .. m)
+template <class SP>
+__device__ __forceinline__ uint32_t upper_idx(const SP &sp, uint32_t m, uint64_t k0, uint64_t k1) {
+    uint32_t lo = 0, hi = m;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        uint64_t s0, s1;
+        sp(mid, s0, s1);
+        if (key_lt(k0, k1, s0, s1)) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+__global__ void k_wmain_counts(BucketArgs A, uint64_t *cnt) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nt = (uint64_t)A.nreg * MRG_NBUCKET;
+    if (s < nt) {
+        const uint32_t b = (uint32_t)(s / A.nreg), w = (uint32_t)(s % A.nreg);
+        cnt[s] = min(A.bcount[(uint64_t)w * MRG_NBUCKET + b], A.bcap[b]);
+    } else if (s < nt + MRG_NBUCKET) {
+        cnt[s] = min(A.monext[s - nt], A.mocap);
+    }
+}
+
+// flushed map tables: weighted entries (count fcnt) as plain arrays for the HBM-table aggregation
+__global__ void k_wflush_counts(BucketArgs A, uint64_t *cnt) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w < A.nreg) cnt[w] = A.foff[(uint64_t)w * (MRG_NBUCKET + 1) + MRG_NBUCKET];
+}
+__global__ void k_wflush_gather(BucketArgs A, const uint64_t *off, uint64_t *k0, uint64_t *k1, uint32_t *c) {
+    const uint32_t w = blockIdx.x;
+    const uint64_t o = off[w], n = off[w + 1] - o;
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint64_t j = (uint64_t)w * A.regcap + i;
+        k0[o + i] = A.fk0[j];
+        k1[o + i] = A.fk1[j];
+        c[o + i] = A.fcnt[j];
+    }
+}
+
+// ---------------------------------------------------------------- L1: sample, splitters
+__global__ void k_wsample1(BucketArgs A, const uint64_t *off, uint64_t nseg, uint64_t n, uint32_t S, uint32_t R,
+                           SortRec *out) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= S) return;
+    const uint64_t i = ((2ull * j + 1ull) * n) / (2ull * S);
+    const uint64_t s = seg_find([&](uint64_t x) { return off[x]; }, 0, nseg, i);
+    uint64_t k0, k1;
+    main_rec(A, s, i - off[s], k0, k1);
+    SortRec r;
+    r.k0 = k0;
+    r.k1 = k1;
+    r.part = part_of(k0, k1, R);
+    r.doc = 0;
+    r.idx = j;
+    r.pad = 0;
+    out[j] = r;
+}
+
+// splitter q (< B1r - 1) of partition r: the sample at quantile (q + 1) / B1r of partition r's samples
+__global__ void k_wsplit1(const SortRec *smp, uint32_t S, uint32_t R, uint32_t B1r, uint64_t *spl) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t m = B1r - 1u;
+    if (t >= R * m) return;
+    const uint32_t r = t / m, q = t % m;
+    auto lower = [&](uint32_t p) {  // first sample with part >= p
+        uint32_t lo = 0, hi = S;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (smp[mid].part < p) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    };
+    const uint32_t lo = lower(r), hi = lower(r + 1u);
+    uint64_t a = 0, b = 0;  // no sample: every key of r lands in the partition's last bucket
+    if (hi > lo) {
+        const uint32_t k = lo + (uint32_t)(((uint64_t)(q + 1u) * (hi - lo)) / B1r);
+        const uint32_t kk = k < hi ? k : hi - 1u;
+        a = smp[kk].k0;
+        b = smp[kk].k1;
+    }
+    spl[2ull * t] = a;
+    spl[2ull * t + 1] = b;
+}
+
+struct L1Args {
+    BucketArgs A;
+    const uint64_t *off;     // main segment offsets [nseg + 1]
+    uint64_t nseg, n;
+    const uint64_t *spl1;    // [R][B1r - 1] (k0, k1)
+    uint32_t R, B1r, B1, ntiles;
+    uint32_t *cnt;           // [B1][ntiles] (scanned in place between the two kernels)
+    uint64_t *out;           // L1 output, 2 words per record
+};
+
+// L1 tile t: records [t * T1, min(n, (t+1) * T1)); WITH_SCATTER: write them, else count them
+template <bool SCATTER>
+__global__ __launch_bounds__(W_WG, 1) void k_wl1(L1Args L) {
+    extern __shared__ uint64_t s_dyn[];  // spl1 (2 * R * (B1r-1) u64) | hist (B1 u32) | seg offsets
+    uint64_t *s_spl = s_dyn;
+    const uint32_t m = L.B1r - 1u;
+    uint32_t *s_h = reinterpret_cast<uint32_t *>(s_spl + 2ull * L.R * m);
+    uint64_t *s_off = reinterpret_cast<uint64_t *>(s_h + ((L.B1 + 1u) & ~1u));
+    __shared__ uint64_t s_lo, s_hi;
+    const uint32_t tid = threadIdx.x, t = blockIdx.x;
+    const uint64_t t0 = (uint64_t)t * MRG_WIDE_T1, t1 = min(L.n, t0 + MRG_WIDE_T1);
+    for (uint32_t i = tid; i < 2u * L.R * m; i += W_WG) s_spl[i] = L.spl1[i];
+    for (uint32_t b = tid; b < L.B1; b += W_WG) s_h[b] = SCATTER ? L.cnt[(uint64_t)b * L.ntiles + t] : 0u;
+    if (tid == 0) {
+        const auto off = [&](uint64_t x) { return L.off[x]; };
+        s_lo = seg_find(off, 0, L.nseg, t0);
+        s_hi = seg_find(off, 0, L.nseg, t1 - 1u) + 1u;
+    }
+    __syncthreads();
+    const uint64_t slo = s_lo, shi = s_hi;
+    const bool cached = shi - slo + 1u <= W_SEGLDS;
+    if (cached)
+        for (uint64_t x = slo + tid; x <= shi; x += W_WG) s_off[x - slo] = L.off[x];
+    __syncthreads();
+    for (uint64_t i = t0 + tid; i < t1; i += W_WG) {
+        uint64_t s;
+        if (cached) s = seg_find([&](uint64_t x) { return s_off[x - slo]; }, slo, shi, i);
+        else s = seg_find([&](uint64_t x) { return L.off[x]; }, slo, shi, i);
+        uint64_t k0, k1;
+        main_rec(L.A, s, i - (cached ? s_off[s - slo] : L.off[s]), k0, k1);
+        const uint32_t r = part_of(k0, k1, L.R);
+        const uint32_t q = upper_idx(
+            [&](uint32_t x, uint64_t &a, uint64_t &b) {
+                a = s_spl[2ull * (r * m + x)];
+                b = s_spl[2ull * (r * m + x) + 1];
+            },
+            m, k0, k1);
+        const uint32_t b = r * L.B1r + q;
+        const uint32_t pos = atomicAdd(&s_h[b], 1u);
+        if (SCATTER) {
+            typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+            *reinterpret_cast<GASW v2 *>(gw(L.out) + 2ull * pos) = v2{k0, k1};
+        }
+    }
+    if (!SCATTER) {
+        __syncthreads();
+        for (uint32_t b = tid; b < L.B1; b += W_WG) L.cnt[(uint64_t)b * L.ntiles + t] = s_h[b];
+    }
+}
+
+// bucket b starts at the scanned count of (b, tile 0); bstart[B1] = n
+__global__ void k_wbstart(const uint32_t *cnt, uint32_t B1, uint32_t ntiles, uint64_t n, uint64_t *bstart) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < B1) bstart[b] = cnt[(uint64_t)b * ntiles];
+    else if (b == B1) bstart[b] = n;
+}
+
+// ---------------------------------------------------------------- block helpers (1024 threads)
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
+    const uint32_t lane = __lane_id();
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(v, o);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
+// exclusive block scan of one value per thread; s_ws holds W_NW words; *total = sum
+__device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t *s_ws, uint32_t *total) {
+    const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+    const uint32_t inc = wave_scan_incl(v);
+    if (lane == 63) s_ws[w] = inc;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (uint32_t i = 0; i < (uint32_t)W_NW; ++i) {
+        const uint32_t x = s_ws[i];
+        base += i < w ? x : 0u;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + inc - v;
+}
+
+// ---------------------------------------------------------------- L2: per L1 bucket
+struct L2Args {
+    const uint64_t *in;      // L1 output (2 words per record)
+    uint64_t *out;           // leaf order (2 words per record)
+    const uint64_t *bstart;  // [B1 + 1]
+    const uint64_t *spl1;
+    uint32_t B1r, target;
+    uint32_t *nleaf;         // [B1]
+    uint64_t *leaf_lo;       // [B1 * MAXB2 + 1] first record of each leaf (absolute)
+    uint64_t *leaf_lb;       // [B1 * MAXB2][2] lower key bound of each leaf
+};
+
+__global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
+    __shared__ uint64_t s_smp[2 * W_S2];            // samples (k0, k1), bitonic-sorted
+    __shared__ uint64_t s_spl[2 * (MRG_WIDE_MAXB2 - 1)];
+    __shared__ uint32_t s_cnt[MRG_WIDE_MAXB2];
+    __shared__ uint32_t s_cur[MRG_WIDE_MAXB2];
+    __shared__ uint32_t s_ws[W_NW];
+    const uint32_t tid = threadIdx.x, b = blockIdx.x;
+    const uint64_t base = L.bstart[b], nb = L.bstart[b + 1] - base;
+    uint32_t B2 = (uint32_t)min<uint64_t>((nb + L.target - 1) / L.target, MRG_WIDE_MAXB2);
+    if (B2 < 1) B2 = 1;
+    const GASW uint64_t *in = gw(L.in) + 2 * base;
+    // ---- splitters from a sorted sample
+    if (B2 > 1) {
+        const uint32_t S = (uint32_t)min<uint64_t>(nb, W_S2);
+        uint32_t P = 1;
+        while (P < S) P <<= 1;
+        for (uint32_t k = tid; k < P; k += W_WG) {
+            uint64_t a = ~0ull, c = ~0ull;  // padding sorts last
+            if (k < S) {
+                const uint64_t i = ((2ull * k + 1ull) * nb) / (2ull * S);
+                a = in[2 * i];
+                c = in[2 * i + 1];
+            }
+            s_smp[2 * k] = a;
+            s_smp[2 * k + 1] = c;
+        }
+        __syncthreads();
+        for (uint32_t size = 2; size <= P; size <<= 1) {
+            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                for (uint32_t t = tid; t < P / 2; t += W_WG) {
+                    const uint32_t i = 2 * t - (t & (stride - 1));  // low element of the pair
+                    const uint32_t j = i + stride;
+                    const bool up = (i & size) == 0;
+                    const uint64_t a0 = s_smp[2 * i], a1 = s_smp[2 * i + 1], b0 = s_smp[2 * j], b1 = s_smp[2 * j + 1];
+                    if (key_lt(b0, b1, a0, a1) == up) {
+                        s_smp[2 * i] = b0; s_smp[2 * i + 1] = b1;
+                        s_smp[2 * j] = a0; s_smp[2 * j + 1] = a1;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (uint32_t q = tid; q + 1 < B2; q += W_WG) {
+            const uint32_t k = (uint32_t)(((uint64_t)(q + 1u) * S) / B2);
+            s_spl[2 * q] = s_smp[2 * k];
+            s_spl[2 * q + 1] = s_smp[2 * k + 1];
+        }
+    }
+    for (uint32_t j = tid; j < MRG_WIDE_MAXB2; j += W_WG) {
+        s_cnt[j] = 0;
+        s_cur[j] = 0;
+    }
+    __syncthreads();
+    auto sub_of = [&](uint64_t k0, uint64_t k1) {
+        return upper_idx([&](uint32_t x, uint64_t &a, uint64_t &c) { a = s_spl[2 * x]; c = s_spl[2 * x + 1]; }, B2 - 1u,
+                         k0, k1);
+    };
+    // ---- histogram
+    for (uint64_t i = tid; i < nb; i += W_WG) atomicAdd(&s_cnt[sub_of(in[2 * i], in[2 * i + 1])], 1u);
+    __syncthreads();
+    {  // exclusive scan of the B2 <= 1024 counts, one per thread
+        const uint32_t v = tid < B2 ? s_cnt[tid] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_scan_excl(v, s_ws, &tot);
+        if (tid < B2) s_cur[tid] = ex;
+        const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + tid;
+        if (tid < B2) {
+            L.leaf_lo[lid] = base + ex;
+            uint64_t a, c;
+            if (tid > 0) {
+                a = s_spl[2 * (tid - 1)];
+                c = s_spl[2 * (tid - 1) + 1];
+            } else {  // the L1 bucket's own lower bound
+                const uint32_t q = b % L.B1r, r = b / L.B1r;
+                if (q == 0) { a = 0; c = 0; }
+                else {
+                    a = L.spl1[2ull * (r * (L.B1r - 1u) + q - 1u)];
+                    c = L.spl1[2ull * (r * (L.B1r - 1u) + q - 1u) + 1];
+                }
+            }
+            L.leaf_lb[2 * lid] = a;
+            L.leaf_lb[2 * lid + 1] = c;
+        }
+        if (tid == 0) L.nleaf[b] = B2;
+    }
+    __syncthreads();
+    // ---- scatter
+    GASW uint64_t *out = gw(L.out) + 2 * base;
+    for (uint64_t i = tid; i < nb; i += W_WG) {
+        const uint64_t k0 = in[2 * i], k1 = in[2 * i + 1];
+        const uint32_t pos = atomicAdd(&s_cur[sub_of(k0, k1)], 1u);
+        typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<GASW v2 *>(out + 2ull * pos) = v2{k0, k1};
+    }
+}
+
+// ---------------------------------------------------------------- leaves
+struct LeafArgs {
+    const uint64_t *kin;     // records in leaf order, 2 words each
+    uint64_t *kout;          // distinct keys, 2 words each, at slot leaf_out[leaf] + i
+    const uint64_t *bstart;
+    const uint32_t *nleaf;
+    const uint64_t *leaf_lo, *leaf_lb;
+    uint32_t B1r, R;
+    // weighted keys (flushed map tables, aggregated), sorted by (part, k0, k1)
+    const uint64_t *wk0, *wk1, *wcnt;
+    const uint32_t *wpart;
+    uint64_t nw;
+    uint32_t maxd;           // distinct keys a leaf may hold (W_MAXD; test knob smaller)
+    // outputs: out key slot = leaf_lo + (weighted keys before the leaf); [slot] counts
+    uint64_t *ocnt;
+    uint64_t *leaf_out;      // first output slot of each leaf
+    uint32_t *leaf_nd;       // distinct keys written (0 for an overflowed leaf)
+    uint64_t *leaf_bytes;    // bytes of the leaf's lines "{key} {count}\n"
+    uint32_t *leaf_last;     // bytes of its last line
+    uint32_t *ovf_list;      // overflowed leaves (ids)
+    unsigned long long *ovf_n;
+    unsigned long long *nkeys;
+    uint64_t *wr;            // [leaves][2] weighted-key range of each leaf (k_wranges)
+};
+
+// first weighted key >= (p, a, b)
+__device__ __forceinline__ uint64_t w_lower(const LeafArgs &L, uint32_t p, uint64_t a, uint64_t b) {
+    uint64_t lo = 0, hi = L.nw;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        const uint32_t mp = L.wpart[mid];
+        const bool less = mp < p || (mp == p && key_lt(L.wk0[mid], L.wk1[mid], a, b));
+        if (less) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint32_t w_hash(uint64_t a, uint64_t b) {
+    return (uint32_t)(mrg_fmix64(a ^ mrg_fmix64(b)) >> 20);
+}
+__device__ __forceinline__ uint32_t line_len(uint64_t k0, uint64_t k1, uint64_t c) {
+    return mrg_short_len(k0, k1) + 2u + mrg_ndigits(c);
+}
+__device__ __forceinline__ uint32_t key_byte(uint64_t k0, uint64_t k1, uint32_t q) {
+    return q < 8u ? (uint32_t)(k0 >> (56u - 8u * q)) & 0xFFu : (uint32_t)(k1 >> (56u - 8u * (q - 8u))) & 0xFFu;
+}
+
+// weighted-key range [wr[2l], wr[2l+1]) of every leaf l: partition r's keys in [lb_l, lb_{l+1})
+__device__ __forceinline__ void leaf_wrange(const LeafArgs &L, uint64_t lid, uint64_t &wlo, uint64_t &whi) {
+    const uint32_t b = (uint32_t)(lid / MRG_WIDE_MAXB2), j = (uint32_t)(lid % MRG_WIDE_MAXB2);
+    const uint32_t r = b / L.B1r, nl = L.nleaf[b];
+    wlo = w_lower(L, r, L.leaf_lb[2 * lid], L.leaf_lb[2 * lid + 1]);
+    if (j + 1 < nl) whi = w_lower(L, r, L.leaf_lb[2 * lid + 2], L.leaf_lb[2 * lid + 3]);
+    else if ((b + 1) % L.B1r != 0) {  // next L1 bucket of the same partition
+        const uint64_t nid = (uint64_t)(b + 1) * MRG_WIDE_MAXB2;
+        whi = w_lower(L, r, L.leaf_lb[2 * nid], L.leaf_lb[2 * nid + 1]);
+    } else whi = w_lower(L, r + 1u, 0, 0);
+}
+__global__ void k_wranges(LeafArgs L, uint32_t B1) {
+    const uint64_t lid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lid >= (uint64_t)B1 * MRG_WIDE_MAXB2) return;
+    const uint32_t b = (uint32_t)(lid / MRG_WIDE_MAXB2), j = (uint32_t)(lid % MRG_WIDE_MAXB2);
+    if (j >= L.nleaf[b]) return;
+    uint64_t lo = 0, hi = 0;
+    if (L.nw) leaf_wrange(L, lid, lo, hi);
+    L.wr[2 * lid] = lo;
+    L.wr[2 * lid + 1] = hi;
+}
+
+// 12 bits of the 128-bit big-endian key (k0:k1) starting at bit position hb (0 = most significant)
+__device__ __forceinline__ uint32_t key_bits12(uint64_t k0, uint64_t k1, uint32_t hb) {
+    // top 64 bits of (k0:k1) << hb
+    const uint64_t t = hb == 0 ? k0 : (hb < 64 ? (k0 << hb) | (k1 >> (64 - hb)) : k1 << (hb - 64));
+    return (uint32_t)(t >> 52);
+}
+
+// One workgroup per L1 bucket walks its leaves.  Per leaf: sum the records per key in an LDS hash
+// table, list the distinct keys, bucket them by the 12 key bits after their common prefix (a
+// counting sort), order each bucket by comparing its (few) keys, write keys + counts + line bytes.
+// A leaf whose buckets are large (keys that agree beyond those 12 bits) is ordered by an LSD radix
+// sort over its varying key bytes instead.
+constexpr uint32_t W_NDIG = 4096;         // 12-bit digits
+constexpr uint32_t W_MAXBKT = 64;         // largest bucket ordered by comparisons
+
+__global__ __launch_bounds__(W_WG, 1) void k_wleaf(LeafArgs L) {
+    __shared__ uint64_t s_k[2 * W_SLOTS];     // table keys (k0, k1); k0 == 0 = empty
+    __shared__ uint64_t s_c[W_SLOTS];         // counts
+    __shared__ uint16_t s_ia[W_MAXD], s_ib[W_MAXD];   // slot lists
+    __shared__ __attribute__((aligned(16))) uint16_t s_x[3 * W_NW * 256];  // digit counts + starts / radix cells (24 KiB)
+    __shared__ uint32_t s_ws[W_NW];
+    __shared__ uint32_t s_nd, s_ovf, s_maxb;
+    __shared__ uint64_t s_or0, s_or1;
+    uint32_t *s_dcnt = reinterpret_cast<uint32_t *>(s_x);   // counting sort: per-digit count (16 KiB)
+    uint16_t *s_doff = s_x + 2 * W_NDIG;                     // and start (8 KiB)
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t b = blockIdx.x;
+    const uint32_t nl = L.nleaf[b];
+    const uint64_t bend = L.bstart[b + 1];
+    const uint64_t lt = mrg_lanemask_lt();
+    for (uint32_t j = 0; j < nl; ++j) {
+        const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + j;
+        const uint64_t mlo = L.leaf_lo[lid], mhi = j + 1 < nl ? L.leaf_lo[lid + 1] : bend;
+        const uint64_t wlo = L.wr[2 * lid], whi = L.wr[2 * lid + 1];
+        const uint64_t nm = mhi - mlo, nwk = whi - wlo;
+        const uint64_t out0 = mlo + wlo;
+        // table size: a power of two >= 2 x records (a leaf of duplicates still fits: distinct counts)
+        uint32_t S = 64;
+        while (S < W_SLOTS && (uint64_t)S < 2 * (nm + nwk)) S <<= 1;
+        for (uint32_t i = tid; i < S; i += W_WG) {
+            s_k[2 * i] = MRG_EMPTY_K0;
+            s_k[2 * i + 1] = MRG_EMPTY_K1;
+            s_c[i] = 0;
+        }
+        if (tid == 0) {
+            s_nd = 0;
+            s_ovf = 0;
+            s_maxb = 0;
+            s_or0 = 0;
+            s_or1 = 0;
+        }
+        __syncthreads();
+        // ---- sum the records per key (exact: full keys compared; slots fill monotonically)
+        auto add = [&](uint64_t a, uint64_t c, uint64_t n) {
+            uint32_t slot = w_hash(a, c) & (S - 1u);
+            for (uint32_t p = 0; p < S; ++p) {
+                const uint64_t ka = s_k[2 * slot], kb = s_k[2 * slot + 1];
+                if (ka == a && kb == c) {
+                    atomicAdd((unsigned long long *)&s_c[slot], (unsigned long long)n);
+                    return;
+                }
+                if (ka == MRG_EMPTY_K0 || (ka == a && kb == MRG_EMPTY_K1)) {
+                    const unsigned long long x = atomicCAS((unsigned long long *)&s_k[2 * slot], MRG_EMPTY_K0, a);
+                    if (x == MRG_EMPTY_K0 || x == a) {
+                        const unsigned long long y =
+                            atomicCAS((unsigned long long *)&s_k[2 * slot + 1], MRG_EMPTY_K1, c);
+                        if (y == MRG_EMPTY_K1 || y == c) {
+                            // a slot becomes a key exactly once, by the CAS that sets k1
+                            if (y == MRG_EMPTY_K1 && atomicAdd(&s_nd, 1u) >= L.maxd) s_ovf = 1;
+                            atomicAdd((unsigned long long *)&s_c[slot], (unsigned long long)n);
+                            return;
+                        }
+                    }
+                }
+                slot = (slot + 1u) & (S - 1u);
+            }
+            s_ovf = 1;  // no slot left
+        };
+        const GASW uint64_t *km = gw(L.kin) + 2 * mlo;
+        for (uint64_t i = tid; i < nm; i += W_WG) {
+            if (s_ovf) break;
+            add(km[2 * i], km[2 * i + 1], 1ull);
+        }
+        for (uint64_t i = tid; i < nwk; i += W_WG) {
+            if (s_ovf) break;
+            add(L.wk0[wlo + i], L.wk1[wlo + i], L.wcnt[wlo + i]);
+        }
+        __syncthreads();
+        if (s_ovf) {  // finished by the global fallback (mrgpu.cpp)
+            if (tid == 0) {
+                const unsigned long long k = atomicAdd(L.ovf_n, 1ull);
+                L.ovf_list[k] = (uint32_t)lid;
+                L.leaf_out[lid] = out0;
+                L.leaf_nd[lid] = 0;
+                L.leaf_bytes[lid] = 0;
+                L.leaf_last[lid] = 0;
+            }
+            __syncthreads();
+            continue;
+        }
+        // ---- list the occupied slots (s_ia), the bits on which keys differ, clear the digit counts
+        const uint32_t D = s_nd;
+        __syncthreads();
+        if (tid == 0) s_nd = 0;
+        for (uint32_t i = tid; i < W_NDIG; i += W_WG) s_dcnt[i] = 0;
+        __syncthreads();
+        for (uint32_t i0 = 0; i0 < S; i0 += W_WG) {
+            const uint32_t i = i0 + tid;
+            const bool full = i < S && s_k[2 * i] != MRG_EMPTY_K0;
+            const uint64_t m = __ballot(full);
+            uint32_t basew = 0;
+            if (lane == 0 && m) basew = atomicAdd(&s_nd, (uint32_t)__popcll(m));
+            basew = __shfl(basew, 0);
+            if (full) s_ia[basew + (uint32_t)__popcll(m & lt)] = (uint16_t)i;
+        }
+        __syncthreads();
+        uint64_t f0 = 0, f1 = 0;
+        if (D) {
+            f0 = s_k[2 * s_ia[0]];
+            f1 = s_k[2 * s_ia[0] + 1];
+        }
+        {
+            uint64_t o0 = 0, o1 = 0;
+            for (uint32_t p = tid; p < D; p += W_WG) {
+                o0 |= s_k[2 * s_ia[p]] ^ f0;
+                o1 |= s_k[2 * s_ia[p] + 1] ^ f1;
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                o0 |= __shfl_xor(o0, o);
+                o1 |= __shfl_xor(o1, o);
+            }
+            if (lane == 0 && (o0 | o1)) {
+                atomicOr((unsigned long long *)&s_or0, (unsigned long long)o0);
+                atomicOr((unsigned long long *)&s_or1, (unsigned long long)o1);
+            }
+        }
+        __syncthreads();
+        const uint64_t o0 = s_or0, o1 = s_or1;
+        // first differing bit (0 = most significant bit of k0); the digit = the 12 bits from there
+        uint32_t hb = o0 ? (uint32_t)__builtin_clzll(o0) : (o1 ? 64u + (uint32_t)__builtin_clzll(o1) : 0u);
+        if (hb > 116u) hb = 116u;
+        // ---- counting sort by digit: bucket counts, then starts
+        uint32_t dg[3], sl[3], within[3];
+        const uint32_t NR = (D + W_WG - 1) / W_WG;   // items per thread (<= 3)
+        for (uint32_t k = 0; k < NR; ++k) {
+            const uint32_t p = k * W_WG + tid;
+            dg[k] = 0xFFFFFFFFu;
+            if (p < D) {
+                sl[k] = s_ia[p];
+                dg[k] = key_bits12(s_k[2 * sl[k]], s_k[2 * sl[k] + 1], hb);
+                within[k] = atomicAdd(&s_dcnt[dg[k]], 1u);  // slot inside the bucket (any order)
+            }
+        }
+        __syncthreads();
+        {  // exclusive scan of the 4096 counts: 4 per thread; note the largest bucket
+            uint32_t v[4], sum = 0, mx = 0;
+            for (uint32_t x = 0; x < 4; ++x) {
+                v[x] = s_dcnt[tid * 4 + x];
+                sum += v[x];
+                mx = max(mx, v[x]);
+            }
+            if (mx > W_MAXBKT) atomicMax(&s_maxb, mx);
+            uint32_t tot;
+            uint32_t run = block_scan_excl(sum, s_ws, &tot);
+            for (uint32_t x = 0; x < 4; ++x) {
+                s_doff[tid * 4 + x] = (uint16_t)run;
+                run += v[x];
+            }
+        }
+        __syncthreads();
+        uint16_t *src = s_ia;
+        if (s_maxb == 0) {
+            // ---- bucket order by comparisons: rank = keys of the same bucket that are smaller
+            for (uint32_t k = 0; k < NR; ++k)
+                if (dg[k] != 0xFFFFFFFFu) s_ib[s_doff[dg[k]] + within[k]] = (uint16_t)sl[k];
+            __syncthreads();
+            for (uint32_t k = 0; k < NR; ++k) {
+                if (dg[k] == 0xFFFFFFFFu) continue;
+                const uint32_t bs = s_doff[dg[k]], bn = s_dcnt[dg[k]];
+                const uint64_t a0 = s_k[2 * sl[k]], a1 = s_k[2 * sl[k] + 1];
+                uint32_t rank = 0;
+                for (uint32_t q = 0; q < bn; ++q) {
+                    const uint32_t o = s_ib[bs + q];
+                    rank += key_lt(s_k[2 * o], s_k[2 * o + 1], a0, a1) ? 1u : 0u;
+                }
+                s_ia[bs + rank] = (uint16_t)sl[k];
+            }
+            __syncthreads();
+        } else {
+            // ---- LSD radix sort of the slot list by the varying key bytes (stable, per-wave ranks)
+            const int qlo = (int)(hb >> 3);
+            const int qhi = o1 ? 15 - (int)(__builtin_ctzll(o1) >> 3) : 7 - (int)(__builtin_ctzll(o0) >> 3);
+            uint16_t *dst = s_ib;
+            uint16_t *s_wc = s_x;
+            for (int q = qhi; q >= qlo; --q) {
+                for (uint32_t i = tid; i < NR * W_NW * 256; i += W_WG) s_wc[i] = 0;
+                __syncthreads();
+                uint32_t rk[3];
+                for (uint32_t k = 0; k < NR; ++k) {
+                    const uint32_t p = k * W_WG + tid;
+                    const bool valid = p < D;
+                    uint32_t d = 0;
+                    if (valid) {
+                        const uint32_t s2 = src[p];
+                        d = key_byte(s_k[2 * s2], s_k[2 * s2 + 1], (uint32_t)q);
+                    }
+                    uint64_t peers = __ballot(valid);
+                    for (int bt = 0; bt < 8; ++bt) {
+                        const uint64_t mb = __ballot(valid && ((d >> bt) & 1u));
+                        peers &= ((d >> bt) & 1u) ? mb : ~mb;
+                    }
+                    const uint32_t rank = (uint32_t)__popcll(peers & lt);
+                    if (valid && rank == 0) s_wc[(d * NR + k) * W_NW + wv] = (uint16_t)__popcll(peers);
+                    dg[k] = d;
+                    rk[k] = valid ? rank : 0xFFFFFFFFu;
+                }
+                __syncthreads();
+                {  // exclusive scan over the cells in (digit, round, wave) order: stable positions
+                    const uint32_t C = 256u * NR * W_NW, per = C / W_WG;   // 4, 8 or 12 cells per thread
+                    uint32_t v[12];
+                    uint32_t sum = 0;
+                    for (uint32_t x = 0; x < per; ++x) {
+                        v[x] = s_wc[tid * per + x];
+                        sum += v[x];
+                    }
+                    uint32_t tot;
+                    uint32_t run = block_scan_excl(sum, s_ws, &tot);
+                    for (uint32_t x = 0; x < per; ++x) {
+                        s_wc[tid * per + x] = (uint16_t)run;
+                        run += v[x];
+                    }
+                }
+                __syncthreads();
+                for (uint32_t k = 0; k < NR; ++k) {
+                    const uint32_t p = k * W_WG + tid;
+                    if (rk[k] != 0xFFFFFFFFu) dst[s_wc[(dg[k] * NR + k) * W_NW + wv] + rk[k]] = src[p];
+                }
+                __syncthreads();
+                uint16_t *tmp = src;
+                src = dst;
+                dst = tmp;
+            }
+        }
+        // ---- write the sorted distinct keys + the leaf's line bytes
+        GASW uint64_t *ko = gw(L.kout) + 2 * out0;
+        uint64_t bytes = 0;
+        for (uint32_t p = tid; p < D; p += W_WG) {
+            const uint32_t s2 = src[p];
+            const uint64_t a = s_k[2 * s2], c = s_k[2 * s2 + 1], n = s_c[s2];
+            typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+            *reinterpret_cast<GASW v2 *>(ko + 2 * p) = v2{a, c};
+            gw(L.ocnt)[out0 + p] = n;
+            const uint32_t ll = line_len(a, c, n);
+            bytes += ll;
+            if (p == D - 1) L.leaf_last[lid] = ll;
+        }
+        for (int o = 32; o > 0; o >>= 1) bytes += __shfl_xor(bytes, o);
+        __syncthreads();
+        if (tid == 0) s_or0 = 0;
+        __syncthreads();
+        if (lane == 0) atomicAdd((unsigned long long *)&s_or0, (unsigned long long)bytes);
+        __syncthreads();
+        if (tid == 0) {
+            L.leaf_out[lid] = out0;
+            L.leaf_nd[lid] = D;
+            L.leaf_bytes[lid] = s_or0;
+            if (D == 0) L.leaf_last[lid] = 0;
+            atomicAdd(L.nkeys, (unsigned long long)D);
+        }
+        __syncthreads();
+    }
+}
+
+// last-group drop (worker.rs:169-184): the last key of the last non-empty leaf of partition r
+__global__ void k_wdrop(const uint32_t *nleaf, uint32_t B1r, uint32_t R, const uint32_t *leaf_nd,
+                        uint64_t *leaf_bytes, const uint32_t *leaf_last, uint32_t *leaf_drop) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    for (int q = (int)B1r - 1; q >= 0; --q) {
+        const uint32_t b = r * B1r + (uint32_t)q;
+        for (int j = (int)nleaf[b] - 1; j >= 0; --j) {
+            const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + (uint32_t)j;
+            if (leaf_nd[lid]) {
+                leaf_bytes[lid] -= leaf_last[lid];
+                leaf_drop[lid] = 1;
+                return;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- lines
+// One workgroup per L1 bucket: for each leaf, 1024 lines at a time are laid out in LDS and stored
+// to the output as aligned dwords (byte stores only at the two ends).
+constexpr uint32_t W_STAGE = 40 * 1024;   // >= 1024 lines of <= 16 + 1 + 20 + 1 bytes
+
+__global__ __launch_bounds__(W_WG, 1) void k_wwrite(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *nleaf,
+                                                    const uint64_t *leaf_out, const uint32_t *leaf_nd,
+                                                    const uint32_t *leaf_drop, const uint64_t *leaf_off,
+                                                    uint8_t *out) {
+    __shared__ uint32_t s_buf[W_STAGE / 4];
+    __shared__ uint32_t s_ws[W_NW];
+    uint8_t *sb = reinterpret_cast<uint8_t *>(s_buf);
+    const uint32_t tid = threadIdx.x, b = blockIdx.x;
+    const uint32_t nl = nleaf[b];
+    for (uint32_t j = 0; j < nl; ++j) {
+        const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + j;
+        const uint32_t D = leaf_nd[lid] - (leaf_drop[lid] ? 1u : 0u);
+        if ((int)D <= 0) continue;
+        const uint64_t o0 = leaf_out[lid];
+        uint64_t dst = leaf_off[lid];
+        for (uint32_t p0 = 0; p0 < D; p0 += W_WG) {
+            const uint32_t p = p0 + tid;
+            uint64_t a = 0, c = 0, n = 0;
+            uint32_t len = 0, nd = 0, ll = 0;
+            if (p < D) {
+                a = keys[2 * (o0 + p)];
+                c = keys[2 * (o0 + p) + 1];
+                n = ocnt[o0 + p];
+                len = mrg_short_len(a, c);
+                nd = mrg_ndigits(n);
+                ll = len + 2u + nd;
+            }
+            uint32_t tot;
+            const uint32_t at = block_scan_excl(ll, s_ws, &tot);
+            // the chunk's bytes start at dst; stage them at LDS offset (dst & 3) so dwords align
+            const uint32_t sh = (uint32_t)(dst & 3u);
+            if (p < D) {
+                uint8_t *o = sb + sh + at;
+                for (uint32_t x = 0; x < len; ++x) o[x] = (uint8_t)mrg_key_byte(a, c, x);
+                o[len] = ' ';
+                uint64_t v = n;
+                for (uint32_t x = nd; x > 0; --x) {
+                    o[len + x] = (uint8_t)('0' + v % 10u);
+                    v /= 10u;
+                }
+                o[len + 1 + nd] = '\n';
+            }
+            __syncthreads();
+            // copy [sh, sh + tot) of the stage to out[dst ..): dwords where both ends are inside
+            const uint64_t end = dst + tot;
+            const uint64_t a4 = (dst + 3u) & ~3ull, e4 = end & ~3ull;
+            for (uint64_t x = dst + tid; x < min(a4, end); x += W_WG) out[x] = sb[sh + (x - dst)];
+            for (uint64_t w = a4 / 4 + tid; w < e4 / 4; w += W_WG)
+                reinterpret_cast<uint32_t *>(out)[w] = s_buf[(sh + (w * 4 - dst)) / 4];
+            for (uint64_t x = max(e4, a4) + tid; x < end; x += W_WG) out[x] = sb[sh + (x - dst)];
+            dst = end;
+            __syncthreads();
+        }
+    }
+}
+
+// part_off[r] = byte offset of partition r's first leaf; part_off[R] = total
+__global__ void k_wpart_off(const uint64_t *leaf_off, uint32_t B1r, uint32_t R, uint64_t total, uint64_t *part_off) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < R) part_off[r] = leaf_off[(uint64_t)r * B1r * MRG_WIDE_MAXB2];
+    else if (r == R) part_off[r] = total;
+}
+
+// dense KeySet (for consumers other than the line writer): leaf l's keys go to dense_off[l] ..
+__global__ __launch_bounds__(256) void k_wdense(const uint64_t *keys, const uint64_t *ocnt, const uint64_t *leaf_out,
+                                                const uint32_t *leaf_nd, const uint32_t *dense_off, uint32_t B1r,
+                                                KeySet ks) {
+    const uint64_t lid = blockIdx.x;
+    const uint32_t D = leaf_nd[lid];
+    const uint64_t o0 = leaf_out[lid], d0 = dense_off[lid];
+    const uint32_t part = (uint32_t)(lid / MRG_WIDE_MAXB2) / B1r;
+    for (uint32_t p = threadIdx.x; p < D; p += blockDim.x) {
+        const uint64_t a = keys[2 * (o0 + p)], c = keys[2 * (o0 + p) + 1];
+        ks.k0[d0 + p] = a;
+        ks.k1[d0 + p] = c;
+        ks.cnt[d0 + p] = ocnt[o0 + p];
+        ks.len[d0 + p] = mrg_short_len(a, c);
+        ks.part[d0 + p] = part;
+        ks.doc[d0 + p] = MRG_EMPTY_DOC;
+        ks.hoff[d0 + p] = MRG_NO_HEAP;
+    }
+}
+
+// ---------------------------------------------------------------- overflowed leaves: global sort
+// records of the listed leaves -> SortRec{key, part = list position, idx = count slot}, counts apart
+__global__ void k_wfb_count(const uint32_t *list, uint32_t nlist, const uint64_t *leaf_lo, const uint32_t *nleaf,
+                            const uint64_t *bstart, const uint64_t *wrange, uint64_t *cnt) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nlist) return;
+    const uint64_t lid = list[k];
+    const uint32_t b = (uint32_t)(lid / MRG_WIDE_MAXB2), j = (uint32_t)(lid % MRG_WIDE_MAXB2);
+    const uint64_t mlo = leaf_lo[lid], mhi = j + 1 < nleaf[b] ? leaf_lo[lid + 1] : bstart[b + 1];
+    cnt[k] = (mhi - mlo) + (wrange[2 * k + 1] - wrange[2 * k]);
+}
+__global__ void k_wfb_gather(const uint32_t *list, const uint64_t *off, const uint64_t *leaf_lo, const uint32_t *nleaf,
+                             const uint64_t *bstart, const uint64_t *wrange, const uint64_t *kin, const uint64_t *wk0,
+                             const uint64_t *wk1, const uint64_t *wcnt, SortRec *recs, uint64_t *rcnt) {
+    const uint32_t k = blockIdx.x;
+    const uint64_t lid = list[k];
+    const uint32_t b = (uint32_t)(lid / MRG_WIDE_MAXB2), j = (uint32_t)(lid % MRG_WIDE_MAXB2);
+    const uint64_t mlo = leaf_lo[lid], mhi = j + 1 < nleaf[b] ? leaf_lo[lid + 1] : bstart[b + 1];
+    const uint64_t wlo = wrange[2 * k], whi = wrange[2 * k + 1];
+    const uint64_t nm = mhi - mlo, n = nm + (whi - wlo), o = off[k];
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        SortRec r;
+        uint64_t c;
+        if (i < nm) {
+            r.k0 = kin[2 * (mlo + i)];
+            r.k1 = kin[2 * (mlo + i) + 1];
+            c = 1;
+        } else {
+            r.k0 = wk0[wlo + i - nm];
+            r.k1 = wk1[wlo + i - nm];
+            c = wcnt[wlo + i - nm];
+        }
+        r.part = k;
+        r.doc = 0;
+        r.idx = (uint32_t)(o + i);
+        r.pad = 0;
+        recs[o + i] = r;
+        rcnt[o + i] = c;
+    }
+}
+// the leaf weighted ranges of the listed leaves (computed by k_wranges)
+__global__ void k_wfb_wrange(LeafArgs L, const uint32_t *list, uint32_t nlist, uint64_t *wrange) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nlist) return;
+    const uint64_t lid = list[k];
+    wrange[2 * k] = L.wr[2 * lid];
+    wrange[2 * k + 1] = L.wr[2 * lid + 1];
+}
+// sorted records -> run heads (new key or new leaf)
+__global__ void k_wfb_heads(const SortRec *r, uint64_t n, uint64_t *head) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    head[i] = (i == 0 || r[i].part != r[i - 1].part || r[i].k0 != r[i - 1].k0 || r[i].k1 != r[i - 1].k1) ? 1u : 0u;
+}
+// run heads write their key + summed count at the leaf's next output slot; E = scan of heads,
+// lfirst[k] = run index of list leaf k's first run
+__global__ void k_wfb_emit(const SortRec *r, uint64_t n, const uint64_t *head, const uint64_t *E, const uint64_t *rcnt,
+                           const uint32_t *list, const uint64_t *lfirst, const uint64_t *leaf_out, uint64_t *keys,
+                           uint64_t *ocnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !head[i]) return;
+    uint64_t c = 0, e = i;
+    do {
+        c += rcnt[r[e].idx];
+        ++e;
+    } while (e < n && !head[e]);
+    const uint32_t k = r[i].part;
+    const uint64_t slot = leaf_out[list[k]] + (E[i] - lfirst[k]);
+    keys[2 * slot] = r[i].k0;
+    keys[2 * slot + 1] = r[i].k1;
+    ocnt[slot] = c;
+}
+__global__ void k_wfb_lfirst(const SortRec *r, uint64_t n, const uint64_t *head, const uint64_t *E, uint64_t *lfirst) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (i == 0 || r[i].part != r[i - 1].part) lfirst[r[i].part] = E[i];
+}
+// stats of the finished leaves: distinct keys, bytes, last line
+__global__ void k_wfb_stats(const uint32_t *list, uint32_t nlist, const uint64_t *lfirst, uint64_t runs,
+                            const uint64_t *keys, const uint64_t *ocnt, const uint64_t *leaf_out, uint32_t *leaf_nd,
+                            uint64_t *leaf_bytes, uint32_t *leaf_last, unsigned long long *nkeys) {
+    const uint32_t k = blockIdx.x;
+    const uint64_t lid = list[k];
+    const uint64_t D = (k + 1 < nlist ? lfirst[k + 1] : runs) - lfirst[k];
+    const uint64_t o0 = leaf_out[lid];
+    uint64_t bytes = 0;
+    for (uint64_t p = threadIdx.x; p < D; p += blockDim.x)
+        bytes += line_len(keys[2 * (o0 + p)], keys[2 * (o0 + p) + 1], ocnt[o0 + p]);
+    __shared__ unsigned long long s_b;
+    if (threadIdx.x == 0) s_b = 0;
+    __syncthreads();
+    atomicAdd(&s_b, (unsigned long long)bytes);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        leaf_nd[lid] = (uint32_t)D;
+        leaf_bytes[lid] = s_b;
+        leaf_last[lid] = D ? line_len(keys[2 * (o0 + D - 1)], keys[2 * (o0 + D - 1) + 1], ocnt[o0 + D - 1]) : 0u;
+        atomicAdd(nkeys, (unsigned long long)D);
+    }
+}
+
+// weighted keys sorted by (part, key): gather from the aggregated KeySet in sort order
+__global__ void k_wweights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *wk0, uint64_t *wk1, uint64_t *wcnt,
+                           uint32_t *wpart) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t e = r[i].idx;
+    wk0[i] = ks.k0[e];
+    wk1[i] = ks.k1[e];
+    wcnt[i] = ks.cnt[e];
+    wpart[i] = r[i].part;
+}
+
+inline dim3 gridw(uint64_t n, int b = 256) { return dim3((unsigned)((n + b - 1) / b)); }
+
+}  // namespace
+
+// ================================================================ host launchers (mrgpu.cpp)
+void mrg_wide_launch_counts(const BucketArgs &a, uint64_t *cnt_main, uint64_t *cnt_flush, hipStream_t s) {
+    const uint64_t nsm = (uint64_t)a.nreg * MRG_NBUCKET + MRG_NBUCKET;
+    hipLaunchKernelGGL(k_wmain_counts, gridw(nsm), dim3(256), 0, s, a, cnt_main);
+    hipLaunchKernelGGL(k_wflush_counts, gridw(a.nreg), dim3(256), 0, s, a, cnt_flush);
+}
+void mrg_wide_launch_flush_gather(const BucketArgs &a, const uint64_t *off, uint64_t *k0, uint64_t *k1, uint32_t *c,
+                                  hipStream_t s) {
+    hipLaunchKernelGGL(k_wflush_gather, dim3(a.nreg), dim3(256), 0, s, a, off, k0, k1, c);
+}
+void mrg_wide_launch_sample1(const BucketArgs &a, const uint64_t *off, uint64_t nseg, uint64_t n, uint32_t S,
+                             uint32_t R, SortRec *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_wsample1, gridw(S), dim3(256), 0, s, a, off, nseg, n, S, R, out);
+}
+void mrg_wide_launch_split1(const SortRec *smp, uint32_t S, uint32_t R, uint32_t B1r, uint64_t *spl, hipStream_t s) {
+    if (B1r > 1) hipLaunchKernelGGL(k_wsplit1, gridw((uint64_t)R * (B1r - 1)), dim3(256), 0, s, smp, S, R, B1r, spl);
+}
+size_t mrg_wide_l1_lds(uint32_t R, uint32_t B1r, uint32_t B1) {
+    return 16ull * R * (B1r - 1u) + 4ull * ((B1 + 1u) & ~1u) + 8ull * W_SEGLDS;
+}
+void mrg_wide_launch_l1(const BucketArgs &a, const uint64_t *off, uint64_t nseg, uint64_t n, const uint64_t *spl1,
+                        uint32_t R, uint32_t B1r, uint32_t *cnt, uint32_t ntiles, uint64_t *out, bool scatter,
+                        hipStream_t s) {
+    L1Args L{a, off, nseg, n, spl1, R, B1r, R * B1r, ntiles, cnt, out};
+    const size_t lds = mrg_wide_l1_lds(R, B1r, R * B1r);
+    if (scatter) hipLaunchKernelGGL(k_wl1<true>, dim3(ntiles), dim3(W_WG), lds, s, L);
+    else hipLaunchKernelGGL(k_wl1<false>, dim3(ntiles), dim3(W_WG), lds, s, L);
+}
+void mrg_wide_launch_bstart(const uint32_t *cnt, uint32_t B1, uint32_t ntiles, uint64_t n, uint64_t *bstart,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_wbstart, gridw(B1 + 1), dim3(256), 0, s, cnt, B1, ntiles, n, bstart);
+}
+void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstart, const uint64_t *spl1, uint32_t B1,
+                        uint32_t B1r, uint32_t target, uint32_t *nleaf, uint64_t *leaf_lo, uint64_t *leaf_lb,
+                        hipStream_t s) {
+    L2Args L{in, out, bstart, spl1, B1r, target, nleaf, leaf_lo, leaf_lb};
+    hipLaunchKernelGGL(k_wl2, dim3(B1), dim3(W_WG), 0, s, L);
+}
+void mrg_wide_launch_weights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *wk0, uint64_t *wk1, uint64_t *wcnt,
+                             uint32_t *wpart, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_wweights, gridw(n), dim3(256), 0, s, r, n, ks, wk0, wk1, wcnt, wpart);
+}
+void mrg_wide_launch_leaf(const WideLeafArgs &w, uint32_t B1, hipStream_t s) {
+    LeafArgs L{w.kin, w.kout, w.bstart, w.nleaf, w.leaf_lo, w.leaf_lb, w.B1r, w.R, w.wk0, w.wk1, w.wcnt, w.wpart, w.nw,
+               w.maxd ? w.maxd : W_MAXD, w.ocnt, w.leaf_out, w.leaf_nd, w.leaf_bytes, w.leaf_last, w.ovf_list,
+               w.ovf_n, w.nkeys, w.wr};
+    hipLaunchKernelGGL(k_wranges, gridw((uint64_t)B1 * MRG_WIDE_MAXB2), dim3(256), 0, s, L, B1);
+    hipLaunchKernelGGL(k_wleaf, dim3(B1), dim3(W_WG), 0, s, L);
+}
+void mrg_wide_launch_fallback(const WideLeafArgs &w, const uint32_t *list, uint32_t nlist, DevPool &pool,
+                              hipStream_t s) {
+    LeafArgs L{w.kin, w.kout, w.bstart, w.nleaf, w.leaf_lo, w.leaf_lb, w.B1r, w.R, w.wk0, w.wk1, w.wcnt, w.wpart, w.nw,
+               w.maxd ? w.maxd : W_MAXD, w.ocnt, w.leaf_out, w.leaf_nd, w.leaf_bytes, w.leaf_last, w.ovf_list,
+               w.ovf_n, w.nkeys, w.wr};
+    uint64_t *wrange = (uint64_t *)pool.get(16ull * nlist);
+    uint64_t *cnt = (uint64_t *)pool.get(8ull * (nlist + 1)), *off = (uint64_t *)pool.get(8ull * (nlist + 1));
+    uint64_t *scantmp = (uint64_t *)pool.get(8ull * mrg_scan_tmp_elems(nlist + 1));
+    hipLaunchKernelGGL(k_wfb_wrange, gridw(nlist), dim3(256), 0, s, L, list, nlist, wrange);
+    hipMemsetAsync(cnt + nlist, 0, 8, s);
+    hipLaunchKernelGGL(k_wfb_count, gridw(nlist), dim3(256), 0, s, list, nlist, w.leaf_lo, w.nleaf, w.bstart, wrange,
+                       cnt);
+    mrg_scan_u64(cnt, off, nlist + 1, scantmp, s);
+    uint64_t n = 0;
+    hipMemcpyAsync(&n, off + nlist, 8, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    SortRec *a = (SortRec *)pool.get(sizeof(SortRec) * (n + 1)), *b = (SortRec *)pool.get(sizeof(SortRec) * (n + 1));
+    uint64_t *rcnt = (uint64_t *)pool.get(8ull * (n + 1));
+    hipLaunchKernelGGL(k_wfb_gather, dim3(nlist), dim3(256), 0, s, list, off, w.leaf_lo, w.nleaf, w.bstart, wrange,
+                       w.kin, w.wk0, w.wk1, w.wcnt, a, rcnt);
+    SortPlan plan{};
+    plan.use_part = nlist > 1;
+    uint32_t pb = 0;
+    for (uint32_t v = nlist - 1; v; v >>= 8) ++pb;
+    plan.part_bytes = pb;
+    plan.use_k0 = plan.use_k1 = true;
+    void *stmp = pool.get(mrg_sort_tmp_bytes(n));
+    int passes = 0;
+    SortRec *srt = mrg_radix_sort(a, b, n, plan, stmp, s, &passes);
+    uint64_t *head = (uint64_t *)pool.get(8ull * (n + 1)), *E = (uint64_t *)pool.get(8ull * (n + 1));
+    uint64_t *lfirst = (uint64_t *)pool.get(8ull * (nlist + 1));
+    uint64_t *scantmp2 = (uint64_t *)pool.get(8ull * mrg_scan_tmp_elems(n + 1));
+    hipLaunchKernelGGL(k_wfb_heads, gridw(n), dim3(256), 0, s, srt, n, head);
+    mrg_scan_u64(head, E, n, scantmp2, s);
+    hipLaunchKernelGGL(k_wfb_lfirst, gridw(n), dim3(256), 0, s, srt, n, head, E, lfirst);
+    uint64_t tail[2] = {0, 0};
+    hipMemcpyAsync(&tail[0], E + (n - 1), 8, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(&tail[1], head + (n - 1), 8, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    const uint64_t runs = tail[0] + tail[1];
+    hipLaunchKernelGGL(k_wfb_emit, gridw(n), dim3(256), 0, s, srt, n, head, E, rcnt, list, lfirst, w.leaf_out, w.kout,
+                       w.ocnt);
+    hipLaunchKernelGGL(k_wfb_stats, dim3(nlist), dim3(256), 0, s, list, nlist, lfirst, runs, w.kout, w.ocnt, w.leaf_out,
+                       w.leaf_nd, w.leaf_bytes, w.leaf_last, w.nkeys);
+    hipStreamSynchronize(s);
+    pool.put(wrange); pool.put(cnt); pool.put(off); pool.put(scantmp); pool.put(a); pool.put(b); pool.put(rcnt);
+    pool.put(stmp); pool.put(head); pool.put(E); pool.put(lfirst); pool.put(scantmp2);
+}
+void mrg_wide_launch_drop(const uint32_t *nleaf, uint32_t B1r, uint32_t R, const uint32_t *leaf_nd, uint64_t *leaf_bytes,
+                          const uint32_t *leaf_last, uint32_t *leaf_drop, hipStream_t s) {
+    hipLaunchKernelGGL(k_wdrop, gridw(R), dim3(256), 0, s, nleaf, B1r, R, leaf_nd, leaf_bytes, leaf_last, leaf_drop);
+}
+void mrg_wide_launch_write(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *nleaf, const uint64_t *leaf_out,
+                           const uint32_t *leaf_nd, const uint32_t *leaf_drop, const uint64_t *leaf_off, uint32_t B1,
+                           uint8_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_wwrite, dim3(B1), dim3(W_WG), 0, s, keys, ocnt, nleaf, leaf_out, leaf_nd, leaf_drop, leaf_off,
+                       out);
+}
+void mrg_wide_launch_part_off(const uint64_t *leaf_off, uint32_t B1r, uint32_t R, uint64_t total, uint64_t *part_off,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(k_wpart_off, gridw(R + 1), dim3(256), 0, s, leaf_off, B1r, R, total, part_off);
+}
+void mrg_wide_launch_dense(const uint64_t *keys, const uint64_t *ocnt, const uint64_t *leaf_out, const uint32_t *leaf_nd,
+                           const uint32_t *dense_off, uint32_t B1, uint32_t B1r, KeySet ks, hipStream_t s) {
+    hipLaunchKernelGGL(k_wdense, dim3(B1 * MRG_WIDE_MAXB2), dim3(256), 0, s, keys, ocnt, leaf_out, leaf_nd, dense_off,
+                       B1r, ks);
+}

@@ -184,6 +184,8 @@ void mrg_launch_iota_u32(uint32_t *p, uint64_t n, hipStream_t s);
 uint64_t mrg_scan_tmp_elems(uint64_t n);
 // exclusive scan of u64 values (in == out allowed); tmp holds mrg_scan_tmp_elems(n) u64
 void mrg_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t s);
+// the same for u32 values (tmp: mrg_scan_tmp_elems(n) u32)
+void mrg_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *tmp, hipStream_t s);
 struct SortRec {  // 32 bytes
     uint64_t k0, k1;
     uint32_t part, doc;
@@ -243,6 +245,60 @@ void mrg_launch_text_lines(const uint8_t *in, const uint64_t *fo, const uint64_t
                            const uint64_t *base, uint64_t *cnt, XRec *out, unsigned long long *err,
                            unsigned long long *nempty, hipStream_t s);
 void mrg_launch_add_first(const SortRec *r, KeySet ks, uint64_t v, hipStream_t s);
+
+// ---- k_wide.hip: high-cardinality aggregation by a two-level sample sort
+#define MRG_WIDE_T1 65536u       // records per L1 tile
+#define MRG_WIDE_MAXB2 1024u     // leaves per L1 bucket; leaf id = bucket * MRG_WIDE_MAXB2 + j
+struct WideLeafArgs {
+    const uint64_t *kin;         // records in leaf order (2 words each)
+    uint64_t *kout;              // distinct keys (2 words each) at leaf_out[leaf] + i
+    const uint64_t *bstart;      // [B1 + 1]
+    const uint32_t *nleaf;       // [B1]
+    const uint64_t *leaf_lo, *leaf_lb;
+    uint32_t B1r, R;
+    const uint64_t *wk0, *wk1, *wcnt;  // weighted keys (flushed map tables), sorted by (part, key)
+    const uint32_t *wpart;
+    uint64_t nw;
+    uint32_t maxd;               // 0 = default capacity
+    uint64_t *ocnt;
+    uint64_t *leaf_out;
+    uint32_t *leaf_nd;
+    uint64_t *leaf_bytes;
+    uint32_t *leaf_last;
+    uint32_t *ovf_list;
+    unsigned long long *ovf_n;
+    unsigned long long *nkeys;   // += distinct keys of every finished leaf
+    uint64_t *wr;                // [B1 * MRG_WIDE_MAXB2][2] scratch: weighted-key range of each leaf
+};
+void mrg_wide_launch_counts(const BucketArgs &a, uint64_t *cnt_main, uint64_t *cnt_flush, hipStream_t s);
+void mrg_wide_launch_flush_gather(const BucketArgs &a, const uint64_t *off, uint64_t *k0, uint64_t *k1, uint32_t *c,
+                                  hipStream_t s);
+void mrg_wide_launch_sample1(const BucketArgs &a, const uint64_t *off, uint64_t nseg, uint64_t n, uint32_t S,
+                             uint32_t R, SortRec *out, hipStream_t s);
+void mrg_wide_launch_split1(const SortRec *smp, uint32_t S, uint32_t R, uint32_t B1r, uint64_t *spl, hipStream_t s);
+size_t mrg_wide_l1_lds(uint32_t R, uint32_t B1r, uint32_t B1);
+void mrg_wide_launch_l1(const BucketArgs &a, const uint64_t *off, uint64_t nseg, uint64_t n, const uint64_t *spl1,
+                        uint32_t R, uint32_t B1r, uint32_t *cnt, uint32_t ntiles, uint64_t *out, bool scatter,
+                        hipStream_t s);
+void mrg_wide_launch_bstart(const uint32_t *cnt, uint32_t B1, uint32_t ntiles, uint64_t n, uint64_t *bstart,
+                            hipStream_t s);
+void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstart, const uint64_t *spl1, uint32_t B1,
+                        uint32_t B1r, uint32_t target, uint32_t *nleaf, uint64_t *leaf_lo, uint64_t *leaf_lb,
+                        hipStream_t s);
+void mrg_wide_launch_weights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *wk0, uint64_t *wk1, uint64_t *wcnt,
+                             uint32_t *wpart, hipStream_t s);
+void mrg_wide_launch_leaf(const WideLeafArgs &w, uint32_t B1, hipStream_t s);
+void mrg_wide_launch_fallback(const WideLeafArgs &w, const uint32_t *list, uint32_t nlist, DevPool &pool,
+                              hipStream_t s);
+void mrg_wide_launch_drop(const uint32_t *nleaf, uint32_t B1r, uint32_t R, const uint32_t *leaf_nd, uint64_t *leaf_bytes,
+                          const uint32_t *leaf_last, uint32_t *leaf_drop, hipStream_t s);
+void mrg_wide_launch_write(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *nleaf, const uint64_t *leaf_out,
+                           const uint32_t *leaf_nd, const uint32_t *leaf_drop, const uint64_t *leaf_off, uint32_t B1,
+                           uint8_t *out, hipStream_t s);
+void mrg_wide_launch_part_off(const uint64_t *leaf_off, uint32_t B1r, uint32_t R, uint64_t total, uint64_t *part_off,
+                              hipStream_t s);
+void mrg_wide_launch_dense(const uint64_t *keys, const uint64_t *ocnt, const uint64_t *leaf_out, const uint32_t *leaf_nd,
+                           const uint32_t *dense_off, uint32_t B1, uint32_t B1r, KeySet ks, hipStream_t s);
 
 // ---- k_gen.hip
 int mrg_gen_zipf_impl(uint8_t *dst, uint64_t n, uint64_t seed, uint64_t file_index, uint32_t vocab, double s,

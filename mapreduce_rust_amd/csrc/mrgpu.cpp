@@ -151,6 +151,21 @@ struct KeysBuf {
     bool sorted = false;  // keys already in (partition, key) order (wide aggregation, no long keys)
 };
 
+// Result of the wide (sample-sort) aggregation, k_wide.hip: distinct keys in output order, per leaf,
+// with gaps between leaves; formatted directly, or made a dense KeySet for the other consumers.
+struct WideRes {
+    bool ready = false;
+    uint32_t B1 = 0, B1r = 0;
+    uint64_t *kout = nullptr, *ocnt = nullptr;
+    uint32_t *nleaf = nullptr, *leaf_nd = nullptr, *leaf_last = nullptr;
+    uint64_t *leaf_out = nullptr, *leaf_bytes = nullptr;
+    uint64_t distinct = 0;
+    void release(Pool &p) {
+        p.put(kout); p.put(ocnt); p.put(nleaf); p.put(leaf_nd); p.put(leaf_last); p.put(leaf_out); p.put(leaf_bytes);
+        *this = WideRes{};
+    }
+};
+
 }  // namespace
 
 struct mrg_ctx {
@@ -175,6 +190,7 @@ struct mrg_ctx {
     std::vector<uint32_t> doc_ids;
     std::vector<std::string> names;
     KeysBuf keys;
+    WideRes wide;
     bool mapped = false;
     uint32_t n_owners = 0;
     std::vector<uint64_t> exp_rec, exp_heap;
@@ -419,7 +435,7 @@ uint32_t bytes_for(uint64_t maxval) {
 // Wide (sort-based) aggregation for high-cardinality inputs (k_keys.hip k_wide_*): every map
 // record is gathered with its partition, sorted by (partition, key) and summed per key; the key set
 // comes out in output order.
-void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap, LongItems li) {
+void wide_aggregate_radix(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap, LongItems li) {
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     BucketArgs B{};
@@ -476,6 +492,187 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     finish_keys(c);
 }
 
+// The wide result as a dense KeySet (sorted by partition and key) for the consumers other than the
+// line writer (export, final.txt, long keys appended); `extra` more slots are reserved.
+void wide_densify(mrg_ctx *c, uint64_t extra) {
+    WideRes &w = c->wide;
+    if (!w.ready) return;
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const uint64_t nl = (uint64_t)w.B1 * MRG_WIDE_MAXB2;
+    uint32_t *doff = pget<uint32_t>(p, nl + 1);
+    uint32_t *tmp = pget<uint32_t>(p, mrg_scan_tmp_elems(nl + 1));
+    mrg_scan_u32(w.leaf_nd, doff, nl, tmp, s);
+    keys_reserve(c, w.distinct + extra + 1);
+    mrg_wide_launch_dense(w.kout, w.ocnt, w.leaf_out, w.leaf_nd, doff, w.B1, w.B1r, c->keys.ks, s);
+    HIPCHK(hipMemcpyAsync(&c->d_cnt[CNT_KEYS], &w.distinct, 8, hipMemcpyHostToDevice, s));
+    sync(c);
+    p.put(doff);
+    p.put(tmp);
+    c->keys.n = w.distinct;
+    c->keys.sorted = true;
+    w.release(p);
+}
+
+// Wide aggregation by the two-level sample sort (k_wide.hip): the map's count-1 records go through
+// L1 (partition + global quantile splitters) and L2 (per-bucket splitters) into leaves; the flushed
+// map-table entries (weighted) are aggregated apart, sorted, and merged into their leaves.
+void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap, LongItems li) {
+    const uint32_t R = c->R;
+    if (R > 4096 || getenv("MRG_WIDE_RADIX")) {  // the L1 histogram holds R x B1r buckets in LDS
+        wide_aggregate_radix(c, A, nreg, regcap, li);
+        return;
+    }
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    BucketArgs B{};
+    B.pool = A.pool; B.rbase = A.rbase; B.bcap = A.bcap; B.bcount = A.bcount;
+    B.movf = A.ovf; B.monext = A.onext; B.mocap = A.ocap;
+    B.fk0 = A.fk0; B.fk1 = A.fk1; B.fcnt = A.fcnt; B.fdoc = A.fdoc; B.foff = A.foff;
+    B.nreg = nreg; B.regcap = regcap;
+    // ---- segment sizes: main (count 1) and flushed tables (weighted)
+    const uint64_t nsm = (uint64_t)nreg * MRG_NBUCKET + MRG_NBUCKET;
+    uint64_t *cm = pget<uint64_t>(p, nsm + 1), *om = pget<uint64_t>(p, nsm + 1);
+    uint64_t *cf = pget<uint64_t>(p, nreg + 1), *of = pget<uint64_t>(p, nreg + 1);
+    uint64_t *st1 = pget<uint64_t>(p, mrg_scan_tmp_elems(nsm + 1));
+    HIPCHK(hipMemsetAsync(cm + nsm, 0, 8, s));
+    HIPCHK(hipMemsetAsync(cf + nreg, 0, 8, s));
+    mrg_wide_launch_counts(B, cm, cf, s);
+    mrg_scan_u64(cm, om, nsm + 1, st1, s);
+    mrg_scan_u64(cf, of, nreg + 1, st1, s);
+    uint64_t nn[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&nn[0], om + nsm, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&nn[1], of + nreg, 8, hipMemcpyDeviceToHost, s));
+    sync(c);
+    const uint64_t n = nn[0], nf = nn[1];
+    if (n >= 0xFFFFFFF0ull) raise(MRG_ENOMEM, "wide aggregation: %llu records exceed one GPU's 32-bit record index",
+                                  (unsigned long long)n);
+    // ---- weighted keys: HBM-table aggregation of the flushed entries, sorted by (partition, key)
+    uint64_t nw = 0;
+    uint64_t *wk0 = pget<uint64_t>(p, nf + 1), *wk1 = pget<uint64_t>(p, nf + 1), *wcnt = pget<uint64_t>(p, nf + 1);
+    uint32_t *wpart = pget<uint32_t>(p, nf + 1);
+    if (nf) {
+        uint64_t *fk0 = pget<uint64_t>(p, nf), *fk1 = pget<uint64_t>(p, nf);
+        uint32_t *fc = pget<uint32_t>(p, nf);
+        mrg_wide_launch_flush_gather(B, of, fk0, fk1, fc, s);
+        KeySet ks{};
+        ks.k0 = pget<uint64_t>(p, nf); ks.k1 = pget<uint64_t>(p, nf); ks.cnt = pget<uint64_t>(p, nf);
+        ks.hoff = pget<uint64_t>(p, nf); ks.doc = pget<uint32_t>(p, nf); ks.len = pget<uint32_t>(p, nf);
+        ks.part = pget<uint32_t>(p, nf);
+        TableArgs T{};
+        T.cap = pow2_at_least(2 * nf);
+        T.tk0 = pget<uint64_t>(p, T.cap); T.tk1 = pget<uint64_t>(p, T.cap); T.tcnt = pget<uint64_t>(p, T.cap);
+        T.hash_bits = hash_bits(c);
+        HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
+        mrg_launch_table_clear(T, false, s);
+        mrg_launch_table_insert(T, fk0, fk1, fc, nullptr, nf, false, s);
+        mrg_launch_table_compact(T, false, ks, &c->d_cnt[CNT_KEYS], s);
+        read_counters(c);
+        nw = c->h_cnt[CNT_KEYS];
+        mrg_launch_partition(ks, nullptr, nw, R, s);
+        SortRec *ra = pget<SortRec>(p, nw), *rb = pget<SortRec>(p, nw);
+        void *stmp = p.get(mrg_sort_tmp_bytes(nw));
+        mrg_launch_make_sortrec(ks, nw, nullptr, ra, s);
+        SortPlan plan{};
+        plan.use_part = R > 1;
+        plan.part_bytes = bytes_for(R - 1);
+        plan.use_k0 = plan.use_k1 = true;
+        int passes = 0;
+        SortRec *srt = mrg_radix_sort(ra, rb, nw, plan, stmp, s, &passes);
+        mrg_wide_launch_weights(srt, nw, ks, wk0, wk1, wcnt, wpart, s);
+        sync(c);
+        p.put(fk0); p.put(fk1); p.put(fc); p.put(ks.k0); p.put(ks.k1); p.put(ks.cnt); p.put(ks.hoff); p.put(ks.doc);
+        p.put(ks.len); p.put(ks.part); p.put(T.tk0); p.put(T.tk1); p.put(T.tcnt); p.put(ra); p.put(rb); p.put(stmp);
+    }
+    // ---- L1 buckets: R partitions x B1r quantile ranges of about 2^19 records
+    uint32_t B1r = (uint32_t)std::min<uint64_t>((n + ((uint64_t)R << 19) - 1) / ((uint64_t)R << 19), 64);
+    B1r = std::max<uint32_t>(1, std::min<uint32_t>(B1r, std::max<uint32_t>(1, 4096 / R)));
+    const uint32_t B1 = R * B1r;
+    uint64_t *spl1 = pget<uint64_t>(p, 2ull * R * B1r + 2);
+    if (B1r > 1 && n) {
+        const uint32_t S1 = (uint32_t)std::min<uint64_t>(64ull * B1, n);
+        SortRec *sa = pget<SortRec>(p, S1), *sb = pget<SortRec>(p, S1);
+        void *stmp = p.get(mrg_sort_tmp_bytes(S1));
+        mrg_wide_launch_sample1(B, om, nsm, n, S1, R, sa, s);
+        SortPlan plan{};
+        plan.use_part = R > 1;
+        plan.part_bytes = bytes_for(R - 1);
+        plan.use_k0 = plan.use_k1 = true;
+        int passes = 0;
+        SortRec *srt = mrg_radix_sort(sa, sb, S1, plan, stmp, s, &passes);
+        mrg_wide_launch_split1(srt, S1, R, B1r, spl1, s);
+        sync(c);
+        p.put(sa); p.put(sb); p.put(stmp);
+    }
+    const uint32_t ntiles = (uint32_t)std::max<uint64_t>(1, (n + MRG_WIDE_T1 - 1) / MRG_WIDE_T1);
+    uint32_t *cnt1 = pget<uint32_t>(p, (uint64_t)B1 * ntiles + 1);
+    uint32_t *st2 = pget<uint32_t>(p, mrg_scan_tmp_elems((uint64_t)B1 * ntiles + 1));
+    uint64_t *K1 = pget<uint64_t>(p, 2 * (n + nw) + 2);
+    uint64_t *bstart = pget<uint64_t>(p, B1 + 1);
+    if (n) {
+        mrg_wide_launch_l1(B, om, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, false, s);
+        mrg_scan_u32(cnt1, cnt1, (uint64_t)B1 * ntiles, st2, s);
+        mrg_wide_launch_l1(B, om, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, true, s);
+    } else {
+        HIPCHK(hipMemsetAsync(cnt1, 0, 4ull * B1 * ntiles, s));
+    }
+    mrg_wide_launch_bstart(cnt1, B1, ntiles, n, bstart, s);
+    p.put(cnt1); p.put(st2); p.put(cm); p.put(om); p.put(cf); p.put(of); p.put(st1);
+    // ---- L2: leaves inside every L1 bucket
+    const uint64_t NL = (uint64_t)B1 * MRG_WIDE_MAXB2;
+    uint64_t *K2 = pget<uint64_t>(p, 2 * n + 2);
+    uint32_t *nleaf = pget<uint32_t>(p, B1);
+    uint64_t *leaf_lo = pget<uint64_t>(p, NL + 1), *leaf_lb = pget<uint64_t>(p, 2 * NL + 2);
+    const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", 1024);
+    mrg_wide_launch_l2(K1, K2, bstart, spl1, B1, B1r, target, nleaf, leaf_lo, leaf_lb, s);
+    // ---- leaves: aggregate + sort + line bytes (K1 becomes the output key array)
+    WideRes &w = c->wide;
+    w.release(p);
+    w.B1 = B1;
+    w.B1r = B1r;
+    w.kout = K1;
+    w.ocnt = pget<uint64_t>(p, n + nw + 1);
+    w.nleaf = nleaf;
+    w.leaf_out = pget<uint64_t>(p, NL);
+    w.leaf_nd = pget<uint32_t>(p, NL + 1);
+    w.leaf_bytes = pget<uint64_t>(p, NL + 1);
+    w.leaf_last = pget<uint32_t>(p, NL);
+    HIPCHK(hipMemsetAsync(w.leaf_nd, 0, 4 * (NL + 1), s));
+    HIPCHK(hipMemsetAsync(w.leaf_bytes, 0, 8 * (NL + 1), s));
+    uint32_t *ovf_list = pget<uint32_t>(p, NL);
+    HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
+    HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
+    WideLeafArgs L{};
+    L.kin = K2; L.kout = K1; L.bstart = bstart; L.nleaf = nleaf; L.leaf_lo = leaf_lo; L.leaf_lb = leaf_lb;
+    L.B1r = B1r; L.R = R; L.wk0 = wk0; L.wk1 = wk1; L.wcnt = wcnt; L.wpart = wpart; L.nw = nw;
+    L.maxd = (uint32_t)env_u64("MRG_TEST_LEAF_CAP", 0);
+    L.ocnt = w.ocnt; L.leaf_out = w.leaf_out; L.leaf_nd = w.leaf_nd; L.leaf_bytes = w.leaf_bytes;
+    L.leaf_last = w.leaf_last; L.ovf_list = ovf_list; L.ovf_n = &c->d_cnt[CNT_OVF2]; L.nkeys = &c->d_cnt[CNT_KEYS];
+    L.wr = pget<uint64_t>(p, 2 * NL);
+    mrg_wide_launch_leaf(L, B1, s);
+    read_counters(c);
+    const uint64_t novf = c->h_cnt[CNT_OVF2];
+    if (novf) mrg_wide_launch_fallback(L, ovf_list, (uint32_t)novf, p, s);
+    read_counters(c);
+    w.distinct = c->h_cnt[CNT_KEYS];
+    w.ready = true;
+    if (getenv("MRG_DEBUG"))
+        fprintf(stderr, "[mrgpu] wide: %llu records, %llu weighted, B1 %u (x%u), %llu distinct, %llu leaves overflowed\n",
+                (unsigned long long)n, (unsigned long long)nw, B1, B1r, (unsigned long long)w.distinct,
+                (unsigned long long)novf);
+    p.put(K2); p.put(leaf_lo); p.put(leaf_lb); p.put(ovf_list); p.put(spl1); p.put(bstart); p.put(L.wr);
+    p.put(wk0); p.put(wk1); p.put(wcnt); p.put(wpart);
+    c->st.overflow_keys = novf;
+    c->keys.n = 0;
+    c->st.distinct_keys = w.distinct;
+    if (li.n) {  // long keys: the dense key set plus the long keys, sorted by the generic path
+        wide_densify(c, li.n);
+        long_aggregate(c, li);
+        finish_keys(c);
+        c->keys.sorted = false;
+    }
+}
+
 void need_job(mrg_ctx *c) {
     if (!c) raise(MRG_EINVAL, "null context");
     if (!c->job) raise(MRG_EINVAL, "no job: call mrg_job_begin first");
@@ -486,6 +683,7 @@ void job_begin(mrg_ctx *c, int app, uint32_t R, uint32_t flags) {
     if (R == 0) raise(MRG_EINVAL, "n_reduce must be > 0");
     sync(c);
     keys_release(c);
+    c->wide.release(c->pool);
     c->job = true;
     c->app = app;
     c->R = R;
@@ -758,9 +956,53 @@ FormatArgs format_args(mrg_ctx *c, const SortRec *recs, KeySet ks, uint32_t R, i
 
 int compat_drop_last(const mrg_ctx *c) { return (c->flags & MRG_FLAG_NO_COMPAT_DROP_LAST) ? 0 : 1; }
 
+// mr-{r}.txt of a wide result straight from its leaves (k_wide.hip): last-group drop on the last
+// non-empty leaf of every partition, a scan of the leaf byte totals, the line writer.
+void wide_reduce(mrg_ctx *c) {
+    WideRes &w = c->wide;
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const uint64_t NL = (uint64_t)w.B1 * MRG_WIDE_MAXB2;
+    ev_rec(c, 4);
+    uint32_t *drop = pget<uint32_t>(p, NL);
+    HIPCHK(hipMemsetAsync(drop, 0, 4 * NL, s));
+    uint64_t *bytes = pget<uint64_t>(p, NL + 1), *off = pget<uint64_t>(p, NL + 1);
+    uint64_t *tmp = pget<uint64_t>(p, mrg_scan_tmp_elems(NL + 1));
+    HIPCHK(hipMemcpyAsync(bytes, w.leaf_bytes, 8 * (NL + 1), hipMemcpyDeviceToDevice, s));
+    if (compat_drop_last(c)) mrg_wide_launch_drop(w.nleaf, w.B1r, c->R, w.leaf_nd, bytes, w.leaf_last, drop, s);
+    mrg_scan_u64(bytes, off, NL + 1, tmp, s);  // off[NL] = total (bytes[NL] == 0)
+    uint64_t total = 0;
+    HIPCHK(hipMemcpyAsync(&total, off + NL, 8, hipMemcpyDeviceToHost, s));
+    sync(c);
+    ev_rec(c, 5);
+    if (total + 16 > c->out_cap) {
+        if (c->d_out) p.put(c->d_out);
+        c->out_cap = total + 16;
+        c->d_out = pget<uint8_t>(p, c->out_cap);
+    }
+    mrg_wide_launch_write(w.kout, w.ocnt, w.nleaf, w.leaf_out, w.leaf_nd, drop, off, w.B1, c->d_out, s);
+    uint64_t *poff = pget<uint64_t>(p, c->R + 1);
+    mrg_wide_launch_part_off(off, w.B1r, c->R, total, poff, s);
+    c->part_off.assign(c->R + 1, 0);
+    HIPCHK(hipMemcpyAsync(c->part_off.data(), poff, 8ull * (c->R + 1), hipMemcpyDeviceToHost, s));
+    ev_rec(c, 6);
+    sync(c);
+    HIPCHK(hipGetLastError());
+    p.put(drop); p.put(bytes); p.put(off); p.put(tmp); p.put(poff);
+    c->out_bytes = total;
+    c->st.ms_sort = ev_ms(c, 4, 5);
+    c->st.ms_format = ev_ms(c, 5, 6);
+    c->st.output_bytes = total;
+    c->reduced = true;
+}
+
 void job_reduce(mrg_ctx *c) {
     need_job(c);
     if (!c->mapped) raise(MRG_EINVAL, "nothing to reduce: call mrg_job_map or mrg_job_import first");
+    if (c->wide.ready) {
+        wide_reduce(c);
+        return;
+    }
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     const uint64_t n = c->keys.n;
@@ -797,6 +1039,7 @@ void job_reduce(mrg_ctx *c) {
 void job_final(mrg_ctx *c) {
     need_job(c);
     if (!c->mapped) raise(MRG_EINVAL, "no keys: call mrg_job_map or mrg_job_import first");
+    wide_densify(c, 0);
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     const uint64_t n = c->keys.n;
@@ -830,6 +1073,7 @@ void export_sizes(mrg_ctx *c, uint32_t n_owners, uint64_t *h_rec, uint64_t *h_he
     need_job(c);
     if (!c->mapped) raise(MRG_EINVAL, "export before map");
     if (n_owners == 0) raise(MRG_EINVAL, "n_owners must be > 0");
+    wide_densify(c, 0);
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     unsigned long long *d = pget<unsigned long long>(p, 2ull * n_owners);

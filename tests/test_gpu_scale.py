@@ -108,7 +108,8 @@ def test_c5_slice_vs_oracle(ctx):
 
 @pytest.fixture
 def knobs():
-    keys = ["MRG_TEST_TAIL_CAP", "MRG_TEST_OVF_CAP", "MRG_TEST_AGG_OCAP", "MRG_WIDE"]
+    keys = ["MRG_TEST_TAIL_CAP", "MRG_TEST_OVF_CAP", "MRG_TEST_AGG_OCAP", "MRG_WIDE", "MRG_TEST_LEAF_CAP",
+            "MRG_TEST_LEAF_TARGET"]
     saved = {k: os.environ.get(k) for k in keys}
 
     def set_(**kw):
@@ -291,3 +292,39 @@ def test_two_ranks_library_exchange(tmp_path):
         assert sorted(int(r) for r in merged[R]) == list(range(int(R)))
         for r in range(int(R)):
             assert merged[R][str(r)] == GOLDEN["wc"][R][f"mr-{r}.txt"], (R, r)
+
+
+@pytest.mark.parametrize("cap,target", [("0", "1024"), ("8", "1024"), ("0", "16"), ("64", "100000")])
+def test_wide_sample_sort_knobs_vs_oracle(ctx, corpus, knobs, cap, target):
+    """The wide aggregation (k_wide.hip) with its leaf capacity / leaf size knobs: cap 8 sends most
+    leaves to the global-sort fallback, target 16 makes thousands of tiny leaves, target 100000 one
+    leaf per L1 bucket (its distinct keys overflow a 64-key cap).  Inputs: near-unique keys, Zipf
+    (hot keys come through the flushed map tables as weighted keys), the corpus, long keys."""
+    import torch
+    import oracle_lib as O
+    from gpu_util import run_wc
+    n = 4 * MIB
+    t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
+    ctx.gen_unique(t.data_ptr(), n, 0xC5, 9)
+    uniq = t[:n].cpu().numpy().tobytes()
+    ctx.gen_zipf(t.data_ptr(), n, 0x5EED2026, 3, 1 << 14, 1.1)
+    zipf = t[:n].cpu().numpy().tobytes()
+    knobs(MRG_WIDE=1, MRG_TEST_LEAF_CAP=cap, MRG_TEST_LEAF_TARGET=target)
+    for docs, R in (([uniq], 16), ([zipf, uniq[:MIB]], 7), (corpus, 10), ([uniq, b"x" * 40 + b" y"], 3)):
+        assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST), (len(docs), R)
+    if cap == "8":
+        assert ctx.stats()["overflow_keys"] > 0   # leaves finished by the fallback
+
+
+def test_wide_many_partitions_vs_oracle(ctx, knobs):
+    """R > 4096 takes the radix-sort form of the wide aggregation (the L1 histogram is per-LDS)."""
+    import torch
+    import oracle_lib as O
+    from gpu_util import run_wc
+    n = 2 * MIB
+    t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
+    ctx.gen_unique(t.data_ptr(), n, 0xC5, 11)
+    docs = [t[:n].cpu().numpy().tobytes()]
+    knobs(MRG_WIDE=1)
+    for R in (5000, 4096):
+        assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST), R
