@@ -34,9 +34,18 @@ __device__ __forceinline__ GASW T *gw(T *p) {
 constexpr int W_WG = 1024;
 constexpr int W_NW = W_WG / 64;
 constexpr uint32_t W_S2 = 8192;       // L2 samples per L1 bucket (sorted in LDS)
-constexpr uint32_t W_SLOTS = 4096;    // leaf LDS table slots
-constexpr uint32_t W_MAXD = 3072;     // distinct keys a leaf may hold (75 % load)
+constexpr int W_LWG = 256;            // leaf workgroup (four per CU: while one waits on memory, others work)
+constexpr int W_LNW = W_LWG / 64;
+constexpr uint32_t W_SLOTS = 1024;    // leaf LDS table slots
+constexpr uint32_t W_MAXD = 768;      // distinct keys a leaf may hold (75 % load)
 constexpr uint32_t W_SEGLDS = 2048;   // segment offsets cached in LDS per L1 tile
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also makes every wave wait for its
+// outstanding global stores (vmcnt(0)) -- a store's full round trip at each of the many barriers of a
+// leaf -- though no kernel here exchanges global data between its waves: only LDS needs ordering.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 __device__ __forceinline__ bool key_lt(uint64_t a0, uint64_t a1, uint64_t b0, uint64_t b1) {
     return a0 < b0 || (a0 == b0 && a1 < b1);
@@ -88,14 +97,18 @@ __device__ __forceinline__ uint32_t upper_idx(const SP &sp, uint32_t m, uint64_t
     return lo;
 }
 
-__global__ void k_wmain_counts(BucketArgs A, uint64_t *cnt) {
+// segment sizes, and each segment's first record as an address (the L1 passes then read a record
+// with one load instead of two dependent table lookups and a 64-bit division)
+__global__ void k_wmain_counts(BucketArgs A, uint64_t *cnt, uint64_t *segptr) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t nt = (uint64_t)A.nreg * MRG_NBUCKET;
     if (s < nt) {
         const uint32_t b = (uint32_t)(s / A.nreg), w = (uint32_t)(s % A.nreg);
         cnt[s] = min(A.bcount[(uint64_t)w * MRG_NBUCKET + b], A.bcap[b]);
+        segptr[s] = (uint64_t)(A.pool + 2 * (A.rbase[b] + (uint64_t)w * A.bcap[b]));
     } else if (s < nt + MRG_NBUCKET) {
         cnt[s] = min(A.monext[s - nt], A.mocap);
+        segptr[s] = (uint64_t)(A.movf + 2 * ((s - nt) * A.mocap));
     }
 }
 
@@ -164,6 +177,7 @@ __global__ void k_wsplit1(const SortRec *smp, uint32_t S, uint32_t R, uint32_t B
 struct L1Args {
     BucketArgs A;
     const uint64_t *off;     // main segment offsets [nseg + 1]
+    const uint64_t *segptr;  // [nseg] address of each segment's first record
     uint64_t nseg, n;
     const uint64_t *spl1;    // [R][B1r - 1] (k0, k1)
     uint32_t R, B1r, B1, ntiles;
@@ -174,11 +188,12 @@ struct L1Args {
 // L1 tile t: records [t * T1, min(n, (t+1) * T1)); WITH_SCATTER: write them, else count them
 template <bool SCATTER>
 __global__ __launch_bounds__(W_WG, 1) void k_wl1(L1Args L) {
-    extern __shared__ uint64_t s_dyn[];  // spl1 (2 * R * (B1r-1) u64) | hist (B1 u32) | seg offsets
+    extern __shared__ uint64_t s_dyn[];  // spl1 (2 * R * (B1r-1) u64) | hist (B1 u32) | seg offsets | seg ptrs
     uint64_t *s_spl = s_dyn;
     const uint32_t m = L.B1r - 1u;
     uint32_t *s_h = reinterpret_cast<uint32_t *>(s_spl + 2ull * L.R * m);
     uint64_t *s_off = reinterpret_cast<uint64_t *>(s_h + ((L.B1 + 1u) & ~1u));
+    uint64_t *s_ptr = s_off + W_SEGLDS;
     __shared__ uint64_t s_lo, s_hi;
     const uint32_t tid = threadIdx.x, t = blockIdx.x;
     const uint64_t t0 = (uint64_t)t * MRG_WIDE_T1, t1 = min(L.n, t0 + MRG_WIDE_T1);
@@ -189,34 +204,55 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl1(L1Args L) {
         s_lo = seg_find(off, 0, L.nseg, t0);
         s_hi = seg_find(off, 0, L.nseg, t1 - 1u) + 1u;
     }
-    __syncthreads();
+    lds_barrier();
     const uint64_t slo = s_lo, shi = s_hi;
     const bool cached = shi - slo + 1u <= W_SEGLDS;
     if (cached)
-        for (uint64_t x = slo + tid; x <= shi; x += W_WG) s_off[x - slo] = L.off[x];
-    __syncthreads();
-    for (uint64_t i = t0 + tid; i < t1; i += W_WG) {
-        uint64_t s;
-        if (cached) s = seg_find([&](uint64_t x) { return s_off[x - slo]; }, slo, shi, i);
-        else s = seg_find([&](uint64_t x) { return L.off[x]; }, slo, shi, i);
-        uint64_t k0, k1;
-        main_rec(L.A, s, i - (cached ? s_off[s - slo] : L.off[s]), k0, k1);
-        const uint32_t r = part_of(k0, k1, L.R);
-        const uint32_t q = upper_idx(
-            [&](uint32_t x, uint64_t &a, uint64_t &b) {
-                a = s_spl[2ull * (r * m + x)];
-                b = s_spl[2ull * (r * m + x) + 1];
-            },
-            m, k0, k1);
-        const uint32_t b = r * L.B1r + q;
-        const uint32_t pos = atomicAdd(&s_h[b], 1u);
-        if (SCATTER) {
+        for (uint64_t x = slo + tid; x <= shi; x += W_WG) {
+            s_off[x - slo] = L.off[x];
+            if (x < shi) s_ptr[x - slo] = L.segptr[x];
+        }
+    lds_barrier();
+    // U records per thread per round: their loads are all in flight before the first is used
+    constexpr int U = 4;
+    for (uint64_t base = t0 + tid; base < t1; base += (uint64_t)U * W_WG) {
+        uint64_t k0[U], k1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = min(base + (uint64_t)u * W_WG, t1 - 1u);  // past the tile: a repeat, unused
+            const GASW uint64_t *rp;
+            if (cached) {
+                const uint64_t sg = seg_find([&](uint64_t x) { return s_off[x - slo]; }, slo, shi, i);
+                rp = reinterpret_cast<const GASW uint64_t *>(s_ptr[sg - slo]) + 2 * (i - s_off[sg - slo]);
+            } else {
+                const uint64_t sg = seg_find([&](uint64_t x) { return L.off[x]; }, slo, shi, i);
+                rp = reinterpret_cast<const GASW uint64_t *>(L.segptr[sg]) + 2 * (i - L.off[sg]);
+            }
             typedef uint64_t v2 __attribute__((ext_vector_type(2)));
-            *reinterpret_cast<GASW v2 *>(gw(L.out) + 2ull * pos) = v2{k0, k1};
+            const v2 x = *reinterpret_cast<const GASW v2 *>(rp);
+            k0[u] = x.x;
+            k1[u] = x.y;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (base + (uint64_t)u * W_WG >= t1) break;
+            const uint32_t r = part_of(k0[u], k1[u], L.R);
+            const uint32_t q = upper_idx(
+                [&](uint32_t x, uint64_t &a, uint64_t &b) {
+                    a = s_spl[2ull * (r * m + x)];
+                    b = s_spl[2ull * (r * m + x) + 1];
+                },
+                m, k0[u], k1[u]);
+            const uint32_t b = r * L.B1r + q;
+            const uint32_t pos = atomicAdd(&s_h[b], 1u);
+            if (SCATTER) {
+                typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+                *reinterpret_cast<GASW v2 *>(gw(L.out) + 2ull * pos) = v2{k0[u], k1[u]};
+            }
         }
     }
     if (!SCATTER) {
-        __syncthreads();
+        lds_barrier();
         for (uint32_t b = tid; b < L.B1; b += W_WG) L.cnt[(uint64_t)b * L.ntiles + t] = s_h[b];
     }
 }
@@ -237,19 +273,20 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
     }
     return v;
 }
-// exclusive block scan of one value per thread; s_ws holds W_NW words; *total = sum
+// exclusive block scan of one value per thread; s_ws holds NW words; *total = sum
+template <int NW = W_NW>
 __device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t *s_ws, uint32_t *total) {
     const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
     const uint32_t inc = wave_scan_incl(v);
     if (lane == 63) s_ws[w] = inc;
-    __syncthreads();
+    lds_barrier();
     uint32_t base = 0, tot = 0;
-    for (uint32_t i = 0; i < (uint32_t)W_NW; ++i) {
+    for (uint32_t i = 0; i < (uint32_t)NW; ++i) {
         const uint32_t x = s_ws[i];
         base += i < w ? x : 0u;
         tot += x;
     }
-    __syncthreads();
+    lds_barrier();
     *total = tot;
     return base + inc - v;
 }
@@ -292,7 +329,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
             s_smp[2 * k] = a;
             s_smp[2 * k + 1] = c;
         }
-        __syncthreads();
+        lds_barrier();
         for (uint32_t size = 2; size <= P; size <<= 1) {
             for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
                 for (uint32_t t = tid; t < P / 2; t += W_WG) {
@@ -305,7 +342,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
                         s_smp[2 * j] = a0; s_smp[2 * j + 1] = a1;
                     }
                 }
-                __syncthreads();
+                lds_barrier();
             }
         }
         for (uint32_t q = tid; q + 1 < B2; q += W_WG) {
@@ -318,14 +355,24 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         s_cnt[j] = 0;
         s_cur[j] = 0;
     }
-    __syncthreads();
+    lds_barrier();
     auto sub_of = [&](uint64_t k0, uint64_t k1) {
         return upper_idx([&](uint32_t x, uint64_t &a, uint64_t &c) { a = s_spl[2 * x]; c = s_spl[2 * x + 1]; }, B2 - 1u,
                          k0, k1);
     };
-    // ---- histogram
-    for (uint64_t i = tid; i < nb; i += W_WG) atomicAdd(&s_cnt[sub_of(in[2 * i], in[2 * i + 1])], 1u);
-    __syncthreads();
+    // ---- histogram (U records per thread in flight)
+    constexpr int U = 4;
+    typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+    const GASW v2 *inv = reinterpret_cast<const GASW v2 *>(in);
+    for (uint64_t i0 = tid; i0 < nb; i0 += (uint64_t)U * W_WG) {
+        v2 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = inv[min(i0 + (uint64_t)u * W_WG, nb - 1u)];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + (uint64_t)u * W_WG < nb) atomicAdd(&s_cnt[sub_of(x[u].x, x[u].y)], 1u);
+    }
+    lds_barrier();
     {  // exclusive scan of the B2 <= 1024 counts, one per thread
         const uint32_t v = tid < B2 ? s_cnt[tid] : 0u;
         uint32_t tot;
@@ -351,14 +398,16 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         }
         if (tid == 0) L.nleaf[b] = B2;
     }
-    __syncthreads();
+    lds_barrier();
     // ---- scatter
-    GASW uint64_t *out = gw(L.out) + 2 * base;
-    for (uint64_t i = tid; i < nb; i += W_WG) {
-        const uint64_t k0 = in[2 * i], k1 = in[2 * i + 1];
-        const uint32_t pos = atomicAdd(&s_cur[sub_of(k0, k1)], 1u);
-        typedef uint64_t v2 __attribute__((ext_vector_type(2)));
-        *reinterpret_cast<GASW v2 *>(out + 2ull * pos) = v2{k0, k1};
+    GASW v2 *outv = reinterpret_cast<GASW v2 *>(gw(L.out) + 2 * base);
+    for (uint64_t i0 = tid; i0 < nb; i0 += (uint64_t)U * W_WG) {
+        v2 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = inv[min(i0 + (uint64_t)u * W_WG, nb - 1u)];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + (uint64_t)u * W_WG < nb) outv[atomicAdd(&s_cur[sub_of(x[u].x, x[u].y)], 1u)] = x[u];
     }
 }
 
@@ -385,6 +434,7 @@ struct LeafArgs {
     unsigned long long *ovf_n;
     unsigned long long *nkeys;
     uint64_t *wr;            // [leaves][2] weighted-key range of each leaf (k_wranges)
+    unsigned long long *prof;  // MRG_WIDE_PROF builds: phase clocks
 };
 
 // first weighted key >= (p, a, b)
@@ -432,48 +482,86 @@ __global__ void k_wranges(LeafArgs L, uint32_t B1) {
     L.wr[2 * lid + 1] = hi;
 }
 
-// 12 bits of the 128-bit big-endian key (k0:k1) starting at bit position hb (0 = most significant)
-__device__ __forceinline__ uint32_t key_bits12(uint64_t k0, uint64_t k1, uint32_t hb) {
+// W_DBITS bits of the 128-bit big-endian key (k0:k1) starting at bit hb (0 = most significant)
+constexpr uint32_t W_DBITS = 10;
+__device__ __forceinline__ uint32_t key_digit(uint64_t k0, uint64_t k1, uint32_t hb) {
     // top 64 bits of (k0:k1) << hb
     const uint64_t t = hb == 0 ? k0 : (hb < 64 ? (k0 << hb) | (k1 >> (64 - hb)) : k1 << (hb - 64));
-    return (uint32_t)(t >> 52);
+    return (uint32_t)(t >> (64 - W_DBITS));
 }
 
 // One workgroup per L1 bucket walks its leaves.  Per leaf: sum the records per key in an LDS hash
-// table, list the distinct keys, bucket them by the 12 key bits after their common prefix (a
-// counting sort), order each bucket by comparing its (few) keys, write keys + counts + line bytes.
-// A leaf whose buckets are large (keys that agree beyond those 12 bits) is ordered by an LSD radix
-// sort over its varying key bytes instead.
-constexpr uint32_t W_NDIG = 4096;         // 12-bit digits
+// table, compact the distinct keys, bucket them by the W_DBITS key bits after their common prefix
+// (a counting sort), rank each key inside its (small) bucket by comparisons and store it at its
+// final position together with its count; the leaf's line bytes are summed on the way.  The next
+// leaf's records are loaded while the current one is sorted.  A leaf whose buckets are large (keys
+// that agree beyond those bits) is ordered by an LSD radix sort over its varying key bytes instead.
+constexpr uint32_t W_NDIG = 1u << W_DBITS;
 constexpr uint32_t W_MAXBKT = 64;         // largest bucket ordered by comparisons
+constexpr uint32_t W_LR = (W_MAXD + W_LWG - 1) / W_LWG;   // items per thread (3)
+constexpr int W_PF = 2;                   // records per thread prefetched for the next leaf
 
-__global__ __launch_bounds__(W_WG, 1) void k_wleaf(LeafArgs L) {
-    __shared__ uint64_t s_k[2 * W_SLOTS];     // table keys (k0, k1); k0 == 0 = empty
-    __shared__ uint64_t s_c[W_SLOTS];         // counts
-    __shared__ uint16_t s_ia[W_MAXD], s_ib[W_MAXD];   // slot lists
-    __shared__ __attribute__((aligned(16))) uint16_t s_x[3 * W_NW * 256];  // digit counts + starts / radix cells (24 KiB)
-    __shared__ uint32_t s_ws[W_NW];
+__global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
+    typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+    __shared__ v2 s_k[W_SLOTS];               // table keys (k0, k1); k0 == 0 = empty; then bucket order
+    __shared__ uint64_t s_c[W_SLOTS];         // table counts
+    __shared__ v2 s_kc[W_MAXD];               // distinct keys, compacted
+    __shared__ uint64_t s_cc[W_MAXD];         // their counts
+    __shared__ uint16_t s_ia[W_MAXD], s_ib[W_MAXD];   // index lists (radix path)
+    // digit counts (u32) + starts (u16), or the radix cells (W_LR x W_LNW x 256 u16): 6 KiB
+    __shared__ __attribute__((aligned(16))) uint16_t s_x[W_LR * W_LNW * 256];
+    __shared__ uint32_t s_ws[W_LNW];
     __shared__ uint32_t s_nd, s_ovf, s_maxb;
-    __shared__ uint64_t s_or0, s_or1;
-    uint32_t *s_dcnt = reinterpret_cast<uint32_t *>(s_x);   // counting sort: per-digit count (16 KiB)
-    uint16_t *s_doff = s_x + 2 * W_NDIG;                     // and start (8 KiB)
+    __shared__ uint64_t s_or0, s_or1, s_bytes;
+    uint32_t *s_dcnt = reinterpret_cast<uint32_t *>(s_x);   // counting sort: per-digit count
+    uint16_t *s_doff = s_x + 2 * W_NDIG;                     // and start
+    v2 *s_kb = s_k;                                          // keys in bucket order (table reused)
+    static_assert(2 * W_NDIG * 2 + W_NDIG * 2 <= sizeof(s_x), "digit arrays fit the cells");
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint32_t nl = L.nleaf[b];
     const uint64_t bend = L.bstart[b + 1];
     const uint64_t lt = mrg_lanemask_lt();
+    const GASW v2 *kin = reinterpret_cast<const GASW v2 *>(gw(L.kin));
+    unsigned long long wg_keys = 0;   // distinct keys of this workgroup's leaves (thread 0)
+#ifdef MRG_WIDE_PROF  // diagnostic build: per-phase clocks of wave 0, summed into L.prof[8]
+    uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl = clock64();
+#define WP(i) { const uint64_t t_ = clock64(); pacc[i] += t_ - tl; tl = t_; }
+#else
+#define WP(i)
+#endif
+    auto leaf_range = [&](uint32_t j, uint64_t &lo, uint64_t &hi) {
+        const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + j;
+        lo = L.leaf_lo[lid];
+        hi = j + 1 < nl ? L.leaf_lo[lid + 1] : bend;
+    };
+    // first W_PF * W_LWG records of leaf j into registers (a record past the leaf: a repeat, unused)
+    v2 pf[W_PF];
+    auto prefetch = [&](uint32_t j) {
+        if (j >= nl) return;
+        uint64_t lo, hi;
+        leaf_range(j, lo, hi);
+        if (hi == lo) return;
+#pragma unroll
+        for (int u = 0; u < W_PF; ++u) pf[u] = kin[lo + min((uint64_t)(tid + u * W_LWG), hi - lo - 1u)];
+    };
+    prefetch(0);
     for (uint32_t j = 0; j < nl; ++j) {
         const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + j;
-        const uint64_t mlo = L.leaf_lo[lid], mhi = j + 1 < nl ? L.leaf_lo[lid + 1] : bend;
+        uint64_t mlo, mhi;
+        leaf_range(j, mlo, mhi);
         const uint64_t wlo = L.wr[2 * lid], whi = L.wr[2 * lid + 1];
         const uint64_t nm = mhi - mlo, nwk = whi - wlo;
         const uint64_t out0 = mlo + wlo;
+        v2 cur[W_PF];
+#pragma unroll
+        for (int u = 0; u < W_PF; ++u) cur[u] = pf[u];
+        prefetch(j + 1);   // in flight while this leaf is processed
         // table size: a power of two >= 2 x records (a leaf of duplicates still fits: distinct counts)
         uint32_t S = 64;
         while (S < W_SLOTS && (uint64_t)S < 2 * (nm + nwk)) S <<= 1;
-        for (uint32_t i = tid; i < S; i += W_WG) {
-            s_k[2 * i] = MRG_EMPTY_K0;
-            s_k[2 * i + 1] = MRG_EMPTY_K1;
+        for (uint32_t i = tid; i < S; i += W_LWG) {
+            s_k[i] = v2{MRG_EMPTY_K0, MRG_EMPTY_K1};
             s_c[i] = 0;
         }
         if (tid == 0) {
@@ -482,22 +570,24 @@ __global__ __launch_bounds__(W_WG, 1) void k_wleaf(LeafArgs L) {
             s_maxb = 0;
             s_or0 = 0;
             s_or1 = 0;
+            s_bytes = 0;
         }
-        __syncthreads();
+        lds_barrier();
+        WP(0);
         // ---- sum the records per key (exact: full keys compared; slots fill monotonically)
         auto add = [&](uint64_t a, uint64_t c, uint64_t n) {
             uint32_t slot = w_hash(a, c) & (S - 1u);
             for (uint32_t p = 0; p < S; ++p) {
-                const uint64_t ka = s_k[2 * slot], kb = s_k[2 * slot + 1];
-                if (ka == a && kb == c) {
+                const v2 k = s_k[slot];
+                if (k.x == a && k.y == c) {
                     atomicAdd((unsigned long long *)&s_c[slot], (unsigned long long)n);
                     return;
                 }
-                if (ka == MRG_EMPTY_K0 || (ka == a && kb == MRG_EMPTY_K1)) {
-                    const unsigned long long x = atomicCAS((unsigned long long *)&s_k[2 * slot], MRG_EMPTY_K0, a);
+                if (k.x == MRG_EMPTY_K0 || (k.x == a && k.y == MRG_EMPTY_K1)) {
+                    unsigned long long *kp = reinterpret_cast<unsigned long long *>(&s_k[slot]);
+                    const unsigned long long x = atomicCAS(kp, MRG_EMPTY_K0, a);
                     if (x == MRG_EMPTY_K0 || x == a) {
-                        const unsigned long long y =
-                            atomicCAS((unsigned long long *)&s_k[2 * slot + 1], MRG_EMPTY_K1, c);
+                        const unsigned long long y = atomicCAS(kp + 1, MRG_EMPTY_K1, c);
                         if (y == MRG_EMPTY_K1 || y == c) {
                             // a slot becomes a key exactly once, by the CAS that sets k1
                             if (y == MRG_EMPTY_K1 && atomicAdd(&s_nd, 1u) >= L.maxd) s_ovf = 1;
@@ -510,16 +600,20 @@ __global__ __launch_bounds__(W_WG, 1) void k_wleaf(LeafArgs L) {
             }
             s_ovf = 1;  // no slot left
         };
-        const GASW uint64_t *km = gw(L.kin) + 2 * mlo;
-        for (uint64_t i = tid; i < nm; i += W_WG) {
+#pragma unroll
+        for (int u = 0; u < W_PF; ++u)
+            if ((uint64_t)(tid + u * W_LWG) < nm) add(cur[u].x, cur[u].y, 1ull);
+        for (uint64_t i = tid + (uint64_t)W_PF * W_LWG; i < nm; i += W_LWG) {   // beyond the prefetch
             if (s_ovf) break;
-            add(km[2 * i], km[2 * i + 1], 1ull);
+            const v2 x = kin[mlo + i];
+            add(x.x, x.y, 1ull);
         }
-        for (uint64_t i = tid; i < nwk; i += W_WG) {
+        for (uint64_t i = tid; i < nwk; i += W_LWG) {
             if (s_ovf) break;
             add(L.wk0[wlo + i], L.wk1[wlo + i], L.wcnt[wlo + i]);
         }
-        __syncthreads();
+        lds_barrier();
+        WP(1);
         if (s_ovf) {  // finished by the global fallback (mrgpu.cpp)
             if (tid == 0) {
                 const unsigned long long k = atomicAdd(L.ovf_n, 1ull);
@@ -529,35 +623,51 @@ __global__ __launch_bounds__(W_WG, 1) void k_wleaf(LeafArgs L) {
                 L.leaf_bytes[lid] = 0;
                 L.leaf_last[lid] = 0;
             }
-            __syncthreads();
+            lds_barrier();
             continue;
         }
-        // ---- list the occupied slots (s_ia), the bits on which keys differ, clear the digit counts
+        // ---- compact the distinct keys (s_kc, s_cc); clear the digit counts
         const uint32_t D = s_nd;
-        __syncthreads();
+        lds_barrier();
         if (tid == 0) s_nd = 0;
-        for (uint32_t i = tid; i < W_NDIG; i += W_WG) s_dcnt[i] = 0;
-        __syncthreads();
-        for (uint32_t i0 = 0; i0 < S; i0 += W_WG) {
+        for (uint32_t i = tid; i < W_NDIG; i += W_LWG) s_dcnt[i] = 0;
+        lds_barrier();
+        for (uint32_t i0 = 0; i0 < S; i0 += W_LWG) {
             const uint32_t i = i0 + tid;
-            const bool full = i < S && s_k[2 * i] != MRG_EMPTY_K0;
+            v2 k = v2{0, 0};
+            uint64_t n = 0;
+            if (i < S) {
+                k = s_k[i];
+                n = s_c[i];
+            }
+            const bool full = k.x != MRG_EMPTY_K0;
             const uint64_t m = __ballot(full);
             uint32_t basew = 0;
             if (lane == 0 && m) basew = atomicAdd(&s_nd, (uint32_t)__popcll(m));
             basew = __shfl(basew, 0);
-            if (full) s_ia[basew + (uint32_t)__popcll(m & lt)] = (uint16_t)i;
+            if (full) {
+                const uint32_t pos = basew + (uint32_t)__popcll(m & lt);
+                s_kc[pos] = k;
+                s_cc[pos] = n;
+            }
         }
-        __syncthreads();
-        uint64_t f0 = 0, f1 = 0;
-        if (D) {
-            f0 = s_k[2 * s_ia[0]];
-            f1 = s_k[2 * s_ia[0] + 1];
-        }
+        lds_barrier();
+        // ---- my items (compacted index p = k * W_LWG + tid) in registers; the bits keys differ on
+        const uint32_t NR = (D + W_LWG - 1) / W_LWG;   // items per thread (<= W_LR)
+        v2 key[W_LR];
+        uint64_t cnt[W_LR];
         {
+            const v2 f = D ? s_kc[0] : v2{0, 0};
             uint64_t o0 = 0, o1 = 0;
-            for (uint32_t p = tid; p < D; p += W_WG) {
-                o0 |= s_k[2 * s_ia[p]] ^ f0;
-                o1 |= s_k[2 * s_ia[p] + 1] ^ f1;
+#pragma unroll
+            for (uint32_t k = 0; k < W_LR; ++k) {
+                const uint32_t p = k * W_LWG + tid;
+                if (k < NR && p < D) {
+                    key[k] = s_kc[p];
+                    cnt[k] = s_cc[p];
+                    o0 |= key[k].x ^ f.x;
+                    o1 |= key[k].y ^ f.y;
+                }
             }
             for (int o = 32; o > 0; o >>= 1) {
                 o0 |= __shfl_xor(o0, o);
@@ -568,75 +678,92 @@ __global__ __launch_bounds__(W_WG, 1) void k_wleaf(LeafArgs L) {
                 atomicOr((unsigned long long *)&s_or1, (unsigned long long)o1);
             }
         }
-        __syncthreads();
+        lds_barrier();
+        WP(2);
         const uint64_t o0 = s_or0, o1 = s_or1;
-        // first differing bit (0 = most significant bit of k0); the digit = the 12 bits from there
+        // first differing bit (0 = most significant bit of k0); the digit = the W_DBITS bits from there
         uint32_t hb = o0 ? (uint32_t)__builtin_clzll(o0) : (o1 ? 64u + (uint32_t)__builtin_clzll(o1) : 0u);
-        if (hb > 116u) hb = 116u;
+        if (hb > 128u - W_DBITS) hb = 128u - W_DBITS;
         // ---- counting sort by digit: bucket counts, then starts
-        uint32_t dg[3], sl[3], within[3];
-        const uint32_t NR = (D + W_WG - 1) / W_WG;   // items per thread (<= 3)
-        for (uint32_t k = 0; k < NR; ++k) {
-            const uint32_t p = k * W_WG + tid;
+        uint32_t dg[W_LR], within[W_LR];
+#pragma unroll
+        for (uint32_t k = 0; k < W_LR; ++k) {
+            const uint32_t p = k * W_LWG + tid;
             dg[k] = 0xFFFFFFFFu;
-            if (p < D) {
-                sl[k] = s_ia[p];
-                dg[k] = key_bits12(s_k[2 * sl[k]], s_k[2 * sl[k] + 1], hb);
+            if (k < NR && p < D) {
+                dg[k] = key_digit(key[k].x, key[k].y, hb);
                 within[k] = atomicAdd(&s_dcnt[dg[k]], 1u);  // slot inside the bucket (any order)
             }
         }
-        __syncthreads();
-        {  // exclusive scan of the 4096 counts: 4 per thread; note the largest bucket
-            uint32_t v[4], sum = 0, mx = 0;
-            for (uint32_t x = 0; x < 4; ++x) {
-                v[x] = s_dcnt[tid * 4 + x];
+        lds_barrier();
+        {  // exclusive scan of the digit counts, W_NDIG / W_LWG per thread; note the largest bucket
+            constexpr uint32_t PT = W_NDIG / W_LWG;
+            uint32_t v[PT], sum = 0, mx = 0;
+            for (uint32_t x = 0; x < PT; ++x) {
+                v[x] = s_dcnt[tid * PT + x];
                 sum += v[x];
                 mx = max(mx, v[x]);
             }
             if (mx > W_MAXBKT) atomicMax(&s_maxb, mx);
             uint32_t tot;
-            uint32_t run = block_scan_excl(sum, s_ws, &tot);
-            for (uint32_t x = 0; x < 4; ++x) {
-                s_doff[tid * 4 + x] = (uint16_t)run;
+            uint32_t run = block_scan_excl<W_LNW>(sum, s_ws, &tot);
+            for (uint32_t x = 0; x < PT; ++x) {
+                s_doff[tid * PT + x] = (uint16_t)run;
                 run += v[x];
             }
         }
-        __syncthreads();
-        uint16_t *src = s_ia;
+        lds_barrier();
+        WP(3);
+        GASW v2 *ko = reinterpret_cast<GASW v2 *>(gw(L.kout)) + out0;
+        GASW uint64_t *co = gw(L.ocnt) + out0;
+        uint64_t bytes = 0;
         if (s_maxb == 0) {
-            // ---- bucket order by comparisons: rank = keys of the same bucket that are smaller
-            for (uint32_t k = 0; k < NR; ++k)
-                if (dg[k] != 0xFFFFFFFFu) s_ib[s_doff[dg[k]] + within[k]] = (uint16_t)sl[k];
-            __syncthreads();
-            for (uint32_t k = 0; k < NR; ++k) {
+            // ---- keys in bucket order, then rank = keys of the same bucket that are smaller
+#pragma unroll
+            for (uint32_t k = 0; k < W_LR; ++k)
+                if (dg[k] != 0xFFFFFFFFu) s_kb[s_doff[dg[k]] + within[k]] = key[k];
+            lds_barrier();
+#pragma unroll
+            for (uint32_t k = 0; k < W_LR; ++k) {
                 if (dg[k] == 0xFFFFFFFFu) continue;
                 const uint32_t bs = s_doff[dg[k]], bn = s_dcnt[dg[k]];
-                const uint64_t a0 = s_k[2 * sl[k]], a1 = s_k[2 * sl[k] + 1];
                 uint32_t rank = 0;
-                for (uint32_t q = 0; q < bn; ++q) {
-                    const uint32_t o = s_ib[bs + q];
-                    rank += key_lt(s_k[2 * o], s_k[2 * o + 1], a0, a1) ? 1u : 0u;
+                uint32_t q = 0;
+                for (; q + 2 <= bn; q += 2) {   // two independent LDS reads per step
+                    const v2 x = s_kb[bs + q], y = s_kb[bs + q + 1];
+                    rank += (key_lt(x.x, x.y, key[k].x, key[k].y) ? 1u : 0u) +
+                            (key_lt(y.x, y.y, key[k].x, key[k].y) ? 1u : 0u);
                 }
-                s_ia[bs + rank] = (uint16_t)sl[k];
+                if (q < bn) {
+                    const v2 x = s_kb[bs + q];
+                    rank += key_lt(x.x, x.y, key[k].x, key[k].y) ? 1u : 0u;
+                }
+                const uint32_t pos = bs + rank;
+                ko[pos] = key[k];
+                co[pos] = cnt[k];
+                const uint32_t ll = line_len(key[k].x, key[k].y, cnt[k]);
+                bytes += ll;
+                if (pos == D - 1) L.leaf_last[lid] = ll;
             }
-            __syncthreads();
         } else {
-            // ---- LSD radix sort of the slot list by the varying key bytes (stable, per-wave ranks)
+            // ---- LSD radix sort of the index list by the varying key bytes (stable, per-wave ranks)
+            for (uint32_t p = tid; p < D; p += W_LWG) s_ia[p] = (uint16_t)p;
+            lds_barrier();
             const int qlo = (int)(hb >> 3);
             const int qhi = o1 ? 15 - (int)(__builtin_ctzll(o1) >> 3) : 7 - (int)(__builtin_ctzll(o0) >> 3);
-            uint16_t *dst = s_ib;
+            uint16_t *src = s_ia, *dst = s_ib;
             uint16_t *s_wc = s_x;
             for (int q = qhi; q >= qlo; --q) {
-                for (uint32_t i = tid; i < NR * W_NW * 256; i += W_WG) s_wc[i] = 0;
-                __syncthreads();
-                uint32_t rk[3];
+                for (uint32_t i = tid; i < NR * W_LNW * 256; i += W_LWG) s_wc[i] = 0;
+                lds_barrier();
+                uint32_t rk[W_LR];
                 for (uint32_t k = 0; k < NR; ++k) {
-                    const uint32_t p = k * W_WG + tid;
+                    const uint32_t p = k * W_LWG + tid;
                     const bool valid = p < D;
                     uint32_t d = 0;
                     if (valid) {
-                        const uint32_t s2 = src[p];
-                        d = key_byte(s_k[2 * s2], s_k[2 * s2 + 1], (uint32_t)q);
+                        const v2 x = s_kc[src[p]];
+                        d = key_byte(x.x, x.y, (uint32_t)q);
                     }
                     uint64_t peers = __ballot(valid);
                     for (int bt = 0; bt < 8; ++bt) {
@@ -644,65 +771,67 @@ __global__ __launch_bounds__(W_WG, 1) void k_wleaf(LeafArgs L) {
                         peers &= ((d >> bt) & 1u) ? mb : ~mb;
                     }
                     const uint32_t rank = (uint32_t)__popcll(peers & lt);
-                    if (valid && rank == 0) s_wc[(d * NR + k) * W_NW + wv] = (uint16_t)__popcll(peers);
+                    if (valid && rank == 0) s_wc[(d * NR + k) * W_LNW + wv] = (uint16_t)__popcll(peers);
                     dg[k] = d;
                     rk[k] = valid ? rank : 0xFFFFFFFFu;
                 }
-                __syncthreads();
+                lds_barrier();
                 {  // exclusive scan over the cells in (digit, round, wave) order: stable positions
-                    const uint32_t C = 256u * NR * W_NW, per = C / W_WG;   // 4, 8 or 12 cells per thread
-                    uint32_t v[12];
+                    const uint32_t C = 256u * NR * W_LNW, per = C / W_LWG;
+                    uint32_t v[4 * W_LR];
                     uint32_t sum = 0;
                     for (uint32_t x = 0; x < per; ++x) {
                         v[x] = s_wc[tid * per + x];
                         sum += v[x];
                     }
                     uint32_t tot;
-                    uint32_t run = block_scan_excl(sum, s_ws, &tot);
+                    uint32_t run = block_scan_excl<W_LNW>(sum, s_ws, &tot);
                     for (uint32_t x = 0; x < per; ++x) {
                         s_wc[tid * per + x] = (uint16_t)run;
                         run += v[x];
                     }
                 }
-                __syncthreads();
+                lds_barrier();
                 for (uint32_t k = 0; k < NR; ++k) {
-                    const uint32_t p = k * W_WG + tid;
-                    if (rk[k] != 0xFFFFFFFFu) dst[s_wc[(dg[k] * NR + k) * W_NW + wv] + rk[k]] = src[p];
+                    const uint32_t p = k * W_LWG + tid;
+                    if (rk[k] != 0xFFFFFFFFu) dst[s_wc[(dg[k] * NR + k) * W_LNW + wv] + rk[k]] = src[p];
                 }
-                __syncthreads();
+                lds_barrier();
                 uint16_t *tmp = src;
                 src = dst;
                 dst = tmp;
             }
+            for (uint32_t p = tid; p < D; p += W_LWG) {
+                const uint32_t i = src[p];
+                const v2 x = s_kc[i];
+                const uint64_t n = s_cc[i];
+                ko[p] = x;
+                co[p] = n;
+                const uint32_t ll = line_len(x.x, x.y, n);
+                bytes += ll;
+                if (p == D - 1) L.leaf_last[lid] = ll;
+            }
         }
-        // ---- write the sorted distinct keys + the leaf's line bytes
-        GASW uint64_t *ko = gw(L.kout) + 2 * out0;
-        uint64_t bytes = 0;
-        for (uint32_t p = tid; p < D; p += W_WG) {
-            const uint32_t s2 = src[p];
-            const uint64_t a = s_k[2 * s2], c = s_k[2 * s2 + 1], n = s_c[s2];
-            typedef uint64_t v2 __attribute__((ext_vector_type(2)));
-            *reinterpret_cast<GASW v2 *>(ko + 2 * p) = v2{a, c};
-            gw(L.ocnt)[out0 + p] = n;
-            const uint32_t ll = line_len(a, c, n);
-            bytes += ll;
-            if (p == D - 1) L.leaf_last[lid] = ll;
-        }
+        WP(4);
         for (int o = 32; o > 0; o >>= 1) bytes += __shfl_xor(bytes, o);
-        __syncthreads();
-        if (tid == 0) s_or0 = 0;
-        __syncthreads();
-        if (lane == 0) atomicAdd((unsigned long long *)&s_or0, (unsigned long long)bytes);
-        __syncthreads();
+        if (lane == 0 && bytes) atomicAdd((unsigned long long *)&s_bytes, (unsigned long long)bytes);
+        lds_barrier();
         if (tid == 0) {
             L.leaf_out[lid] = out0;
             L.leaf_nd[lid] = D;
-            L.leaf_bytes[lid] = s_or0;
+            L.leaf_bytes[lid] = s_bytes;
             if (D == 0) L.leaf_last[lid] = 0;
-            atomicAdd(L.nkeys, (unsigned long long)D);
+            wg_keys += D;
         }
-        __syncthreads();
+        lds_barrier();
+        WP(5);
     }
+#ifdef MRG_WIDE_PROF
+    if (tid == 0)
+        for (int i = 0; i < 6; ++i) atomicAdd(&L.prof[i], (unsigned long long)pacc[i]);
+#endif
+    // one device-scope add per workgroup (a per-leaf add on one word would serialise ~2.7 M adds)
+    if (tid == 0 && wg_keys) atomicAdd(L.nkeys, wg_keys);
 }
 
 // last-group drop (worker.rs:169-184): the last key of the last non-empty leaf of partition r
@@ -724,63 +853,99 @@ __global__ void k_wdrop(const uint32_t *nleaf, uint32_t B1r, uint32_t R, const u
 }
 
 // ---------------------------------------------------------------- lines
-// One workgroup per L1 bucket: for each leaf, 1024 lines at a time are laid out in LDS and stored
-// to the output as aligned dwords (byte stores only at the two ends).
-constexpr uint32_t W_STAGE = 40 * 1024;   // >= 1024 lines of <= 16 + 1 + 20 + 1 bytes
+// One workgroup per L1 bucket streams the bucket's distinct keys (all its leaves, the dropped last
+// key of a partition excluded) in chunks of W_WCH: key i of the bucket -> its leaf by a search of
+// the leaves' running key counts (LDS), the lines laid out in LDS by a block scan of their lengths,
+// then stored to the output as aligned dwords (byte stores only at the two ends of a chunk).
+constexpr uint32_t W_WCH = 2048;              // keys per chunk (2 per thread)
+constexpr uint32_t W_STAGE = 40 * W_WCH;      // >= W_WCH lines of <= 16 + 1 + 20 + 1 bytes
 
 __global__ __launch_bounds__(W_WG, 1) void k_wwrite(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *nleaf,
                                                     const uint64_t *leaf_out, const uint32_t *leaf_nd,
                                                     const uint32_t *leaf_drop, const uint64_t *leaf_off,
                                                     uint8_t *out) {
     __shared__ uint32_t s_buf[W_STAGE / 4];
+    __shared__ uint32_t s_kst[MRG_WIDE_MAXB2 + 1];   // keys before leaf l (this bucket)
+    __shared__ uint64_t s_lout[MRG_WIDE_MAXB2];
     __shared__ uint32_t s_ws[W_NW];
     uint8_t *sb = reinterpret_cast<uint8_t *>(s_buf);
     const uint32_t tid = threadIdx.x, b = blockIdx.x;
     const uint32_t nl = nleaf[b];
-    for (uint32_t j = 0; j < nl; ++j) {
-        const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + j;
-        const uint32_t D = leaf_nd[lid] - (leaf_drop[lid] ? 1u : 0u);
-        if ((int)D <= 0) continue;
-        const uint64_t o0 = leaf_out[lid];
-        uint64_t dst = leaf_off[lid];
-        for (uint32_t p0 = 0; p0 < D; p0 += W_WG) {
-            const uint32_t p = p0 + tid;
-            uint64_t a = 0, c = 0, n = 0;
-            uint32_t len = 0, nd = 0, ll = 0;
-            if (p < D) {
-                a = keys[2 * (o0 + p)];
-                c = keys[2 * (o0 + p) + 1];
-                n = ocnt[o0 + p];
-                len = mrg_short_len(a, c);
-                nd = mrg_ndigits(n);
-                ll = len + 2u + nd;
-            }
-            uint32_t tot;
-            const uint32_t at = block_scan_excl(ll, s_ws, &tot);
-            // the chunk's bytes start at dst; stage them at LDS offset (dst & 3) so dwords align
-            const uint32_t sh = (uint32_t)(dst & 3u);
-            if (p < D) {
-                uint8_t *o = sb + sh + at;
-                for (uint32_t x = 0; x < len; ++x) o[x] = (uint8_t)mrg_key_byte(a, c, x);
-                o[len] = ' ';
-                uint64_t v = n;
-                for (uint32_t x = nd; x > 0; --x) {
-                    o[len + x] = (uint8_t)('0' + v % 10u);
-                    v /= 10u;
-                }
-                o[len + 1 + nd] = '\n';
-            }
-            __syncthreads();
-            // copy [sh, sh + tot) of the stage to out[dst ..): dwords where both ends are inside
-            const uint64_t end = dst + tot;
-            const uint64_t a4 = (dst + 3u) & ~3ull, e4 = end & ~3ull;
-            for (uint64_t x = dst + tid; x < min(a4, end); x += W_WG) out[x] = sb[sh + (x - dst)];
-            for (uint64_t w = a4 / 4 + tid; w < e4 / 4; w += W_WG)
-                reinterpret_cast<uint32_t *>(out)[w] = s_buf[(sh + (w * 4 - dst)) / 4];
-            for (uint64_t x = max(e4, a4) + tid; x < end; x += W_WG) out[x] = sb[sh + (x - dst)];
-            dst = end;
-            __syncthreads();
+    const uint64_t l0 = (uint64_t)b * MRG_WIDE_MAXB2;
+    {  // running key counts of the leaves (MAXB2 / W_WG per thread)
+        constexpr uint32_t PT = MRG_WIDE_MAXB2 / W_WG;
+        uint32_t v[PT], sum = 0;
+        for (uint32_t x = 0; x < PT; ++x) {
+            const uint32_t l = tid * PT + x;
+            v[x] = l < nl ? leaf_nd[l0 + l] - (leaf_drop[l0 + l] ? 1u : 0u) : 0u;
+            if (l < nl) s_lout[l] = leaf_out[l0 + l];
+            sum += v[x];
         }
+        uint32_t tot;
+        uint32_t run = block_scan_excl(sum, s_ws, &tot);
+        for (uint32_t x = 0; x < PT; ++x) {
+            s_kst[tid * PT + x] = run;
+            run += v[x];
+        }
+        if (tid == 0) s_kst[MRG_WIDE_MAXB2] = tot;
+    }
+    lds_barrier();
+    const uint32_t K = s_kst[MRG_WIDE_MAXB2];
+    uint64_t dst = leaf_off[l0];
+    for (uint32_t c0 = 0; c0 < K; c0 += W_WCH) {
+        uint64_t a[2], c[2], n[2];
+        uint32_t len[2] = {0, 0}, nd[2] = {0, 0}, ll[2] = {0, 0};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const uint32_t i = c0 + 2 * tid + (uint32_t)u;   // thread t: keys 2t, 2t + 1 of the chunk
+            a[u] = c[u] = n[u] = 0;
+            if (i < K) {
+                uint32_t lo = 0, hi = nl;   // leaf l: s_kst[l] <= i < s_kst[l + 1] (last such l)
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_kst[mid] <= i) lo = mid;
+                    else hi = mid;
+                }
+                const uint64_t slot = s_lout[lo] + (i - s_kst[lo]);
+                a[u] = keys[2 * slot];
+                c[u] = keys[2 * slot + 1];
+                n[u] = ocnt[slot];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (c0 + 2 * tid + (uint32_t)u < K) {
+                len[u] = mrg_short_len(a[u], c[u]);
+                nd[u] = mrg_ndigits(n[u]);
+                ll[u] = len[u] + 2u + nd[u];
+            }
+        uint32_t tot;
+        const uint32_t at = block_scan_excl(ll[0] + ll[1], s_ws, &tot);
+        const uint32_t sh = (uint32_t)(dst & 3u);   // stage at (dst & 3): output dwords align in LDS
+        uint32_t o = sh + at;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (!ll[u]) continue;
+            uint8_t *q = sb + o;
+            for (uint32_t x = 0; x < len[u]; ++x) q[x] = (uint8_t)mrg_key_byte(a[u], c[u], x);
+            q[len[u]] = ' ';
+            uint64_t v = n[u];
+            for (uint32_t x = nd[u]; x > 0; --x) {
+                q[len[u] + x] = (uint8_t)('0' + v % 10u);
+                v /= 10u;
+            }
+            q[len[u] + 1 + nd[u]] = '\n';
+            o += ll[u];
+        }
+        lds_barrier();
+        const uint64_t end = dst + tot;
+        const uint64_t a4 = (dst + 3u) & ~3ull, e4 = end & ~3ull;
+        for (uint64_t x = dst + tid; x < min(a4, end); x += W_WG) out[x] = sb[sh + (x - dst)];
+        for (uint64_t w = a4 / 4 + tid; w < e4 / 4; w += W_WG)
+            reinterpret_cast<uint32_t *>(out)[w] = s_buf[(sh + (w * 4 - dst)) / 4];
+        for (uint64_t x = max(e4, a4) + tid; x < end; x += W_WG) out[x] = sb[sh + (x - dst)];
+        dst = end;
+        lds_barrier();
     }
 }
 
@@ -901,9 +1066,9 @@ __global__ void k_wfb_stats(const uint32_t *list, uint32_t nlist, const uint64_t
         bytes += line_len(keys[2 * (o0 + p)], keys[2 * (o0 + p) + 1], ocnt[o0 + p]);
     __shared__ unsigned long long s_b;
     if (threadIdx.x == 0) s_b = 0;
-    __syncthreads();
+    lds_barrier();
     atomicAdd(&s_b, (unsigned long long)bytes);
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x == 0) {
         leaf_nd[lid] = (uint32_t)D;
         leaf_bytes[lid] = s_b;
@@ -929,9 +1094,10 @@ inline dim3 gridw(uint64_t n, int b = 256) { return dim3((unsigned)((n + b - 1) 
 }  // namespace
 
 // ================================================================ host launchers (mrgpu.cpp)
-void mrg_wide_launch_counts(const BucketArgs &a, uint64_t *cnt_main, uint64_t *cnt_flush, hipStream_t s) {
+void mrg_wide_launch_counts(const BucketArgs &a, uint64_t *cnt_main, uint64_t *segptr, uint64_t *cnt_flush,
+                            hipStream_t s) {
     const uint64_t nsm = (uint64_t)a.nreg * MRG_NBUCKET + MRG_NBUCKET;
-    hipLaunchKernelGGL(k_wmain_counts, gridw(nsm), dim3(256), 0, s, a, cnt_main);
+    hipLaunchKernelGGL(k_wmain_counts, gridw(nsm), dim3(256), 0, s, a, cnt_main, segptr);
     hipLaunchKernelGGL(k_wflush_counts, gridw(a.nreg), dim3(256), 0, s, a, cnt_flush);
 }
 void mrg_wide_launch_flush_gather(const BucketArgs &a, const uint64_t *off, uint64_t *k0, uint64_t *k1, uint32_t *c,
@@ -946,12 +1112,12 @@ void mrg_wide_launch_split1(const SortRec *smp, uint32_t S, uint32_t R, uint32_t
     if (B1r > 1) hipLaunchKernelGGL(k_wsplit1, gridw((uint64_t)R * (B1r - 1)), dim3(256), 0, s, smp, S, R, B1r, spl);
 }
 size_t mrg_wide_l1_lds(uint32_t R, uint32_t B1r, uint32_t B1) {
-    return 16ull * R * (B1r - 1u) + 4ull * ((B1 + 1u) & ~1u) + 8ull * W_SEGLDS;
+    return 16ull * R * (B1r - 1u) + 4ull * ((B1 + 1u) & ~1u) + 16ull * W_SEGLDS;
 }
-void mrg_wide_launch_l1(const BucketArgs &a, const uint64_t *off, uint64_t nseg, uint64_t n, const uint64_t *spl1,
-                        uint32_t R, uint32_t B1r, uint32_t *cnt, uint32_t ntiles, uint64_t *out, bool scatter,
-                        hipStream_t s) {
-    L1Args L{a, off, nseg, n, spl1, R, B1r, R * B1r, ntiles, cnt, out};
+void mrg_wide_launch_l1(const BucketArgs &a, const uint64_t *off, const uint64_t *segptr, uint64_t nseg, uint64_t n,
+                        const uint64_t *spl1, uint32_t R, uint32_t B1r, uint32_t *cnt, uint32_t ntiles, uint64_t *out,
+                        bool scatter, hipStream_t s) {
+    L1Args L{a, off, segptr, nseg, n, spl1, R, B1r, R * B1r, ntiles, cnt, out};
     const size_t lds = mrg_wide_l1_lds(R, B1r, R * B1r);
     if (scatter) hipLaunchKernelGGL(k_wl1<true>, dim3(ntiles), dim3(W_WG), lds, s, L);
     else hipLaunchKernelGGL(k_wl1<false>, dim3(ntiles), dim3(W_WG), lds, s, L);
@@ -972,16 +1138,16 @@ void mrg_wide_launch_weights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *
 }
 void mrg_wide_launch_leaf(const WideLeafArgs &w, uint32_t B1, hipStream_t s) {
     LeafArgs L{w.kin, w.kout, w.bstart, w.nleaf, w.leaf_lo, w.leaf_lb, w.B1r, w.R, w.wk0, w.wk1, w.wcnt, w.wpart, w.nw,
-               w.maxd ? w.maxd : W_MAXD, w.ocnt, w.leaf_out, w.leaf_nd, w.leaf_bytes, w.leaf_last, w.ovf_list,
-               w.ovf_n, w.nkeys, w.wr};
+               w.maxd ? min(w.maxd, W_MAXD) : W_MAXD, w.ocnt, w.leaf_out, w.leaf_nd, w.leaf_bytes, w.leaf_last, w.ovf_list,
+               w.ovf_n, w.nkeys, w.wr, w.prof};
     hipLaunchKernelGGL(k_wranges, gridw((uint64_t)B1 * MRG_WIDE_MAXB2), dim3(256), 0, s, L, B1);
-    hipLaunchKernelGGL(k_wleaf, dim3(B1), dim3(W_WG), 0, s, L);
+    hipLaunchKernelGGL(k_wleaf, dim3(B1), dim3(W_LWG), 0, s, L);
 }
 void mrg_wide_launch_fallback(const WideLeafArgs &w, const uint32_t *list, uint32_t nlist, DevPool &pool,
                               hipStream_t s) {
     LeafArgs L{w.kin, w.kout, w.bstart, w.nleaf, w.leaf_lo, w.leaf_lb, w.B1r, w.R, w.wk0, w.wk1, w.wcnt, w.wpart, w.nw,
-               w.maxd ? w.maxd : W_MAXD, w.ocnt, w.leaf_out, w.leaf_nd, w.leaf_bytes, w.leaf_last, w.ovf_list,
-               w.ovf_n, w.nkeys, w.wr};
+               w.maxd ? min(w.maxd, W_MAXD) : W_MAXD, w.ocnt, w.leaf_out, w.leaf_nd, w.leaf_bytes, w.leaf_last, w.ovf_list,
+               w.ovf_n, w.nkeys, w.wr, w.prof};
     uint64_t *wrange = (uint64_t *)pool.get(16ull * nlist);
     uint64_t *cnt = (uint64_t *)pool.get(8ull * (nlist + 1)), *off = (uint64_t *)pool.get(8ull * (nlist + 1));
     uint64_t *scantmp = (uint64_t *)pool.get(8ull * mrg_scan_tmp_elems(nlist + 1));

@@ -269,17 +269,19 @@ struct WideLeafArgs {
     unsigned long long *ovf_n;
     unsigned long long *nkeys;   // += distinct keys of every finished leaf
     uint64_t *wr;                // [B1 * MRG_WIDE_MAXB2][2] scratch: weighted-key range of each leaf
+    unsigned long long *prof;    // diagnostics (builds with -DMRG_WIDE_PROF): leaf phase clocks [8]
 };
-void mrg_wide_launch_counts(const BucketArgs &a, uint64_t *cnt_main, uint64_t *cnt_flush, hipStream_t s);
+void mrg_wide_launch_counts(const BucketArgs &a, uint64_t *cnt_main, uint64_t *segptr, uint64_t *cnt_flush,
+                            hipStream_t s);
 void mrg_wide_launch_flush_gather(const BucketArgs &a, const uint64_t *off, uint64_t *k0, uint64_t *k1, uint32_t *c,
                                   hipStream_t s);
 void mrg_wide_launch_sample1(const BucketArgs &a, const uint64_t *off, uint64_t nseg, uint64_t n, uint32_t S,
                              uint32_t R, SortRec *out, hipStream_t s);
 void mrg_wide_launch_split1(const SortRec *smp, uint32_t S, uint32_t R, uint32_t B1r, uint64_t *spl, hipStream_t s);
 size_t mrg_wide_l1_lds(uint32_t R, uint32_t B1r, uint32_t B1);
-void mrg_wide_launch_l1(const BucketArgs &a, const uint64_t *off, uint64_t nseg, uint64_t n, const uint64_t *spl1,
-                        uint32_t R, uint32_t B1r, uint32_t *cnt, uint32_t ntiles, uint64_t *out, bool scatter,
-                        hipStream_t s);
+void mrg_wide_launch_l1(const BucketArgs &a, const uint64_t *off, const uint64_t *segptr, uint64_t nseg, uint64_t n,
+                        const uint64_t *spl1, uint32_t R, uint32_t B1r, uint32_t *cnt, uint32_t ntiles, uint64_t *out,
+                        bool scatter, hipStream_t s);
 void mrg_wide_launch_bstart(const uint32_t *cnt, uint32_t B1, uint32_t ntiles, uint64_t n, uint64_t *bstart,
                             hipStream_t s);
 void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstart, const uint64_t *spl1, uint32_t B1,

@@ -89,15 +89,20 @@ class Pool : public DevPool {
    public:
     void *get(size_t bytes) override {
         const size_t c = cls(bytes ? bytes : 1);
-        auto it = free_.find(c);
-        if (it != free_.end()) {
+        // smallest free block of this class or up to two classes above (record counts drift by a few
+        // between jobs over the same input: an exact-class pool would then miss, run out of device
+        // memory and trim everything)
+        auto it = free_.lower_bound(c);
+        if (it != free_.end() && it->first <= c + (c >> 2)) {
             void *p = it->second;
             free_.erase(it);
             return p;
         }
         void *p = nullptr;
+        if (debug_) fprintf(stderr, "[mrgpu] pool: allocating %zu bytes\n", c);
         if (hipMalloc(&p, c) != hipSuccess) {
             (void)hipGetLastError();
+            if (debug_) fprintf(stderr, "[mrgpu] pool: device full, trimming %zu free blocks\n", free_.size());
             trim();
             if (hipMalloc(&p, c) != hipSuccess) {
                 (void)hipGetLastError();
@@ -135,6 +140,7 @@ class Pool : public DevPool {
     }
     std::multimap<size_t, void *> free_;
     std::unordered_map<void *, size_t> size_;
+    bool debug_ = getenv("MRG_DEBUG") != nullptr;
 };
 
 template <class T>
@@ -530,14 +536,24 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     B.movf = A.ovf; B.monext = A.onext; B.mocap = A.ocap;
     B.fk0 = A.fk0; B.fk1 = A.fk1; B.fcnt = A.fcnt; B.fdoc = A.fdoc; B.foff = A.foff;
     B.nreg = nreg; B.regcap = regcap;
+    // MRG_DEBUG: HIP-event time of each phase
+    const bool dbg = getenv("MRG_DEBUG") != nullptr;
+    hipEvent_t pe[8] = {};
+    int npe = 0;
+    auto mark = [&]() {
+        if (!dbg || npe >= 8) return;
+        HIPCHK(hipEventCreate(&pe[npe]));
+        HIPCHK(hipEventRecord(pe[npe++], s));
+    };
+    mark();
     // ---- segment sizes: main (count 1) and flushed tables (weighted)
     const uint64_t nsm = (uint64_t)nreg * MRG_NBUCKET + MRG_NBUCKET;
-    uint64_t *cm = pget<uint64_t>(p, nsm + 1), *om = pget<uint64_t>(p, nsm + 1);
+    uint64_t *cm = pget<uint64_t>(p, nsm + 1), *om = pget<uint64_t>(p, nsm + 1), *segptr = pget<uint64_t>(p, nsm);
     uint64_t *cf = pget<uint64_t>(p, nreg + 1), *of = pget<uint64_t>(p, nreg + 1);
     uint64_t *st1 = pget<uint64_t>(p, mrg_scan_tmp_elems(nsm + 1));
     HIPCHK(hipMemsetAsync(cm + nsm, 0, 8, s));
     HIPCHK(hipMemsetAsync(cf + nreg, 0, 8, s));
-    mrg_wide_launch_counts(B, cm, cf, s);
+    mrg_wide_launch_counts(B, cm, segptr, cf, s);
     mrg_scan_u64(cm, om, nsm + 1, st1, s);
     mrg_scan_u64(cf, of, nreg + 1, st1, s);
     uint64_t nn[2] = {0, 0};
@@ -584,8 +600,9 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
         p.put(fk0); p.put(fk1); p.put(fc); p.put(ks.k0); p.put(ks.k1); p.put(ks.cnt); p.put(ks.hoff); p.put(ks.doc);
         p.put(ks.len); p.put(ks.part); p.put(T.tk0); p.put(T.tk1); p.put(T.tcnt); p.put(ra); p.put(rb); p.put(stmp);
     }
-    // ---- L1 buckets: R partitions x B1r quantile ranges of about 2^19 records
-    uint32_t B1r = (uint32_t)std::min<uint64_t>((n + ((uint64_t)R << 19) - 1) / ((uint64_t)R << 19), 64);
+    mark();  // 1: weighted keys done
+    // ---- L1 buckets: R partitions x B1r quantile ranges of about 2^18 records
+    uint32_t B1r = (uint32_t)std::min<uint64_t>((n + ((uint64_t)R << 18) - 1) / ((uint64_t)R << 18), 64);
     B1r = std::max<uint32_t>(1, std::min<uint32_t>(B1r, std::max<uint32_t>(1, 4096 / R)));
     const uint32_t B1 = R * B1r;
     uint64_t *spl1 = pget<uint64_t>(p, 2ull * R * B1r + 2);
@@ -604,27 +621,30 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
         sync(c);
         p.put(sa); p.put(sb); p.put(stmp);
     }
+    mark();  // 2: splitters
     const uint32_t ntiles = (uint32_t)std::max<uint64_t>(1, (n + MRG_WIDE_T1 - 1) / MRG_WIDE_T1);
     uint32_t *cnt1 = pget<uint32_t>(p, (uint64_t)B1 * ntiles + 1);
     uint32_t *st2 = pget<uint32_t>(p, mrg_scan_tmp_elems((uint64_t)B1 * ntiles + 1));
     uint64_t *K1 = pget<uint64_t>(p, 2 * (n + nw) + 2);
     uint64_t *bstart = pget<uint64_t>(p, B1 + 1);
     if (n) {
-        mrg_wide_launch_l1(B, om, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, false, s);
+        mrg_wide_launch_l1(B, om, segptr, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, false, s);
         mrg_scan_u32(cnt1, cnt1, (uint64_t)B1 * ntiles, st2, s);
-        mrg_wide_launch_l1(B, om, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, true, s);
+        mrg_wide_launch_l1(B, om, segptr, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, true, s);
     } else {
         HIPCHK(hipMemsetAsync(cnt1, 0, 4ull * B1 * ntiles, s));
     }
     mrg_wide_launch_bstart(cnt1, B1, ntiles, n, bstart, s);
-    p.put(cnt1); p.put(st2); p.put(cm); p.put(om); p.put(cf); p.put(of); p.put(st1);
+    p.put(cnt1); p.put(st2); p.put(cm); p.put(om); p.put(cf); p.put(of); p.put(st1); p.put(segptr);
+    mark();  // 3: L1
     // ---- L2: leaves inside every L1 bucket
     const uint64_t NL = (uint64_t)B1 * MRG_WIDE_MAXB2;
     uint64_t *K2 = pget<uint64_t>(p, 2 * n + 2);
     uint32_t *nleaf = pget<uint32_t>(p, B1);
     uint64_t *leaf_lo = pget<uint64_t>(p, NL + 1), *leaf_lb = pget<uint64_t>(p, 2 * NL + 2);
-    const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", 1024);
+    const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", 384);
     mrg_wide_launch_l2(K1, K2, bstart, spl1, B1, B1r, target, nleaf, leaf_lo, leaf_lb, s);
+    mark();  // 4: L2
     // ---- leaves: aggregate + sort + line bytes (K1 becomes the output key array)
     WideRes &w = c->wide;
     w.release(p);
@@ -649,18 +669,40 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     L.ocnt = w.ocnt; L.leaf_out = w.leaf_out; L.leaf_nd = w.leaf_nd; L.leaf_bytes = w.leaf_bytes;
     L.leaf_last = w.leaf_last; L.ovf_list = ovf_list; L.ovf_n = &c->d_cnt[CNT_OVF2]; L.nkeys = &c->d_cnt[CNT_KEYS];
     L.wr = pget<uint64_t>(p, 2 * NL);
+    L.prof = pget<unsigned long long>(p, 8);
+    HIPCHK(hipMemsetAsync(L.prof, 0, 64, s));
     mrg_wide_launch_leaf(L, B1, s);
+    mark();  // 5: leaves
     read_counters(c);
     const uint64_t novf = c->h_cnt[CNT_OVF2];
     if (novf) mrg_wide_launch_fallback(L, ovf_list, (uint32_t)novf, p, s);
+    mark();  // 6: fallback
     read_counters(c);
     w.distinct = c->h_cnt[CNT_KEYS];
     w.ready = true;
+    if (dbg) {
+        static const char *nm[] = {"weights", "splitters", "L1", "L2", "leaves", "fallback"};
+        fprintf(stderr, "[mrgpu] wide phases (ms):");
+        for (int i = 1; i < npe; ++i) {
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, pe[i - 1], pe[i]));
+            fprintf(stderr, " %s %.2f", nm[i - 1], ms);
+        }
+        fprintf(stderr, "\n");
+        for (int i = 0; i < npe; ++i) (void)hipEventDestroy(pe[i]);
+        unsigned long long pr[8];
+        HIPCHK(hipMemcpy(pr, L.prof, sizeof pr, hipMemcpyDeviceToHost));
+        if (pr[0] | pr[1] | pr[5])
+            fprintf(stderr, "[mrgpu] leaf phase clocks (wave 0, all WGs): clear %.3g insert %.3g list %.3g digits %.3g "
+                            "order %.3g write %.3g\n", (double)pr[0], (double)pr[1], (double)pr[2], (double)pr[3],
+                    (double)pr[4], (double)pr[5]);
+    }
     if (getenv("MRG_DEBUG"))
         fprintf(stderr, "[mrgpu] wide: %llu records, %llu weighted, B1 %u (x%u), %llu distinct, %llu leaves overflowed\n",
                 (unsigned long long)n, (unsigned long long)nw, B1, B1r, (unsigned long long)w.distinct,
                 (unsigned long long)novf);
     p.put(K2); p.put(leaf_lo); p.put(leaf_lb); p.put(ovf_list); p.put(spl1); p.put(bstart); p.put(L.wr);
+    p.put(L.prof);
     p.put(wk0); p.put(wk1); p.put(wcnt); p.put(wpart);
     c->st.overflow_keys = novf;
     c->keys.n = 0;
