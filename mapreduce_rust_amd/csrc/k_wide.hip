@@ -435,6 +435,8 @@ struct LeafArgs {
     unsigned long long *nkeys;
     uint64_t *wr;            // [leaves][2] weighted-key range of each leaf (k_wranges)
     unsigned long long *prof;  // MRG_WIDE_PROF builds: phase clocks
+    uint32_t *big_list;      // leaves the one-wave kernel passes to the workgroup kernel
+    unsigned long long *big_n;
 };
 
 // first weighted key >= (p, a, b)
@@ -499,7 +501,7 @@ __device__ __forceinline__ uint32_t key_digit(uint64_t k0, uint64_t k1, uint32_t
 constexpr uint32_t W_NDIG = 1u << W_DBITS;
 constexpr uint32_t W_MAXBKT = 64;         // largest bucket ordered by comparisons
 constexpr uint32_t W_LR = (W_MAXD + W_LWG - 1) / W_LWG;   // items per thread (3)
-constexpr int W_PF = 2;                   // records per thread prefetched for the next leaf
+constexpr int W_PF = (int)W_LR;           // records per thread prefetched for the next leaf
 
 __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
     typedef uint64_t v2 __attribute__((ext_vector_type(2)));
@@ -518,9 +520,7 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
     v2 *s_kb = s_k;                                          // keys in bucket order (table reused)
     static_assert(2 * W_NDIG * 2 + W_NDIG * 2 <= sizeof(s_x), "digit arrays fit the cells");
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    const uint32_t b = blockIdx.x;
-    const uint32_t nl = L.nleaf[b];
-    const uint64_t bend = L.bstart[b + 1];
+    const uint32_t nlist = (uint32_t)*L.big_n;   // leaves passed on by k_wleafw
     const uint64_t lt = mrg_lanemask_lt();
     const GASW v2 *kin = reinterpret_cast<const GASW v2 *>(gw(L.kin));
     unsigned long long wg_keys = 0;   // distinct keys of this workgroup's leaves (thread 0)
@@ -530,33 +530,201 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
 #else
 #define WP(i)
 #endif
-    auto leaf_range = [&](uint32_t j, uint64_t &lo, uint64_t &hi) {
-        const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + j;
+    auto leaf_at = [&](uint32_t i, uint64_t &lid, uint64_t &lo, uint64_t &hi) {
+        lid = L.big_list[i];
+        const uint32_t b = (uint32_t)(lid / MRG_WIDE_MAXB2), j = (uint32_t)(lid % MRG_WIDE_MAXB2);
         lo = L.leaf_lo[lid];
-        hi = j + 1 < nl ? L.leaf_lo[lid + 1] : bend;
+        hi = j + 1 < L.nleaf[b] ? L.leaf_lo[lid + 1] : L.bstart[b + 1];
     };
     // first W_PF * W_LWG records of leaf j into registers (a record past the leaf: a repeat, unused)
-    v2 pf[W_PF];
-    auto prefetch = [&](uint32_t j) {
-        if (j >= nl) return;
-        uint64_t lo, hi;
-        leaf_range(j, lo, hi);
+    v2 pf[W_PF], pff = v2{0, 0};   // pff: the leaf's first record (the same in every thread)
+#pragma unroll
+    for (int u = 0; u < W_PF; ++u) pf[u] = v2{0, 0};
+    auto prefetch = [&](uint32_t i) {
+        if (i >= nlist) return;
+        uint64_t lid, lo, hi;
+        leaf_at(i, lid, lo, hi);
         if (hi == lo) return;
 #pragma unroll
         for (int u = 0; u < W_PF; ++u) pf[u] = kin[lo + min((uint64_t)(tid + u * W_LWG), hi - lo - 1u)];
+        pff = kin[lo];
     };
-    prefetch(0);
-    for (uint32_t j = 0; j < nl; ++j) {
-        const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + j;
-        uint64_t mlo, mhi;
-        leaf_range(j, mlo, mhi);
+    prefetch(blockIdx.x);
+    if (tid == 0) {
+        s_or0 = 0;
+        s_or1 = 0;
+        s_maxb = 0;
+        s_bytes = 0;
+    }
+    for (uint32_t i = tid; i < W_NDIG; i += W_LWG) s_dcnt[i] = 0;
+    lds_barrier();
+    for (uint32_t i = blockIdx.x; i < nlist; i += gridDim.x) {
+        uint64_t lid, mlo, mhi;
+        leaf_at(i, lid, mlo, mhi);
         const uint64_t wlo = L.wr[2 * lid], whi = L.wr[2 * lid + 1];
         const uint64_t nm = mhi - mlo, nwk = whi - wlo;
         const uint64_t out0 = mlo + wlo;
         v2 cur[W_PF];
 #pragma unroll
         for (int u = 0; u < W_PF; ++u) cur[u] = pf[u];
-        prefetch(j + 1);   // in flight while this leaf is processed
+        const v2 f = pff;
+        prefetch(i + gridDim.x);   // in flight while this leaf is processed
+        const uint64_t NT = nm + nwk;
+        GASW v2 *ko = reinterpret_cast<GASW v2 *>(gw(L.kout)) + out0;
+        GASW uint64_t *co = gw(L.ocnt) + out0;
+        if (NT <= L.maxd) {
+            // ---- sort-then-combine (no hash table): every record is an item held in registers; the
+            // items are bucketed by the W_DBITS key bits after the leaf's common prefix (a counting
+            // sort), ranked inside their bucket by comparisons (equal keys by bucket slot), and the runs
+            // of equal keys of the sorted leaf are summed into its distinct keys.  s_dcnt is zero and
+            // s_or*, s_maxb, s_bytes are 0 on entry (cleared by the previous leaf).
+            v2 key[W_LR];
+            uint64_t cnt[W_LR];
+            uint64_t o0 = 0, o1 = 0;
+            // f: one reference key for the whole workgroup (the leaf's first record).  The keys agree
+            // on every bit above the first set bit of OR(key ^ f), so the digit taken from there orders
+            // them; with f a member that bit is exactly the first one the keys differ on.
+#pragma unroll
+            for (uint32_t k = 0; k < W_LR; ++k) {
+                const uint64_t p = (uint64_t)k * W_LWG + tid;
+                cnt[k] = 0;
+                key[k] = f;
+                if (p < nm) {
+                    key[k] = cur[k];
+                    cnt[k] = 1;
+                } else if (p < NT) {
+                    key[k] = v2{L.wk0[wlo + p - nm], L.wk1[wlo + p - nm]};
+                    cnt[k] = L.wcnt[wlo + p - nm];
+                }
+                o0 |= key[k].x ^ f.x;
+                o1 |= key[k].y ^ f.y;
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                o0 |= __shfl_xor(o0, o);
+                o1 |= __shfl_xor(o1, o);
+            }
+            if (lane == 0 && (o0 | o1)) {
+                atomicOr((unsigned long long *)&s_or0, (unsigned long long)o0);
+                atomicOr((unsigned long long *)&s_or1, (unsigned long long)o1);
+            }
+            lds_barrier();
+            WP(0);
+            const uint64_t r0 = s_or0, r1 = s_or1;
+            uint32_t hb = r0 ? (uint32_t)__builtin_clzll(r0) : (r1 ? 64u + (uint32_t)__builtin_clzll(r1) : 0u);
+            if (hb > 128u - W_DBITS) hb = 128u - W_DBITS;
+            uint32_t dg[W_LR], within[W_LR];
+#pragma unroll
+            for (uint32_t k = 0; k < W_LR; ++k) {
+                const uint64_t p = (uint64_t)k * W_LWG + tid;
+                dg[k] = 0xFFFFFFFFu;
+                if (p < NT) {
+                    dg[k] = key_digit(key[k].x, key[k].y, hb);
+                    within[k] = atomicAdd(&s_dcnt[dg[k]], 1u);
+                }
+            }
+            lds_barrier();
+            {
+                constexpr uint32_t PT = W_NDIG / W_LWG;
+                uint32_t v[PT], sum = 0, mx = 0;
+#pragma unroll
+                for (uint32_t x = 0; x < PT; ++x) {
+                    v[x] = s_dcnt[tid * PT + x];
+                    sum += v[x];
+                    mx = max(mx, v[x]);
+                }
+                if (mx > W_MAXBKT) atomicMax(&s_maxb, mx);
+                uint32_t tot;
+                uint32_t run = block_scan_excl<W_LNW>(sum, s_ws, &tot);
+#pragma unroll
+                for (uint32_t x = 0; x < PT; ++x) {
+                    s_doff[tid * PT + x] = (uint16_t)run;
+                    run += v[x];
+                }
+            }
+            lds_barrier();
+            WP(1);
+            const bool small = s_maxb == 0;
+            if (small) {
+#pragma unroll
+                for (uint32_t k = 0; k < W_LR; ++k)
+                    if (dg[k] != 0xFFFFFFFFu) s_kb[s_doff[dg[k]] + within[k]] = key[k];
+                lds_barrier();
+#pragma unroll
+                for (uint32_t k = 0; k < W_LR; ++k) {
+                    if (dg[k] == 0xFFFFFFFFu) continue;
+                    const uint32_t bs = s_doff[dg[k]], bn = s_dcnt[dg[k]];
+                    uint32_t rank = 0;
+                    for (uint32_t q = 0; q < bn; ++q) {
+                        const v2 x = s_kb[bs + q];
+                        rank += (key_lt(x.x, x.y, key[k].x, key[k].y) ||
+                                 (x.x == key[k].x && x.y == key[k].y && q < within[k])) ? 1u : 0u;
+                    }
+                    s_kc[bs + rank] = key[k];
+                    s_cc[bs + rank] = cnt[k];
+                }
+                lds_barrier();
+                WP(2);
+                for (uint32_t i = tid; i < W_NDIG; i += W_LWG) s_dcnt[i] = 0;   // for the next leaf
+                // runs of equal keys: thread t owns sorted items [W_LR t, W_LR t + W_LR)
+                const uint32_t p0 = tid * W_LR;
+                bool head[W_LR];
+                uint32_t nh = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < W_LR; ++k) {
+                    const uint32_t p = p0 + k;
+                    head[k] = false;
+                    if (p < NT) {
+                        head[k] = p == 0;
+                        if (p) {
+                            const v2 a = s_kc[p - 1], c = s_kc[p];
+                            head[k] = a.x != c.x || a.y != c.y;
+                        }
+                    }
+                    nh += head[k] ? 1u : 0u;
+                }
+                uint32_t D;
+                uint32_t dpos = block_scan_excl<W_LNW>(nh, s_ws, &D);
+                WP(3);
+                uint64_t bytes = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < W_LR; ++k) {
+                    if (!head[k]) continue;
+                    const uint32_t p = p0 + k;
+                    const v2 x = s_kc[p];
+                    uint64_t n = s_cc[p];
+                    for (uint32_t q = p + 1; q < NT; ++q) {
+                        const v2 y = s_kc[q];
+                        if (y.x != x.x || y.y != x.y) break;
+                        n += s_cc[q];
+                    }
+                    ko[dpos] = x;
+                    co[dpos] = n;
+                    const uint32_t ll = line_len(x.x, x.y, n);
+                    bytes += ll;
+                    if (dpos == D - 1) L.leaf_last[lid] = ll;
+                    ++dpos;
+                }
+                for (int o = 32; o > 0; o >>= 1) bytes += __shfl_xor(bytes, o);
+                if (lane == 0 && bytes) atomicAdd((unsigned long long *)&s_bytes, (unsigned long long)bytes);
+                lds_barrier();
+                if (tid == 0) {
+                    L.leaf_out[lid] = out0;
+                    L.leaf_nd[lid] = D;
+                    L.leaf_bytes[lid] = s_bytes;
+                    if (D == 0) L.leaf_last[lid] = 0;
+                    wg_keys += D;
+                    s_or0 = 0;
+                    s_or1 = 0;
+                    s_bytes = 0;
+                }
+                lds_barrier();
+                WP(4);
+                continue;
+            }
+            // a bucket too large to rank by comparisons (many equal keys): the hash path below, once
+            // every wave has read s_maxb
+            lds_barrier();
+        }
         // table size: a power of two >= 2 x records (a leaf of duplicates still fits: distinct counts)
         uint32_t S = 64;
         while (S < W_SLOTS && (uint64_t)S < 2 * (nm + nwk)) S <<= 1;
@@ -622,7 +790,12 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
                 L.leaf_nd[lid] = 0;
                 L.leaf_bytes[lid] = 0;
                 L.leaf_last[lid] = 0;
+                s_or0 = 0;
+                s_or1 = 0;
+                s_maxb = 0;
+                s_bytes = 0;
             }
+            for (uint32_t i = tid; i < W_NDIG; i += W_LWG) s_dcnt[i] = 0;
             lds_barrier();
             continue;
         }
@@ -714,8 +887,6 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
         }
         lds_barrier();
         WP(3);
-        GASW v2 *ko = reinterpret_cast<GASW v2 *>(gw(L.kout)) + out0;
-        GASW uint64_t *co = gw(L.ocnt) + out0;
         uint64_t bytes = 0;
         if (s_maxb == 0) {
             // ---- keys in bucket order, then rank = keys of the same bucket that are smaller
@@ -757,7 +928,9 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
                 for (uint32_t i = tid; i < NR * W_LNW * 256; i += W_LWG) s_wc[i] = 0;
                 lds_barrier();
                 uint32_t rk[W_LR];
-                for (uint32_t k = 0; k < NR; ++k) {
+#pragma unroll
+                for (uint32_t k = 0; k < W_LR; ++k) {
+                    if (k >= NR) break;
                     const uint32_t p = k * W_LWG + tid;
                     const bool valid = p < D;
                     uint32_t d = 0;
@@ -780,19 +953,23 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
                     const uint32_t C = 256u * NR * W_LNW, per = C / W_LWG;
                     uint32_t v[4 * W_LR];
                     uint32_t sum = 0;
-                    for (uint32_t x = 0; x < per; ++x) {
-                        v[x] = s_wc[tid * per + x];
+#pragma unroll
+                    for (uint32_t x = 0; x < 4 * W_LR; ++x) {
+                        v[x] = x < per ? s_wc[tid * per + x] : 0u;
                         sum += v[x];
                     }
                     uint32_t tot;
                     uint32_t run = block_scan_excl<W_LNW>(sum, s_ws, &tot);
-                    for (uint32_t x = 0; x < per; ++x) {
-                        s_wc[tid * per + x] = (uint16_t)run;
+#pragma unroll
+                    for (uint32_t x = 0; x < 4 * W_LR; ++x) {
+                        if (x < per) s_wc[tid * per + x] = (uint16_t)run;
                         run += v[x];
                     }
                 }
                 lds_barrier();
-                for (uint32_t k = 0; k < NR; ++k) {
+#pragma unroll
+                for (uint32_t k = 0; k < W_LR; ++k) {
+                    if (k >= NR) break;
                     const uint32_t p = k * W_LWG + tid;
                     if (rk[k] != 0xFFFFFFFFu) dst[s_wc[(dg[k] * NR + k) * W_LNW + wv] + rk[k]] = src[p];
                 }
@@ -822,7 +999,12 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
             L.leaf_bytes[lid] = s_bytes;
             if (D == 0) L.leaf_last[lid] = 0;
             wg_keys += D;
+            s_or0 = 0;
+            s_or1 = 0;
+            s_maxb = 0;
+            s_bytes = 0;
         }
+        for (uint32_t i = tid; i < W_NDIG; i += W_LWG) s_dcnt[i] = 0;
         lds_barrier();
         WP(5);
     }
@@ -832,6 +1014,273 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
 #endif
     // one device-scope add per workgroup (a per-leaf add on one word would serialise ~2.7 M adds)
     if (tid == 0 && wg_keys) atomicAdd(L.nkeys, wg_keys);
+}
+
+// ---------------------------------------------------------------- leaves, one wave each
+// The common case: a leaf of at most W_VC items (records + weighted keys) is finished by ONE wave,
+// wave-synchronously (LDS traffic inside a wave is ordered; no workgroup barrier), so a CU keeps
+// eight independent leaves in flight.  Items sit in registers (W_VIPL per lane).
+//   digit   bit hb = the first bit the leaf's keys differ on splits them into two sides; inside
+//           each side the keys agree above that side's own first differing bit hs, so
+//           digit = side : the 8 key bits from hs  orders the keys (a window from hb alone collapses
+//           when the leaf straddles a carry such as '9' -> 'a' or 'o' -> 'p').
+//   order   counting sort of the items by digit in LDS, then each item's rank inside its (small)
+//           bucket by comparisons (equal keys by bucket slot);
+//   runs    the sorted order is walked once: each run of equal keys becomes one distinct key, stored
+//           with its summed count at leaf_out + its rank among the distinct keys (stores coalesced).
+// Leaves with more items, or with a bucket of more than W_VMAXB items, are listed for k_wleaf.
+constexpr uint32_t W_VC = 576;
+constexpr uint32_t W_VIPL = W_VC / 64;
+constexpr uint32_t W_VND = 512;         // digits: side bit + 8 key bits
+constexpr uint32_t W_VMAXB = 64;
+constexpr uint32_t W_VQ = 4;            // waves (one-wave workgroups) per L1 bucket
+constexpr uint32_t W_VPASS = MRG_WIDE_MAXB2 / W_VQ;   // leaves one wave may pass on
+
+__device__ __forceinline__ void wave_lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ uint32_t first_bit(uint64_t o0, uint64_t o1) {   // 128 if none
+    return o0 ? (uint32_t)__builtin_clzll(o0) : (o1 ? 64u + (uint32_t)__builtin_clzll(o1) : 128u);
+}
+__device__ __forceinline__ uint32_t key_bit(uint64_t k0, uint64_t k1, uint32_t hb) {
+    return hb < 64 ? (uint32_t)(k0 >> (63u - hb)) & 1u : (uint32_t)(k1 >> (127u - hb)) & 1u;
+}
+__device__ __forceinline__ uint64_t wave_or(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
+    return v;
+}
+
+__global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
+    typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+    __shared__ v2 s_kb[W_VC];            // items in digit-bucket order
+    __shared__ uint64_t s_cb[W_VC];      // their counts
+    __shared__ uint16_t s_ix[W_VC];      // sorted position -> bucket slot
+    __shared__ uint32_t s_dc[W_VND];     // digit counts
+    __shared__ uint16_t s_ds[W_VND];     // digit starts
+    __shared__ uint32_t s_pass[W_VPASS]; // leaves passed on to k_wleaf
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x / W_VQ, q0 = blockIdx.x % W_VQ;
+    const uint32_t nl = L.nleaf[b];
+    const uint64_t bend = L.bstart[b + 1];
+    const uint32_t cap = min(L.maxd, W_VC);
+    const uint64_t lt = mrg_lanemask_lt();
+    const GASW v2 *kin = reinterpret_cast<const GASW v2 *>(gw(L.kin));
+    GASW v2 *kout = reinterpret_cast<GASW v2 *>(gw(L.kout));
+    GASW uint64_t *cout = gw(L.ocnt);
+    unsigned long long keys = 0;
+    uint32_t npass = 0;
+    for (uint32_t j = q0; j < nl; j += W_VQ) {
+        const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + j;
+        const uint64_t mlo = L.leaf_lo[lid], mhi = j + 1 < nl ? L.leaf_lo[lid + 1] : bend;
+        const uint64_t wlo = L.wr[2 * lid], whi = L.wr[2 * lid + 1];
+        const uint64_t nm = mhi - mlo, NT = nm + (whi - wlo);
+        if (NT > cap) {
+            if (lane == 0) s_pass[npass] = (uint32_t)lid;
+            ++npass;
+#ifdef MRG_WIDE_PROF
+            if (lane == 0) atomicAdd(&L.prof[6], 1ull);
+#endif
+            continue;
+        }
+        const uint64_t out0 = mlo + wlo;
+        GASW v2 *ko = kout + out0;
+        GASW uint64_t *co = cout + out0;
+        v2 key[W_VIPL];
+        uint64_t cnt[W_VIPL];
+#pragma unroll
+        for (uint32_t k = 0; k < W_VIPL; ++k) {
+            const uint64_t p = (uint64_t)k * 64u + lane;
+            key[k] = v2{0, 0};
+            cnt[k] = 0;
+            if (p < nm) {
+                key[k] = kin[mlo + p];
+                cnt[k] = 1;
+            } else if (p < NT) {
+                key[k] = v2{L.wk0[wlo + p - nm], L.wk1[wlo + p - nm]};
+                cnt[k] = L.wcnt[wlo + p - nm];
+            }
+        }
+        const v2 f = v2{__shfl(key[0].x, 0), __shfl(key[0].y, 0)};   // item 0 (a member if NT > 0)
+        uint64_t o0 = 0, o1 = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < W_VIPL; ++k) {
+            if ((uint64_t)k * 64u + lane >= NT) key[k] = f;   // padding: f's twin, never stored
+            o0 |= key[k].x ^ f.x;
+            o1 |= key[k].y ^ f.y;
+        }
+        o0 = wave_or(o0);
+        o1 = wave_or(o1);
+        const uint32_t hb = first_bit(o0, o1);
+        uint32_t D = 0, my_last = 0xFFFFFFFFu, my_ll = 0;
+        uint64_t bytes = 0;
+        if (hb == 128u) {   // every item has the same key (or none): one line
+            uint64_t n = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < W_VIPL; ++k) n += cnt[k];
+            for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+            if (NT) {
+                D = 1;
+                my_ll = line_len(f.x, f.y, n);
+                if (lane == 0) {
+                    ko[0] = f;
+                    co[0] = n;
+                    my_last = 0;
+                    bytes = my_ll;
+                }
+            }
+        } else {
+            // the other side's reference: the first item whose bit hb differs from f's
+            const uint32_t sf = key_bit(f.x, f.y, hb);
+            v2 g = f;
+            bool found = false;
+#pragma unroll
+            for (uint32_t k = 0; k < W_VIPL; ++k) {
+                const uint64_t m = __ballot(key_bit(key[k].x, key[k].y, hb) != sf);
+                if (m && !found) {
+                    const int src = __ffsll((long long)m) - 1;
+                    g = v2{__shfl(key[k].x, src), __shfl(key[k].y, src)};
+                    found = true;
+                }
+            }
+            uint64_t a0 = 0, a1 = 0, c0 = 0, c1 = 0;   // OR (key ^ reference) of side sf, of the other side
+#pragma unroll
+            for (uint32_t k = 0; k < W_VIPL; ++k) {
+                if (key_bit(key[k].x, key[k].y, hb) == sf) {
+                    a0 |= key[k].x ^ f.x;
+                    a1 |= key[k].y ^ f.y;
+                } else {
+                    c0 |= key[k].x ^ g.x;
+                    c1 |= key[k].y ^ g.y;
+                }
+            }
+            a0 = wave_or(a0);
+            a1 = wave_or(a1);
+            c0 = wave_or(c0);
+            c1 = wave_or(c1);
+            const uint32_t hf = min(first_bit(a0, a1), 120u), hg = min(first_bit(c0, c1), 120u);
+            for (uint32_t i = lane; i < W_VND; i += 64) s_dc[i] = 0;
+            wave_lds_sync();
+            uint32_t dg[W_VIPL], wi[W_VIPL];
+#pragma unroll
+            for (uint32_t k = 0; k < W_VIPL; ++k) {
+                dg[k] = 0xFFFFFFFFu;
+                wi[k] = 0;
+                if ((uint64_t)k * 64u + lane < NT) {
+                    const uint32_t sd = key_bit(key[k].x, key[k].y, hb);
+                    const uint32_t hs = sd == sf ? hf : hg;
+                    const uint64_t t = hs == 0 ? key[k].x
+                                       : (hs < 64 ? (key[k].x << hs) | (key[k].y >> (64 - hs)) : key[k].y << (hs - 64));
+                    dg[k] = (sd << 8) | (uint32_t)(t >> 56);
+                    wi[k] = atomicAdd(&s_dc[dg[k]], 1u);
+                }
+            }
+            wave_lds_sync();
+            uint32_t mx = 0;
+            {
+                constexpr uint32_t PT = W_VND / 64;
+                uint32_t v[PT], sum = 0;
+#pragma unroll
+                for (uint32_t x = 0; x < PT; ++x) {
+                    v[x] = s_dc[lane * PT + x];
+                    sum += v[x];
+                    mx = max(mx, v[x]);
+                }
+                uint32_t run = wave_scan_incl(sum) - sum;
+#pragma unroll
+                for (uint32_t x = 0; x < PT; ++x) {
+                    s_ds[lane * PT + x] = (uint16_t)run;
+                    run += v[x];
+                }
+                for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
+            }
+            if (mx > W_VMAXB) {   // many equal (or near-equal) keys: the workgroup kernel
+                if (lane == 0) s_pass[npass] = (uint32_t)lid;
+                ++npass;
+#ifdef MRG_WIDE_PROF
+                if (lane == 0) atomicAdd(&L.prof[7], 1ull);
+#endif
+                wave_lds_sync();
+                continue;
+            }
+            wave_lds_sync();
+            uint32_t slot[W_VIPL];
+#pragma unroll
+            for (uint32_t k = 0; k < W_VIPL; ++k) {
+                slot[k] = 0;
+                if (dg[k] == 0xFFFFFFFFu) continue;
+                slot[k] = s_ds[dg[k]] + wi[k];
+                s_kb[slot[k]] = key[k];
+                s_cb[slot[k]] = cnt[k];
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (uint32_t k = 0; k < W_VIPL; ++k) {
+                if (dg[k] == 0xFFFFFFFFu) continue;
+                const uint32_t bs = s_ds[dg[k]], bn = s_dc[dg[k]];
+                uint32_t rank = 0;
+                for (uint32_t q = 0; q < bn; ++q) {
+                    const v2 x = s_kb[bs + q];
+                    rank += (key_lt(x.x, x.y, key[k].x, key[k].y) ||
+                             (x.x == key[k].x && x.y == key[k].y && q < wi[k])) ? 1u : 0u;
+                }
+                s_ix[bs + rank] = (uint16_t)slot[k];
+            }
+            wave_lds_sync();
+            // runs of equal keys in sorted order (position p = k * 64 + lane)
+#pragma unroll
+            for (uint32_t k = 0; k < W_VIPL; ++k) {
+                const uint32_t p = k * 64u + lane;
+                bool head = false;
+                v2 x = v2{0, 0};
+                uint32_t sl = 0;
+                if (p < NT) {
+                    sl = s_ix[p];
+                    x = s_kb[sl];
+                    head = p == 0;
+                    if (p) {
+                        const v2 y = s_kb[s_ix[p - 1]];
+                        head = y.x != x.x || y.y != x.y;
+                    }
+                }
+                const uint64_t hm = __ballot(head);
+                if (head) {
+                    const uint32_t dpos = D + (uint32_t)__popcll(hm & lt);
+                    uint64_t n = s_cb[sl];
+                    for (uint32_t q = p + 1; q < NT; ++q) {
+                        const uint32_t s2 = s_ix[q];
+                        const v2 y = s_kb[s2];
+                        if (y.x != x.x || y.y != x.y) break;
+                        n += s_cb[s2];
+                    }
+                    ko[dpos] = x;
+                    co[dpos] = n;
+                    my_ll = line_len(x.x, x.y, n);
+                    bytes += my_ll;
+                    my_last = dpos;
+                }
+                D += (uint32_t)__popcll(hm);
+            }
+        }
+        if (D && my_last == D - 1) L.leaf_last[lid] = my_ll;
+        for (int o = 32; o > 0; o >>= 1) bytes += __shfl_xor(bytes, o);
+        if (lane == 0) {
+            L.leaf_out[lid] = out0;
+            L.leaf_nd[lid] = D;
+            L.leaf_bytes[lid] = bytes;
+            if (D == 0) L.leaf_last[lid] = 0;
+        }
+        keys += D;
+        wave_lds_sync();
+    }
+    // the passed-on leaves, with one device atomic per wave
+    if (npass) {
+        wave_lds_sync();
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(L.big_n, (unsigned long long)npass);
+        base = __shfl(base, 0);
+        for (uint32_t i = lane; i < npass; i += 64) L.big_list[base + i] = s_pass[i];
+    }
+    if (lane == 0 && keys) atomicAdd(L.nkeys, keys);
 }
 
 // last-group drop (worker.rs:169-184): the last key of the last non-empty leaf of partition r
@@ -1139,15 +1588,17 @@ void mrg_wide_launch_weights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *
 void mrg_wide_launch_leaf(const WideLeafArgs &w, uint32_t B1, hipStream_t s) {
     LeafArgs L{w.kin, w.kout, w.bstart, w.nleaf, w.leaf_lo, w.leaf_lb, w.B1r, w.R, w.wk0, w.wk1, w.wcnt, w.wpart, w.nw,
                w.maxd ? min(w.maxd, W_MAXD) : W_MAXD, w.ocnt, w.leaf_out, w.leaf_nd, w.leaf_bytes, w.leaf_last, w.ovf_list,
-               w.ovf_n, w.nkeys, w.wr, w.prof};
+               w.ovf_n, w.nkeys, w.wr, w.prof, w.big_list, w.big_n};
     hipLaunchKernelGGL(k_wranges, gridw((uint64_t)B1 * MRG_WIDE_MAXB2), dim3(256), 0, s, L, B1);
-    hipLaunchKernelGGL(k_wleaf, dim3(B1), dim3(W_LWG), 0, s, L);
+    hipLaunchKernelGGL(k_wleafw, dim3(B1 * W_VQ), dim3(64), 0, s, L);
+    // the passed-on leaves: a fixed grid loops over the list (its length is read on the device)
+    hipLaunchKernelGGL(k_wleaf, dim3(B1 < 2048u ? B1 : 2048u), dim3(W_LWG), 0, s, L);
 }
 void mrg_wide_launch_fallback(const WideLeafArgs &w, const uint32_t *list, uint32_t nlist, DevPool &pool,
                               hipStream_t s) {
     LeafArgs L{w.kin, w.kout, w.bstart, w.nleaf, w.leaf_lo, w.leaf_lb, w.B1r, w.R, w.wk0, w.wk1, w.wcnt, w.wpart, w.nw,
                w.maxd ? min(w.maxd, W_MAXD) : W_MAXD, w.ocnt, w.leaf_out, w.leaf_nd, w.leaf_bytes, w.leaf_last, w.ovf_list,
-               w.ovf_n, w.nkeys, w.wr, w.prof};
+               w.ovf_n, w.nkeys, w.wr, w.prof, w.big_list, w.big_n};
     uint64_t *wrange = (uint64_t *)pool.get(16ull * nlist);
     uint64_t *cnt = (uint64_t *)pool.get(8ull * (nlist + 1)), *off = (uint64_t *)pool.get(8ull * (nlist + 1));
     uint64_t *scantmp = (uint64_t *)pool.get(8ull * mrg_scan_tmp_elems(nlist + 1));

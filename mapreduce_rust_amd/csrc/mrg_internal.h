@@ -270,6 +270,8 @@ struct WideLeafArgs {
     unsigned long long *nkeys;   // += distinct keys of every finished leaf
     uint64_t *wr;                // [B1 * MRG_WIDE_MAXB2][2] scratch: weighted-key range of each leaf
     unsigned long long *prof;    // diagnostics (builds with -DMRG_WIDE_PROF): leaf phase clocks [8]
+    uint32_t *big_list;          // [B1 * MRG_WIDE_MAXB2] leaves passed from the one-wave to the workgroup kernel
+    unsigned long long *big_n;   // their count (zeroed by the caller)
 };
 void mrg_wide_launch_counts(const BucketArgs &a, uint64_t *cnt_main, uint64_t *segptr, uint64_t *cnt_flush,
                             hipStream_t s);

@@ -642,7 +642,7 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     uint64_t *K2 = pget<uint64_t>(p, 2 * n + 2);
     uint32_t *nleaf = pget<uint32_t>(p, B1);
     uint64_t *leaf_lo = pget<uint64_t>(p, NL + 1), *leaf_lb = pget<uint64_t>(p, 2 * NL + 2);
-    const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", 384);
+    const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", 300);
     mrg_wide_launch_l2(K1, K2, bstart, spl1, B1, B1r, target, nleaf, leaf_lo, leaf_lb, s);
     mark();  // 4: L2
     // ---- leaves: aggregate + sort + line bytes (K1 becomes the output key array)
@@ -671,6 +671,9 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     L.wr = pget<uint64_t>(p, 2 * NL);
     L.prof = pget<unsigned long long>(p, 8);
     HIPCHK(hipMemsetAsync(L.prof, 0, 64, s));
+    L.big_list = pget<uint32_t>(p, NL);
+    L.big_n = pget<unsigned long long>(p, 1);
+    HIPCHK(hipMemsetAsync(L.big_n, 0, 8, s));
     mrg_wide_launch_leaf(L, B1, s);
     mark();  // 5: leaves
     read_counters(c);
@@ -690,8 +693,30 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
         }
         fprintf(stderr, "\n");
         for (int i = 0; i < npe; ++i) (void)hipEventDestroy(pe[i]);
-        unsigned long long pr[8];
+        unsigned long long pr[8], nbig = 0;
         HIPCHK(hipMemcpy(pr, L.prof, sizeof pr, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&nbig, L.big_n, 8, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[mrgpu] wide: %llu passed to the workgroup kernel (%llu by size, %llu by bucket)\n", nbig,
+                pr[6], pr[7]);
+        {  // leaf sizes (records)
+            std::vector<uint32_t> hn(B1);
+            std::vector<uint64_t> hlo(NL), hbs(B1 + 1);
+            HIPCHK(hipMemcpy(hn.data(), nleaf, 4ull * B1, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hlo.data(), leaf_lo, 8ull * NL, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hbs.data(), bstart, 8ull * (B1 + 1), hipMemcpyDeviceToHost));
+            std::vector<uint64_t> sz;
+            for (uint32_t bb = 0; bb < B1; ++bb)
+                for (uint32_t j = 0; j < hn[bb]; ++j) {
+                    const uint64_t lid = (uint64_t)bb * MRG_WIDE_MAXB2 + j;
+                    sz.push_back((j + 1 < hn[bb] ? hlo[lid + 1] : hbs[bb + 1]) - hlo[lid]);
+                }
+            std::sort(sz.begin(), sz.end());
+            if (!sz.empty())
+                fprintf(stderr, "[mrgpu] wide: %zu leaves, records p10 %llu p50 %llu p63 %llu p87 %llu p99 %llu max %llu\n",
+                        sz.size(), (unsigned long long)sz[sz.size() / 10], (unsigned long long)sz[sz.size() / 2],
+                        (unsigned long long)sz[sz.size() * 63 / 100], (unsigned long long)sz[sz.size() * 87 / 100],
+                        (unsigned long long)sz[sz.size() * 99 / 100], (unsigned long long)sz.back());
+        }
         if (pr[0] | pr[1] | pr[5])
             fprintf(stderr, "[mrgpu] leaf phase clocks (wave 0, all WGs): clear %.3g insert %.3g list %.3g digits %.3g "
                             "order %.3g write %.3g\n", (double)pr[0], (double)pr[1], (double)pr[2], (double)pr[3],
@@ -702,7 +727,7 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
                 (unsigned long long)n, (unsigned long long)nw, B1, B1r, (unsigned long long)w.distinct,
                 (unsigned long long)novf);
     p.put(K2); p.put(leaf_lo); p.put(leaf_lb); p.put(ovf_list); p.put(spl1); p.put(bstart); p.put(L.wr);
-    p.put(L.prof);
+    p.put(L.prof); p.put(L.big_list); p.put(L.big_n);
     p.put(wk0); p.put(wk1); p.put(wcnt); p.put(wpart);
     c->st.overflow_keys = novf;
     c->keys.n = 0;
