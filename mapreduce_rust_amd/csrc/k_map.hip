@@ -558,6 +558,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // offset field of ds_read, so a lookup needs no separate address add
     __shared__ __attribute__((aligned(2048))) uint16_t s_lut[128];  // ASCII class: W | S << 8
     __shared__ __attribute__((aligned(1024))) uint32_t s_zm[17][4];  // key-length byte masks
+    // v_perm selectors per (key length, 1-byte gap position; 16 = none) over the r-aligned window
+    __shared__ __attribute__((aligned(16))) uint32_t s_sel[17 * 17][4];
     // workgroup: combine table + tail-region cursors
     __shared__ KeyPair s_key[CAP];
     __shared__ unsigned int s_cnt[CAP];
@@ -595,12 +597,19 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const uint32_t c = mrg_uclass((uint32_t)tid);
         s_lut[tid] = (uint16_t)((c == MRG_CLS_W ? 1u : 0u) | (c == MRG_CLS_S ? 0x100u : 0u));
     }
-    if (tid < 17 * 4) {  // word j, byte p (p = 0 least significant) holds key byte 4j + 3 - p
-        const uint32_t L = (uint32_t)tid >> 2, j = (uint32_t)tid & 3u;
+    auto zmask = [](uint32_t L, uint32_t j) {  // word j, byte p (p = 0 least significant) holds key byte 4j + 3 - p
         uint32_t m = 0;
         for (uint32_t p = 0; p < 4; ++p)
             if (4u * j + 3u - p >= L) m |= 0xFFu << (8u * p);
-        s_zm[L][j] = m;
+        return m;
+    };
+    if (tid < 17 * 4) s_zm[tid >> 2][tid & 3] = zmask((uint32_t)tid >> 2, (uint32_t)tid & 3u);
+    for (int i = tid; i < 17 * 17 * 4; i += WG) {
+        // key byte 4j + 3 - p comes from aligned-window byte 4j + 3 - p (+ 1 from the gap on); bytes
+        // at or past the key length select the constant 0 (v_perm selector 0x0C)
+        const uint32_t L = (uint32_t)i / 68u, g = ((uint32_t)i / 4u) % 17u, j = (uint32_t)i & 3u;
+        const uint32_t zm = zmask(L, j), gm = zmask(g, j);
+        s_sel[L * 17u + g][j] = ((0x00010203u + (gm & 0x01010101u)) & ~zm) | (0x0C0C0C0Cu & zm);
     }
     LdsTable<CAP, IDX> table{s_key, s_cnt, s_doc, s_door};
     uint32_t my_tokens = 0;
@@ -830,16 +839,15 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 const uint32_t dw = off >> 2, r = off & 3u;
                 const uint32_t d0 = win32[dw], d1 = win32[dw + 1], d2 = win32[dw + 2], d3 = win32[dw + 3],
                                d4 = win32[dw + 4];
-                const uint32_t *zm = s_zm[fast ? tlen : 0u];
-                const uint32_t *gm = s_zm[ga];
-                const uint32_t bsel = 0x00010203u + __builtin_amdgcn_perm(0u, r, 0u);  // + r in every byte
-                auto sel = [&](int j) {
-                    return ((bsel + (gm[j] & 0x01010101u)) & ~zm[j]) | (0x0C0C0C0Cu & zm[j]);
-                };
-                const uint32_t o0 = __builtin_amdgcn_perm(d1, d0, sel(0));
-                const uint32_t o1 = __builtin_amdgcn_perm(d2, d1, sel(1));
-                const uint32_t o2 = __builtin_amdgcn_perm(d3, d2, sel(2));
-                const uint32_t o3 = __builtin_amdgcn_perm(d4, d3, sel(3));
+                // the window aligned to the key's first byte, then one selector word per output word
+                const u32x4 sl = *reinterpret_cast<const u32x4 *>(s_sel[(fast ? tlen : 0u) * 17u + ga]);
+                const uint32_t a0 = __builtin_amdgcn_alignbyte(d1, d0, r), a1 = __builtin_amdgcn_alignbyte(d2, d1, r),
+                               a2 = __builtin_amdgcn_alignbyte(d3, d2, r), a3 = __builtin_amdgcn_alignbyte(d4, d3, r),
+                               a4 = __builtin_amdgcn_alignbyte(0u, d4, r);
+                const uint32_t o0 = __builtin_amdgcn_perm(a1, a0, sl.x);
+                const uint32_t o1 = __builtin_amdgcn_perm(a2, a1, sl.y);
+                const uint32_t o2 = __builtin_amdgcn_perm(a3, a2, sl.z);
+                const uint32_t o3 = __builtin_amdgcn_perm(a4, a3, sl.w);
                 tk0 = ((uint64_t)o0 << 32) | o1;
                 tk1 = ((uint64_t)o2 << 32) | o3;
                 return one_gap ? 0u : gaps;  // gaps still to squeeze out
