@@ -28,7 +28,7 @@ constexpr int BA_WG = 1024;
 constexpr int BA_NW = BA_WG / 64;
 constexpr int BA_CAP = MRG_BA_CAP;
 constexpr int BA_PROBE = 64;
-constexpr int BA_U = 4;            // records per lane per chunk
+constexpr int BA_U = 8;            // records per lane per chunk
 constexpr int BA_MAXREG = 2048;    // map workgroups (regions) the per-region size table holds
 
 #define GASK __attribute__((address_space(1)))
