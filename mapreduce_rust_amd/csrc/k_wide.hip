@@ -80,7 +80,9 @@ __device__ __forceinline__ uint64_t seg_find(const OFF &off, uint64_t lo, uint64
 }
 
 __device__ __forceinline__ uint32_t part_of(uint64_t k0, uint64_t k1, uint32_t R) {
-    return (uint32_t)(mrg_siphash_short(k0, k1, mrg_short_len(k0, k1)) % (uint64_t)R);
+    const uint64_t h = mrg_siphash_short(k0, k1, mrg_short_len(k0, k1));
+    if ((R & (R - 1u)) == 0u) return (uint32_t)h & (R - 1u);   // uniform: no 64-bit division
+    return (uint32_t)(h % (uint64_t)R);
 }
 
 // number of splitters <= key among sp[0 .. m)
@@ -183,6 +185,7 @@ struct L1Args {
     uint32_t R, B1r, B1, ntiles;
     uint32_t *cnt;           // [B1][ntiles] (scanned in place between the two kernels)
     uint64_t *out;           // L1 output, 2 words per record
+    uint16_t *bid;           // [n] L1 bucket of each record: written by the counting pass, read by the scatter
 };
 
 // L1 tile t: records [t * T1, min(n, (t+1) * T1)); WITH_SCATTER: write them, else count them
@@ -233,17 +236,28 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl1(L1Args L) {
             k0[u] = x.x;
             k1[u] = x.y;
         }
+        uint32_t bk[U];
+        if (SCATTER) {   // the bucket the counting pass found (no SipHash, no splitter search again)
+#pragma unroll
+            for (int u = 0; u < U; ++u) bk[u] = gw(L.bid)[min(base + (uint64_t)u * W_WG, t1 - 1u)];
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (base + (uint64_t)u * W_WG >= t1) break;
-            const uint32_t r = part_of(k0[u], k1[u], L.R);
-            const uint32_t q = upper_idx(
-                [&](uint32_t x, uint64_t &a, uint64_t &b) {
-                    a = s_spl[2ull * (r * m + x)];
-                    b = s_spl[2ull * (r * m + x) + 1];
-                },
-                m, k0[u], k1[u]);
-            const uint32_t b = r * L.B1r + q;
+            uint32_t b;
+            if (SCATTER) {
+                b = bk[u];
+            } else {
+                const uint32_t r = part_of(k0[u], k1[u], L.R);
+                const uint32_t q = upper_idx(
+                    [&](uint32_t x, uint64_t &a, uint64_t &c) {
+                        a = s_spl[2ull * (r * m + x)];
+                        c = s_spl[2ull * (r * m + x) + 1];
+                    },
+                    m, k0[u], k1[u]);
+                b = r * L.B1r + q;
+                gw(L.bid)[base + (uint64_t)u * W_WG] = (uint16_t)b;
+            }
             const uint32_t pos = atomicAdd(&s_h[b], 1u);
             if (SCATTER) {
                 typedef uint64_t v2 __attribute__((ext_vector_type(2)));
@@ -1565,8 +1579,8 @@ size_t mrg_wide_l1_lds(uint32_t R, uint32_t B1r, uint32_t B1) {
 }
 void mrg_wide_launch_l1(const BucketArgs &a, const uint64_t *off, const uint64_t *segptr, uint64_t nseg, uint64_t n,
                         const uint64_t *spl1, uint32_t R, uint32_t B1r, uint32_t *cnt, uint32_t ntiles, uint64_t *out,
-                        bool scatter, hipStream_t s) {
-    L1Args L{a, off, segptr, nseg, n, spl1, R, B1r, R * B1r, ntiles, cnt, out};
+                        uint16_t *bid, bool scatter, hipStream_t s) {
+    L1Args L{a, off, segptr, nseg, n, spl1, R, B1r, R * B1r, ntiles, cnt, out, bid};
     const size_t lds = mrg_wide_l1_lds(R, B1r, R * B1r);
     if (scatter) hipLaunchKernelGGL(k_wl1<true>, dim3(ntiles), dim3(W_WG), lds, s, L);
     else hipLaunchKernelGGL(k_wl1<false>, dim3(ntiles), dim3(W_WG), lds, s, L);

@@ -628,9 +628,11 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     uint64_t *K1 = pget<uint64_t>(p, 2 * (n + nw) + 2);
     uint64_t *bstart = pget<uint64_t>(p, B1 + 1);
     if (n) {
-        mrg_wide_launch_l1(B, om, segptr, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, false, s);
+        uint16_t *bid = pget<uint16_t>(p, n);
+        mrg_wide_launch_l1(B, om, segptr, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, bid, false, s);
         mrg_scan_u32(cnt1, cnt1, (uint64_t)B1 * ntiles, st2, s);
-        mrg_wide_launch_l1(B, om, segptr, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, true, s);
+        mrg_wide_launch_l1(B, om, segptr, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, bid, true, s);
+        p.put(bid);
     } else {
         HIPCHK(hipMemsetAsync(cnt1, 0, 4ull * B1 * ntiles, s));
     }
