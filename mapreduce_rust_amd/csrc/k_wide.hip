@@ -1240,31 +1240,54 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
                 s_ix[bs + rank] = (uint16_t)slot[k];
             }
             wave_lds_sync();
-            // runs of equal keys in sorted order (position p = k * 64 + lane)
+            // runs of equal keys in sorted order (position p = k * 64 + lane): every position's key
+            // and count in registers first (independent reads); the previous / next position's key
+            // comes from the neighbour lane (lane 0 / 63: the last / first lane of row k - 1 / k + 1)
+            v2 xs[W_VIPL];
+            uint64_t cs[W_VIPL];
+            {
+                uint32_t sl[W_VIPL];
+#pragma unroll
+                for (uint32_t k = 0; k < W_VIPL; ++k) sl[k] = k * 64u + lane < NT ? s_ix[k * 64u + lane] : 0u;
+#pragma unroll
+                for (uint32_t k = 0; k < W_VIPL; ++k) {
+                    xs[k] = s_kb[sl[k]];
+                    cs[k] = s_cb[sl[k]];
+                }
+            }
+            bool head[W_VIPL];
 #pragma unroll
             for (uint32_t k = 0; k < W_VIPL; ++k) {
                 const uint32_t p = k * 64u + lane;
-                bool head = false;
-                v2 x = v2{0, 0};
-                uint32_t sl = 0;
-                if (p < NT) {
-                    sl = s_ix[p];
-                    x = s_kb[sl];
-                    head = p == 0;
-                    if (p) {
-                        const v2 y = s_kb[s_ix[p - 1]];
-                        head = y.x != x.x || y.y != x.y;
-                    }
+                // every lane takes part in every shuffle (a shuffle inside a branch reads inactive lanes)
+                const uint32_t kp = k > 0 ? k - 1 : 0;
+                const uint64_t z0 = __shfl(xs[kp].x, 63), z1 = __shfl(xs[kp].y, 63);
+                uint64_t y0 = __shfl_up(xs[k].x, 1), y1 = __shfl_up(xs[k].y, 1);
+                if (lane == 0) {
+                    y0 = z0;
+                    y1 = z1;
                 }
-                const uint64_t hm = __ballot(head);
-                if (head) {
+                head[k] = p < NT && (p == 0 || y0 != xs[k].x || y1 != xs[k].y);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < W_VIPL; ++k) {
+                const uint32_t p = k * 64u + lane;
+                // is position p + 1 the start of another run (or the end)?
+                const bool dn = __shfl_down(head[k] ? 1u : 0u, 1) != 0u;
+                const bool nx = k + 1 < W_VIPL ? __shfl(head[k + 1 < W_VIPL ? k + 1 : k] ? 1u : 0u, 0) != 0u : true;
+                const bool nh = (lane == 63 ? nx : dn) || p + 1 >= NT;
+                const uint64_t hm = __ballot(head[k]);
+                if (head[k]) {
                     const uint32_t dpos = D + (uint32_t)__popcll(hm & lt);
-                    uint64_t n = s_cb[sl];
-                    for (uint32_t q = p + 1; q < NT; ++q) {
-                        const uint32_t s2 = s_ix[q];
-                        const v2 y = s_kb[s2];
-                        if (y.x != x.x || y.y != x.y) break;
-                        n += s_cb[s2];
+                    const v2 x = xs[k];
+                    uint64_t n = cs[k];
+                    if (!nh) {   // equal keys follow (rare): sum the run
+                        for (uint32_t q = p + 1; q < NT; ++q) {
+                            const uint32_t s2 = s_ix[q];
+                            const v2 y = s_kb[s2];
+                            if (y.x != x.x || y.y != x.y) break;
+                            n += s_cb[s2];
+                        }
                     }
                     ko[dpos] = x;
                     co[dpos] = n;
