@@ -1043,7 +1043,7 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
 //   runs    the sorted order is walked once: each run of equal keys becomes one distinct key, stored
 //           with its summed count at leaf_out + its rank among the distinct keys (stores coalesced).
 // Leaves with more items, or with a bucket of more than W_VMAXB items, are listed for k_wleaf.
-constexpr uint32_t W_VC = 576;
+constexpr uint32_t W_VC = 448;
 constexpr uint32_t W_VIPL = W_VC / 64;
 constexpr uint32_t W_VND = 512;         // digits: side bit + 8 key bits
 constexpr uint32_t W_VMAXB = 64;
@@ -1067,7 +1067,7 @@ __device__ __forceinline__ uint64_t wave_or(uint64_t v) {
 __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
     typedef uint64_t v2 __attribute__((ext_vector_type(2)));
     __shared__ v2 s_kb[W_VC];            // items in digit-bucket order
-    __shared__ uint64_t s_cb[W_VC];      // their counts
+    __shared__ uint32_t s_cb[W_VC];      // their counts (a leaf with a larger weighted count is passed on)
     __shared__ uint16_t s_ix[W_VC];      // sorted position -> bucket slot
     __shared__ uint32_t s_dc[W_VND];     // digit counts
     __shared__ uint16_t s_ds[W_VND];     // digit starts
@@ -1113,6 +1113,14 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
                 key[k] = v2{L.wk0[wlo + p - nm], L.wk1[wlo + p - nm]};
                 cnt[k] = L.wcnt[wlo + p - nm];
             }
+        }
+        bool big = false;
+#pragma unroll
+        for (uint32_t k = 0; k < W_VIPL; ++k) big |= cnt[k] > 0xFFFFFFFFull;
+        if (__any(big)) {   // a count beyond the LDS count width: the workgroup kernel
+            if (lane == 0) s_pass[npass] = (uint32_t)lid;
+            ++npass;
+            continue;
         }
         const v2 f = v2{__shfl(key[0].x, 0), __shfl(key[0].y, 0)};   // item 0 (a member if NT > 0)
         uint64_t o0 = 0, o1 = 0;
@@ -1224,7 +1232,7 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
                 if (dg[k] == 0xFFFFFFFFu) continue;
                 slot[k] = s_ds[dg[k]] + wi[k];
                 s_kb[slot[k]] = key[k];
-                s_cb[slot[k]] = cnt[k];
+                s_cb[slot[k]] = (uint32_t)cnt[k];
             }
             wave_lds_sync();
 #pragma unroll

@@ -644,7 +644,7 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     uint64_t *K2 = pget<uint64_t>(p, 2 * n + 2);
     uint32_t *nleaf = pget<uint32_t>(p, B1);
     uint64_t *leaf_lo = pget<uint64_t>(p, NL + 1), *leaf_lb = pget<uint64_t>(p, 2 * NL + 2);
-    const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", 300);
+    const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", 256);
     mrg_wide_launch_l2(K1, K2, bstart, spl1, B1, B1r, target, nleaf, leaf_lo, leaf_lb, s);
     mark();  // 4: L2
     // ---- leaves: aggregate + sort + line bytes (K1 becomes the output key array)
