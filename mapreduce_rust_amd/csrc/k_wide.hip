@@ -315,6 +315,7 @@ struct L2Args {
     uint32_t *nleaf;         // [B1]
     uint64_t *leaf_lo;       // [B1 * MAXB2 + 1] first record of each leaf (absolute)
     uint64_t *leaf_lb;       // [B1 * MAXB2][2] lower key bound of each leaf
+    uint16_t *sub;           // [n] leaf (inside its L1 bucket) of each record: histogram pass -> scatter
 };
 
 __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
@@ -384,7 +385,11 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         for (int u = 0; u < U; ++u) x[u] = inv[min(i0 + (uint64_t)u * W_WG, nb - 1u)];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (i0 + (uint64_t)u * W_WG < nb) atomicAdd(&s_cnt[sub_of(x[u].x, x[u].y)], 1u);
+            if (i0 + (uint64_t)u * W_WG < nb) {
+                const uint32_t j = sub_of(x[u].x, x[u].y);
+                atomicAdd(&s_cnt[j], 1u);
+                gw(L.sub)[base + i0 + (uint64_t)u * W_WG] = (uint16_t)j;
+            }
     }
     lds_barrier();
     {  // exclusive scan of the B2 <= 1024 counts, one per thread
@@ -417,11 +422,16 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     GASW v2 *outv = reinterpret_cast<GASW v2 *>(gw(L.out) + 2 * base);
     for (uint64_t i0 = tid; i0 < nb; i0 += (uint64_t)U * W_WG) {
         v2 x[U];
+        uint32_t j[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = inv[min(i0 + (uint64_t)u * W_WG, nb - 1u)];
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = min(i0 + (uint64_t)u * W_WG, nb - 1u);
+            x[u] = inv[i];
+            j[u] = gw(L.sub)[base + i];   // the histogram pass's leaf: no second splitter search
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (i0 + (uint64_t)u * W_WG < nb) outv[atomicAdd(&s_cur[sub_of(x[u].x, x[u].y)], 1u)] = x[u];
+            if (i0 + (uint64_t)u * W_WG < nb) outv[atomicAdd(&s_cur[j[u]], 1u)] = x[u];
     }
 }
 
@@ -1622,8 +1632,8 @@ void mrg_wide_launch_bstart(const uint32_t *cnt, uint32_t B1, uint32_t ntiles, u
 }
 void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstart, const uint64_t *spl1, uint32_t B1,
                         uint32_t B1r, uint32_t target, uint32_t *nleaf, uint64_t *leaf_lo, uint64_t *leaf_lb,
-                        hipStream_t s) {
-    L2Args L{in, out, bstart, spl1, B1r, target, nleaf, leaf_lo, leaf_lb};
+                        uint16_t *sub, hipStream_t s) {
+    L2Args L{in, out, bstart, spl1, B1r, target, nleaf, leaf_lo, leaf_lb, sub};
     hipLaunchKernelGGL(k_wl2, dim3(B1), dim3(W_WG), 0, s, L);
 }
 void mrg_wide_launch_weights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *wk0, uint64_t *wk1, uint64_t *wcnt,

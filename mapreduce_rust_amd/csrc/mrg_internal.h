@@ -288,7 +288,7 @@ void mrg_wide_launch_bstart(const uint32_t *cnt, uint32_t B1, uint32_t ntiles, u
                             hipStream_t s);
 void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstart, const uint64_t *spl1, uint32_t B1,
                         uint32_t B1r, uint32_t target, uint32_t *nleaf, uint64_t *leaf_lo, uint64_t *leaf_lb,
-                        hipStream_t s);
+                        uint16_t *sub, hipStream_t s);
 void mrg_wide_launch_weights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *wk0, uint64_t *wk1, uint64_t *wcnt,
                              uint32_t *wpart, hipStream_t s);
 void mrg_wide_launch_leaf(const WideLeafArgs &w, uint32_t B1, hipStream_t s);

@@ -627,12 +627,11 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     uint32_t *st2 = pget<uint32_t>(p, mrg_scan_tmp_elems((uint64_t)B1 * ntiles + 1));
     uint64_t *K1 = pget<uint64_t>(p, 2 * (n + nw) + 2);
     uint64_t *bstart = pget<uint64_t>(p, B1 + 1);
+    uint16_t *bid = pget<uint16_t>(p, std::max<uint64_t>(n, 1));   // L1 bucket, then L2 leaf, of each record
     if (n) {
-        uint16_t *bid = pget<uint16_t>(p, n);
         mrg_wide_launch_l1(B, om, segptr, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, bid, false, s);
         mrg_scan_u32(cnt1, cnt1, (uint64_t)B1 * ntiles, st2, s);
         mrg_wide_launch_l1(B, om, segptr, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, bid, true, s);
-        p.put(bid);
     } else {
         HIPCHK(hipMemsetAsync(cnt1, 0, 4ull * B1 * ntiles, s));
     }
@@ -645,7 +644,8 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     uint32_t *nleaf = pget<uint32_t>(p, B1);
     uint64_t *leaf_lo = pget<uint64_t>(p, NL + 1), *leaf_lb = pget<uint64_t>(p, 2 * NL + 2);
     const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", 256);
-    mrg_wide_launch_l2(K1, K2, bstart, spl1, B1, B1r, target, nleaf, leaf_lo, leaf_lb, s);
+    mrg_wide_launch_l2(K1, K2, bstart, spl1, B1, B1r, target, nleaf, leaf_lo, leaf_lb, bid, s);
+    p.put(bid);
     mark();  // 4: L2
     // ---- leaves: aggregate + sort + line bytes (K1 becomes the output key array)
     WideRes &w = c->wide;
