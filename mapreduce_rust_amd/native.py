@@ -260,6 +260,10 @@ class Context:
         _check(load().mrg_job_copy_output(self.h, buf, off[-1]))
         return buf.raw[:off[-1]], off
 
+    def copy_output_to(self, host_ptr, n):
+        """mrg_job_copy_output into caller memory (e.g. a pinned buffer) of at least n bytes."""
+        _check(load().mrg_job_copy_output(self.h, C.c_void_p(host_ptr), n))
+
     def outputs(self):
         """mr-{r}.txt contents for every partition r."""
         data, off = self.copy_output()
