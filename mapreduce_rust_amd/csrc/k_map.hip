@@ -308,62 +308,31 @@ __device__ __forceinline__ bool walk_token(const RD &rd, uint64_t a, uint64_t do
     return true;
 }
 
-// Emission of the fast path's tokens (keys <= 16 bytes, never long), written to keep the wave on
-// one path: the hash for every lane, LDS adds of 0 or 1, branches only around the store and the
-// rare paths (region overflow).
-template <int CAP, bool IDX>
-__device__ __forceinline__ void emit_fast(const MapArgs &A, uint32_t abl, uint32_t hbits, LdsTable<CAP, IDX> &table,
-                                          uint32_t *bcount, const uint32_t *bcap, const unsigned long long *bbase,
-                                          GAS uint64_t *pool, bool have, uint64_t tk0, uint64_t tk1, uint32_t docid) {
-    const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
-    const uint32_t h = key_hash(tk0, tk1, dkey, hbits);
-    const bool hit = table.insert_wave(have && !(abl & 2u), tk0, tk1, dkey, h, abl);
-    const bool tail = have && !hit && !(abl & 1u);
-    const uint32_t b = bucket_of(h);
-    const uint32_t slot = atomicAdd(&bcount[b], tail ? 1u : 0u);
-    const bool ok = tail && slot < bcap[b];
-    if (ok) {
-        GAS uint64_t *dst = pool + (bbase[b] + slot) * (IDX ? 3u : 2u);
-        if (IDX) {
-            dst[0] = tk0;
-            dst[1] = tk1;
-            dst[2] = docid;
-        } else {
-            *reinterpret_cast<GAS u64x2 *>(dst) = u64x2{tk0, tk1};  // one 16-byte store
-        }
-    }
-    const bool ovf = tail && !ok;
-    if (__any(ovf)) {  // region full (rare): the bucket's shared overflow list
-        if (ovf) {
-            const uint32_t j = g_add(&A.onext[b], 1u);
-            if (j < A.ocap) {
-                GAS uint64_t *dst = gp(A.ovf) + ((uint64_t)b * A.ocap + j) * (IDX ? 3u : 2u);
-                dst[0] = tk0;
-                dst[1] = tk1;
-                if (IDX) dst[2] = docid;
-            } else {
-                g_add(&A.counters[CNT_OVF], 1ull);
-            }
-        }
-    }
-}
+// Tail regions of this workgroup, one per hash bucket b: cur[b] = the pool record index of the next
+// append (starts at the region's first record), end[b] = one past the region's last record.  An
+// append is ONE 64-bit LDS atomic that returns the record index itself, and the end is read beside
+// it (it does not depend on the atomic), so a tail token costs one LDS round trip before its store.
+struct TailRegions {
+    unsigned long long *cur;
+    const unsigned long long *end;
+};
 
 // Two tokens per lane (a and b) through the LDS table in one instruction stream: the tag reads,
 // key reads, count adds and tail-cursor adds of both are issued back to back, so every LDS round
 // trip is paid once for two tokens.  Same semantics as emit_fast() applied to a, then b.
 template <int CAP, bool IDX>
 __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint32_t hbits, LdsTable<CAP, IDX> &T,
-                                           uint32_t *bcount, const uint32_t *bcap, const unsigned long long *bbase,
-                                           GAS uint64_t *pool, bool ha, uint64_t a0, uint64_t a1, bool hb,
-                                           uint64_t b0, uint64_t b1, uint32_t docid) {
+                                           TailRegions R, GAS uint64_t *pool, bool ha, uint64_t a0, uint64_t a1,
+                                           bool hb, uint64_t b0, uint64_t b1, uint32_t docid) {
     constexpr uint32_t NS = LdsTable<CAP, IDX>::NS;
     const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
     const uint32_t hA = key_hash(a0, a1, dkey, hbits), hB = key_hash(b0, b1, dkey, hbits);
     const bool actA = ha && !(abl & 2u), actB = hb && !(abl & 2u);
     const uint32_t sA = actA ? 2u * (hA & (NS - 1)) : 0u, sB = actB ? 2u * (hB & (NS - 1)) : 0u;
     const uint32_t bA = bucket_of(hA), bB = bucket_of(hB);
-    // both ways of both sets: four 16-byte reads in flight together
+    // both ways of both sets: four 16-byte reads in flight together, with the two region ends
     const KeyPair kA0 = T.key[sA], kA1 = T.key[sA + 1], kB0 = T.key[sB], kB1 = T.key[sB + 1];
+    const uint64_t endA = R.end[bA], endB = R.end[bB];
     auto eq = [&](const KeyPair &k, uint64_t x, uint64_t y, uint32_t s) {
         return (((k.a ^ x) | (k.b ^ y)) == 0) & (!IDX || T.doc[s] == dkey);
     };
@@ -382,23 +351,20 @@ __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint3
         if (nB) hitB = T.claim(sB, eB0, eB1, b0, b1, dkey, hB);
     }
     const bool tA = ha && !hitA && !(abl & 1u), tB = hb && !hitB && !(abl & 1u);
-    uint32_t slA = 0, slB = 0, capA = 0, capB = 0;
-    if (tA) {
-        slA = atomicAdd(&bcount[bA], 1u);
-        capA = bcap[bA];
+    // both appends in one region (a lane adds 0 to the other token's cursor): one LDS round trip
+    uint64_t iA = 0, iB = 0;
+    if (tA || tB) {
+        iA = atomicAdd(&R.cur[bA], tA ? 1ull : 0ull);
+        iB = atomicAdd(&R.cur[bB], tB ? 1ull : 0ull);
     }
-    if (tB) {
-        slB = atomicAdd(&bcount[bB], 1u);
-        capB = bcap[bB];
-    }
-    const bool okA = tA && slA < capA, okB = tB && slB < capB;
+    const bool okA = tA && iA < endA, okB = tB && iB < endB;
     if (okA) {
-        GAS uint64_t *dst = pool + (bbase[bA] + slA) * (IDX ? 3u : 2u);
+        GAS uint64_t *dst = pool + iA * (IDX ? 3u : 2u);
         if (IDX) { dst[0] = a0; dst[1] = a1; dst[2] = docid; }
         else *reinterpret_cast<GAS u64x2 *>(dst) = u64x2{a0, a1};
     }
     if (okB) {
-        GAS uint64_t *dst = pool + (bbase[bB] + slB) * (IDX ? 3u : 2u);
+        GAS uint64_t *dst = pool + iB * (IDX ? 3u : 2u);
         if (IDX) { dst[0] = b0; dst[1] = b1; dst[2] = docid; }
         else *reinterpret_cast<GAS u64x2 *>(dst) = u64x2{b0, b1};
     }
@@ -424,9 +390,9 @@ __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint3
 // keys; a miss is appended to its hash bucket's region of this workgroup (an LDS counter per
 // bucket, no HBM atomics).  Long keys become long-token records.
 template <int CAP, bool IDX>
-__device__ __forceinline__ void emit(const MapArgs &A, LdsTable<CAP, IDX> &table, uint32_t *bcount,
-                                     const uint32_t *bcap, const unsigned long long *bbase, bool have, uint64_t tk0,
-                                     uint64_t tk1, uint32_t tlen, uint64_t tstart, uint32_t traw, uint32_t docid) {
+__device__ __forceinline__ void emit(const MapArgs &A, LdsTable<CAP, IDX> &table, TailRegions R, bool have,
+                                     uint64_t tk0, uint64_t tk1, uint32_t tlen, uint64_t tstart, uint32_t traw,
+                                     uint32_t docid) {
     const bool is_long = have && tlen > 16u;
     bool tail = false;
     uint32_t h = 0;
@@ -440,10 +406,11 @@ __device__ __forceinline__ void emit(const MapArgs &A, LdsTable<CAP, IDX> &table
     }
     if (tail && !(A.ablate & 1u)) {
         const uint32_t b = bucket_of(h);
-        const uint32_t slot = atomicAdd(&bcount[b], 1u);
+        const uint64_t end = R.end[b];
+        const uint64_t idx = atomicAdd(&R.cur[b], 1ull);
         GAS uint64_t *dst = nullptr;
-        if (slot < bcap[b]) {
-            dst = gp(A.pool) + (bbase[b] + slot) * (IDX ? 3u : 2u);
+        if (idx < end) {
+            dst = gp(A.pool) + idx * (IDX ? 3u : 2u);
         } else {  // region full (rare): the bucket's shared overflow list
             const uint32_t j = g_add(&A.onext[b], 1u);
             if (j < A.ocap) dst = gp(A.ovf) + ((uint64_t)b * A.ocap + j) * (IDX ? 3u : 2u);
@@ -474,8 +441,7 @@ __device__ __forceinline__ void emit(const MapArgs &A, LdsTable<CAP, IDX> &table
 // loop (the main loop only records which tiles need it), so its registers never add to the hot
 // loop's.
 template <int CAP, bool IDX>
-__device__ __forceinline__ uint32_t generic_tile(const MapArgs &A, LdsTable<CAP, IDX> table, uint32_t *s_bcount,
-                                              const uint32_t *s_bcap, const unsigned long long *s_bbase,
+__device__ __forceinline__ uint32_t generic_tile(const MapArgs &A, LdsTable<CAP, IDX> table, TailRegions R,
                                               const uint8_t *win, uint64_t At, uint64_t t0, uint64_t t1,
                                               uint64_t doc_lo, uint64_t doc_hi, uint64_t wlo, uint64_t whi,
                                               uint32_t docid) {
@@ -540,7 +506,7 @@ __device__ __forceinline__ uint32_t generic_tile(const MapArgs &A, LdsTable<CAP,
             }
             if (!__any(have)) break;
             my_tokens += have ? 1u : 0u;
-            emit(A, table, s_bcount, s_bcap, s_bbase, have, tk0, tk1, tlen, tstart, traw, docid);
+            emit(A, table, R, have, tk0, tk1, tlen, tstart, traw, docid);
         }
     return my_tokens;
 }
@@ -556,17 +522,17 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ uint16_t s_q[NW][QCAP];
     // LUT and length masks first in LDS (highest alignment): their base then fits the 16-bit
     // offset field of ds_read, so a lookup needs no separate address add
-    __shared__ __attribute__((aligned(2048))) uint16_t s_lut[128];  // ASCII class: W | S << 8
-    __shared__ __attribute__((aligned(1024))) uint32_t s_zm[17][4];  // key-length byte masks
+    // ASCII class W | S << 4, one byte per character: the 128 entries are 32 dwords, one per LDS
+    // bank, so a wave's lookups never conflict (lanes reading the same dword share it)
+    __shared__ __attribute__((aligned(1024))) uint8_t s_lut[128];
     // v_perm selectors per (key length, 1-byte gap position; 16 = none) over the r-aligned window
     __shared__ __attribute__((aligned(16))) uint32_t s_sel[17 * 17][4];
     // workgroup: combine table + tail-region cursors
     __shared__ KeyPair s_key[CAP];
     __shared__ unsigned int s_cnt[CAP];
     __shared__ __attribute__((aligned(16))) unsigned int s_doc[IDX ? CAP : 1];
-    __shared__ uint32_t s_bcount[MRG_NBUCKET];           // records appended to (bucket, this WG)
-    __shared__ uint32_t s_bcap[MRG_NBUCKET];
-    __shared__ unsigned long long s_bbase[MRG_NBUCKET];  // first pool record of (bucket, this WG)
+    __shared__ unsigned long long s_tcur[MRG_NBUCKET];  // next pool record of (bucket, this WG)
+    __shared__ unsigned long long s_tend[MRG_NBUCKET];  // end of that region
     __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
     __shared__ uint32_t s_next, s_ngen;                  // next block of the workgroup's share; list length
     __shared__ unsigned int s_door[MRG_MAP_DOOR ? LdsTable<CAP, IDX>::DW : 1];  // admission bitmap
@@ -584,10 +550,10 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     if (MRG_MAP_DOOR)
         for (int i = tid; i < (int)LdsTable<CAP, IDX>::DW; i += WG) s_door[i] = 0;
     for (int b = tid; b < MRG_NBUCKET; b += WG) {
-        s_bcount[b] = 0;
         const uint32_t cap = gp(A.bcap)[b];
-        s_bcap[b] = cap;
-        s_bbase[b] = gp(A.rbase)[b] + (uint64_t)blockIdx.x * cap;
+        const uint64_t base = gp(A.rbase)[b] + (uint64_t)blockIdx.x * cap;
+        s_tcur[b] = base;
+        s_tend[b] = base + cap;
     }
     if (tid == 0) {
         s_next = 0;
@@ -595,7 +561,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     }
     if (tid < 128) {
         const uint32_t c = mrg_uclass((uint32_t)tid);
-        s_lut[tid] = (uint16_t)((c == MRG_CLS_W ? 1u : 0u) | (c == MRG_CLS_S ? 0x100u : 0u));
+        s_lut[tid] = (uint8_t)((c == MRG_CLS_W ? 1u : 0u) | (c == MRG_CLS_S ? 0x10u : 0u));
     }
     auto zmask = [](uint32_t L, uint32_t j) {  // word j, byte p (p = 0 least significant) holds key byte 4j + 3 - p
         uint32_t m = 0;
@@ -603,7 +569,6 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             if (4u * j + 3u - p >= L) m |= 0xFFu << (8u * p);
         return m;
     };
-    if (tid < 17 * 4) s_zm[tid >> 2][tid & 3] = zmask((uint32_t)tid >> 2, (uint32_t)tid & 3u);
     for (int i = tid; i < 17 * 17 * 4; i += WG) {
         // key byte 4j + 3 - p comes from aligned-window byte 4j + 3 - p (+ 1 from the gap on); bytes
         // at or past the key length select the constant 0 (v_perm selector 0x0C)
@@ -612,6 +577,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         s_sel[L * 17u + g][j] = ((0x00010203u + (gm & 0x01010101u)) & ~zm) | (0x0C0C0C0Cu & zm);
     }
     LdsTable<CAP, IDX> table{s_key, s_cnt, s_doc, s_door};
+    const TailRegions tails{s_tcur, s_tend};
     uint32_t my_tokens = 0;
     // uniform job parameters used in the hot loop, read once
     const uint32_t abl = A.ablate;
@@ -693,24 +659,24 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const uint32_t lo_rel = doc_lo > Ab ? (uint32_t)(doc_lo - Ab) : 0u;
         const uint32_t hi_rel = (uint32_t)min(doc_hi - Ab, (uint64_t)(BLK + HALO));
         auto classify = [&](const uint4 &x, uint32_t B) -> uint32_t {
-            if (B >= hi_rel) return 0xFFFF0000u;
-            uint32_t mA = 0, mB = 0;  // bytes 0..7 and 8..15: W bits 0..7, S bits 8..15
+            // all 16 lookups in flight before the first use (one LDS wait per segment)
+            uint32_t e[16];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint32_t w = k == 0 ? x.x : (k == 1 ? x.y : (k == 2 ? x.z : x.w));
 #pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    // 2 x byte value (ASCII: the bit below each byte is the 0 top bit of the byte before)
-                    const uint32_t i2 = b == 0 ? ((w << 1) & 0xFEu) : __builtin_amdgcn_ubfe(w, 8 * b - 1, 8);
-                    const uint32_t cl = *reinterpret_cast<const uint16_t *>(reinterpret_cast<const uint8_t *>(s_lut) + i2);
-                    const int i = 4 * k + b;
-                    if (i < 8) mA |= cl << i;
-                    else mB |= cl << (i - 8);
-                }
+                for (int b = 0; b < 4; ++b)
+                    e[4 * k + b] = s_lut[b == 0 ? (w & 0x7Fu) : __builtin_amdgcn_ubfe(w, 8 * b, 7)];
             }
-            const uint32_t m = __builtin_amdgcn_perm(mB, mA, 0x05010400u);  // W16 | S16 << 16
+            // nibbles: W of bytes 0-3, S of bytes 0-3, W of bytes 4-7, ... (byte i: bit i % 4)
+            uint32_t y = e[0];
+#pragma unroll
+            for (int i = 1; i < 16; ++i) y |= e[i] << (i + 4 * (i / 4));
+            const uint32_t t = y & 0x0F0F0F0Fu, u = (y >> 4) & 0x0F0F0F0Fu;
+            // bytes 0 and 2 of t | t >> 4: W of bytes 0-7 and 8-15 (u: S)
+            const uint32_t m = __builtin_amdgcn_perm(u | (u >> 4), t | (t >> 4), 0x06040200u);  // W16 | S16 << 16
             const uint32_t lo_inv = lo_rel > B ? min(lo_rel - B, 16u) : 0u;
-            const uint32_t hi_ok = min(hi_rel - B, 16u);
+            const uint32_t hi_ok = B < hi_rel ? min(hi_rel - B, 16u) : 0u;
             const uint32_t valid = ((1u << hi_ok) - 1u) & ~((1u << lo_inv) - 1u);
             return (m & (valid | (valid << 16))) | ((~valid & 0xFFFFu) << 16);
         };
@@ -727,13 +693,13 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const uint32_t cl = s_lut[__builtin_amdgcn_ubfe(dwv, 8u * (k & 3u), 7)];
             const bool in = (uint32_t)BLK + k < hi_rel;  // bytes past the document are White_Space
             const uint32_t wm = (uint32_t)__ballot(lane < 16 && in && (cl & 1u));
-            const uint32_t sm = (uint32_t)__ballot(lane < 16 && (!in || (cl & 0x100u)));
+            const uint32_t sm = (uint32_t)__ballot(lane < 16 && (!in || (cl & 0x10u)));
             mh = (wm & 0xFFFFu) | (sm << 16);
         }
         const bool n0 = na(X.v0), n1 = na(X.v1), ne = na(X.e);
         // class of the byte before the block (lane 0's e, byte 15)
         const uint32_t prev_blk =
-            Ab > doc_lo ? (uint32_t)(s_lut[(lane_u32(X.e.w, 0) >> 24) & 0x7Fu] >> 8) : 1u;
+            Ab > doc_lo ? (uint32_t)(s_lut[(lane_u32(X.e.w, 0) >> 24) & 0x7Fu] >> 4) : 1u;
         MRG_PT(1);
         // the next block's registers are waited for HERE, before this block's tail stores are
         // issued: vmcnt also counts stores, so a wait placed after them would wait for their
@@ -897,7 +863,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                     nslow += na + (uint32_t)__builtin_popcountll(mb);
                 }
                 my_tokens += (fa ? 1u : 0u) + (fb ? 1u : 0u);
-                emit_fast2(A, abl, hbits, table, s_bcount, s_bcap, s_bbase, pool, fa, a0, a1, fb, b0, b1, docid);
+                emit_fast2(A, abl, hbits, table, tails, pool, fa, a0, a1, fb, b0, b1, docid);
             }
             // deferred slow tokens: the exact per-codepoint walker, one token per lane (forward
             // reads only: the staged bytes are [At, whi))
@@ -922,7 +888,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                         }
                     }
                     my_tokens += have ? 1u : 0u;
-                    emit(A, table, s_bcount, s_bcap, s_bbase, have, tk0, tk1, tlen, a, traw, docid);
+                    emit(A, table, tails, have, tk0, tk1, tlen, a, traw, docid);
                 }
             }
         }
@@ -985,7 +951,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 if (j0 >= T.v0 && j0 < T.v1) reinterpret_cast<uint4 *>(win)[j0] = x0;
                 if (has1 && j1 >= T.v0 && j1 < T.v1) reinterpret_cast<uint4 *>(win)[j1] = x1;
                 wave_sync_lds();
-                my_tokens += generic_tile<CAP, IDX>(A, table, s_bcount, s_bcap, s_bbase, win, T.At, T.t0, T.t1,
+                my_tokens += generic_tile<CAP, IDX>(A, table, tails, win, T.At, T.t0, T.t1,
                                                     T.doc_lo, T.doc_hi, T.wlo, T.whi, T.docid);
             }
         }
@@ -997,9 +963,10 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     uint16_t *s_rank = &s_q[0][0];
     GAS uint32_t *bcount = gp(A.bcount) + (uint64_t)blockIdx.x * MRG_NBUCKET;
     uint32_t my_tail = 0;
-    for (int b = tid; b < MRG_NBUCKET; b += WG) {
-        my_tail += s_bcount[b];
-        bcount[b] = s_bcount[b];
+    for (int b = tid; b < MRG_NBUCKET; b += WG) {  // appends made (may exceed the capacity)
+        const uint32_t n = (uint32_t)(s_tcur[b] - (s_tend[b] - gp(A.bcap)[b]));
+        my_tail += n;
+        bcount[b] = n;
     }
     for (int b = tid; b <= MRG_NBUCKET; b += WG) s_hist[b] = 0;
     __syncthreads();

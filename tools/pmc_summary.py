@@ -12,9 +12,9 @@ import json
 import os
 
 
-def load(pmc_dir):
+def load(pmc_dir, pattern="*counter_collection.csv"):
     per = collections.defaultdict(lambda: collections.defaultdict(list))
-    for f in sorted(glob.glob(os.path.join(pmc_dir, "*counter_collection.csv"))):
+    for f in sorted(glob.glob(os.path.join(pmc_dir, "**", pattern), recursive=True)):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
             per[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -34,8 +34,10 @@ def main():
     ap.add_argument("--dir", default="gpurun_out/pmc")
     ap.add_argument("--traffic", type=int, default=0, help="input bytes per k_map launch")
     ap.add_argument("--out", default="profiles/map_traffic.json")
+    ap.add_argument("--glob", default="*counter_collection.csv", help="CSV file pattern under --dir")
+    ap.add_argument("--only", default="", help="print only kernels whose short name starts with this")
     a = ap.parse_args()
-    per = load(a.dir)
+    per = load(a.dir, a.glob)
     rows = []
     for name, ctr in per.items():
         s = short(name)
@@ -44,6 +46,8 @@ def main():
         avg = {c: sum(v) / len(v) for c, v in ctr.items()}
         rows.append((s, avg, max(len(v) for v in ctr.values())))
     for s, avg, n in rows:
+        if a.only and not s.startswith(a.only):
+            continue
         print(f"{s}  ({n} dispatch-counter rows)")
         for c in sorted(avg):
             print(f"    {c:28s} {avg[c]:.4g}")
