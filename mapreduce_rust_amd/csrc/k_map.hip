@@ -105,6 +105,11 @@ __device__ __forceinline__ uint64_t g_wave_append(unsigned long long *counter, b
     return base + (uint64_t)__popcll(mask & mrg_lanemask_lt());
 }
 
+// 64-bit min/max as plain compares (HIP's overload set can resolve max(u64, u64) to the double
+// version: a VALU f64 round trip per call)
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
 struct TileInfo {
     uint64_t At, t0, t1, doc_lo, doc_hi, wlo, whi;
     uint32_t docid, v0, v1;
@@ -127,8 +132,8 @@ __device__ __forceinline__ BlkInfo locate_blk(const MapArgs &A, uint64_t c, uint
     b.Ab = (b.doc_lo & ~15ull) + (c - cb[d]) * (uint64_t)BLK;
     b.docid = A.doc_id ? cp(A.doc_id)[d] : d;
     const uint64_t vbase = b.Ab - (uint64_t)BEHIND;  // may wrap below 0: only differences are used
-    const uint64_t wlo = max(b.doc_lo, b.Ab >= (uint64_t)BEHIND ? b.Ab - BEHIND : 0ull);
-    const uint64_t whi = min(b.Ab + (uint64_t)(BLK + HALO), b.doc_hi);
+    const uint64_t wlo = umax64(b.doc_lo, b.Ab >= (uint64_t)BEHIND ? b.Ab - BEHIND : 0ull);
+    const uint64_t whi = umin64(b.Ab + (uint64_t)(BLK + HALO), b.doc_hi);
     b.v0 = (uint32_t)(((wlo & ~15ull) - vbase) >> 4);
     b.v1 = (uint32_t)((((whi + 15u) & ~15ull) - vbase) >> 4);
     return b;
@@ -153,11 +158,11 @@ __device__ __forceinline__ TileInfo sub_tile(const BlkInfo &b, uint32_t j) {
     t.doc_lo = b.doc_lo;
     t.doc_hi = b.doc_hi;
     t.docid = b.docid;
-    t.t0 = max(t.At, t.doc_lo);
-    t.t1 = min(t.At + (uint64_t)TILE, t.doc_hi);
+    t.t0 = umax64(t.At, t.doc_lo);
+    t.t1 = umin64(t.At + (uint64_t)TILE, t.doc_hi);
     const uint64_t wbase = t.At - (uint64_t)BEHIND;
-    t.wlo = max(t.doc_lo, t.At >= (uint64_t)BEHIND ? t.At - BEHIND : 0ull);
-    t.whi = min(t.t1 + (uint64_t)HALO, t.doc_hi);
+    t.wlo = umax64(t.doc_lo, t.At >= (uint64_t)BEHIND ? t.At - BEHIND : 0ull);
+    t.whi = umin64(t.t1 + (uint64_t)HALO, t.doc_hi);
     t.v0 = (uint32_t)(((t.wlo & ~15ull) - wbase) >> 4);
     t.v1 = (uint32_t)((((t.whi + 15u) & ~15ull) - wbase) >> 4);
     return t;
@@ -454,8 +459,8 @@ __device__ __forceinline__ uint32_t generic_tile(const MapArgs &A, LdsTable<CAP,
     uint32_t my_tokens = 0;
         // ================= generic path: per-lane codepoint walker =================
         const uint64_t sg0 = At + (uint64_t)lane * SEG;
-        const uint64_t s0 = max(sg0, t0);
-        const uint64_t s1 = min(sg0 + (uint64_t)SEG, t1);
+        const uint64_t s0 = umax64(sg0, t0);
+        const uint64_t s1 = umin64(sg0 + (uint64_t)SEG, t1);
         bool done = s0 >= s1;
         uint64_t p = s0;
         bool prevS = true;
@@ -657,7 +662,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         // classify segment [B, B + 16) (relative to Ab) into W16 | S16 << 16; bytes outside the
         // document count as White_Space (exact for every staged byte: no window cut)
         const uint32_t lo_rel = doc_lo > Ab ? (uint32_t)(doc_lo - Ab) : 0u;
-        const uint32_t hi_rel = (uint32_t)min(doc_hi - Ab, (uint64_t)(BLK + HALO));
+        const uint32_t hi_rel = (uint32_t)umin64(doc_hi - Ab, (uint64_t)(BLK + HALO));
         auto classify = [&](const uint4 &x, uint32_t B) -> uint32_t {
             // all 16 lookups in flight before the first use (one LDS wait per segment)
             uint32_t e[16];
@@ -733,8 +738,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 }
                 continue;
             }
-            const uint64_t t1 = min(At + (uint64_t)TILE, doc_hi);
-            const uint64_t whi = min(t1 + (uint64_t)HALO, doc_hi);
+            const uint64_t t1 = umin64(At + (uint64_t)TILE, doc_hi);
+            const uint64_t whi = umin64(t1 + (uint64_t)HALO, doc_hi);
             const uint64_t wbase = At - (uint64_t)BEHIND;
 
             // stage the tile and its 64-byte halo (the previous tile's readers are done: program order)

@@ -382,7 +382,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     for (uint64_t i0 = tid; i0 < nb; i0 += (uint64_t)U * W_WG) {
         v2 x[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = inv[min(i0 + (uint64_t)u * W_WG, nb - 1u)];
+        for (int u = 0; u < U; ++u) x[u] = inv[min(i0 + (uint64_t)u * W_WG, (uint64_t)(nb - 1u))];
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (i0 + (uint64_t)u * W_WG < nb) {
@@ -425,7 +425,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         uint32_t j[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t i = min(i0 + (uint64_t)u * W_WG, nb - 1u);
+            const uint64_t i = min(i0 + (uint64_t)u * W_WG, (uint64_t)(nb - 1u));
             x[u] = inv[i];
             j[u] = gw(L.sub)[base + i];   // the histogram pass's leaf: no second splitter search
         }
