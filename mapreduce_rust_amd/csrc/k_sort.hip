@@ -6,6 +6,10 @@
 // whose digit is constant are skipped (e.g. key bytes beyond the longest key, nReduce <= 256).
 // Per pass: per-tile histogram -> scan -> stable scatter, the local rank computed by a wave64
 // 8-ballot match (peers with the same digit) plus per-wave digit counters in LDS.
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
 #include "mrg_device.h"
 #include "mrg_internal.h"
 
@@ -248,6 +252,91 @@ typename TR::R *radix_sort_t(typename TR::R *a, typename TR::R *b, uint64_t n, c
     return a;
 }
 
+// ------------------------------------------------------------------ MSD bucket sort of SortRecs
+// The distinct keys of a job (~1e6) sorted by (part, k0, k1, doc) in three passes instead of up to
+// 13 LSD passes: every record takes a bucket = (part, leading key bits) and its rank inside the
+// bucket from one global atomic; the buckets' offsets are scanned; records are scattered; each bucket
+// of at most MSD_LCAP records is then sorted in LDS by one workgroup (bitonic network over whole
+// records).  The key bits of the bucket id come from the first three key bytes clamped to 7 bits
+// (monotone: every byte >= 0x7F maps to 0x7F), so text keys, whose bytes leave the top bit unused,
+// spread over the buckets.  A few oversized buckets are sorted by the LSD radix sort on their own
+// segments; many of them (a skewed key set) send the whole array through the LSD sort.  Keys are
+// distinct (or fully ordered afterwards by k_fix_runs for > 16-byte keys): stability is not needed.
+constexpr int MSD_BITS = 16;
+constexpr uint32_t MSD_NB = 1u << MSD_BITS;
+constexpr int MSD_WG = 512;
+constexpr uint32_t MSD_LCAP = 2048;
+constexpr uint32_t MSD_MAX_BIG = 16;
+
+__device__ __forceinline__ uint32_t msd_bucket(const SortRec &r, uint32_t pbits) {
+    if (pbits >= (uint32_t)MSD_BITS) return r.part >> (pbits - MSD_BITS);
+    const uint32_t b0 = min((uint32_t)(r.k0 >> 56), 127u), b1 = min((uint32_t)(r.k0 >> 48) & 0xFFu, 127u),
+                   b2 = min((uint32_t)(r.k0 >> 40) & 0xFFu, 127u);
+    const uint32_t code = (b0 << 14) | (b1 << 7) | b2;  // 21 bits, monotone in the key
+    const uint32_t kb = MSD_BITS - pbits;              // key bits of the bucket id (1..16)
+    return (r.part << kb) | (code >> (21 - kb));
+}
+
+__device__ __forceinline__ bool rec_less(const SortRec &a, const SortRec &b) {
+    if (a.part != b.part) return a.part < b.part;
+    if (a.k0 != b.k0) return a.k0 < b.k0;
+    if (a.k1 != b.k1) return a.k1 < b.k1;
+    return a.doc < b.doc;
+}
+
+__global__ void k_msd_count(const SortRec *in, uint64_t n, uint32_t pbits, uint32_t *cnt, uint32_t *rank) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    rank[i] = atomicAdd(&cnt[msd_bucket(in[i], pbits)], 1u);
+}
+
+__global__ void k_msd_scatter(const SortRec *in, SortRec *out, uint64_t n, uint32_t pbits, const uint32_t *off,
+                              const uint32_t *rank) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const SortRec r = in[i];
+    out[off[msd_bucket(r, pbits)] + rank[i]] = r;
+}
+
+// one workgroup per bucket: the bucket's records through LDS, bitonic-sorted (padding sorts last);
+// an oversized bucket is only listed (big[0] = how many, big[1..] = which, up to MSD_MAX_BIG)
+__global__ __launch_bounds__(MSD_WG) void k_msd_leaf(SortRec *recs, const uint32_t *off, uint32_t lcap,
+                                                    uint32_t *big) {
+    __shared__ SortRec s_r[MSD_LCAP];
+    const uint32_t b = blockIdx.x, lo = off[b], m = off[b + 1] - lo;
+    if (m <= 1) return;
+    if (m > lcap) {
+        if (threadIdx.x == 0) {
+            const uint32_t k = atomicAdd(&big[0], 1u);
+            if (k < MSD_MAX_BIG) big[1 + k] = b;
+        }
+        return;
+    }
+    uint32_t P = 2;
+    while (P < m) P <<= 1;
+    for (uint32_t i = threadIdx.x; i < P; i += MSD_WG) {
+        SortRec r;
+        if (i < m) r = recs[lo + i];
+        else r = SortRec{~0ull, ~0ull, ~0u, ~0u, 0u, 0u};
+        s_r[i] = r;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < P / 2; t += MSD_WG) {
+                const uint32_t i = 2 * t - (t & (j - 1)), l = i + j;
+                const SortRec x = s_r[i], y = s_r[l];
+                if (rec_less(y, x) == ((i & k) == 0)) {
+                    s_r[i] = y;
+                    s_r[l] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < m; i += MSD_WG) recs[lo + i] = s_r[i];
+}
+
 __global__ void k_pack_kv(const uint64_t *k, const uint32_t *v, uint64_t n, KV64 *out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = KV64{k[i], v[i], 0};
@@ -271,7 +360,47 @@ void mrg_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *tmp, 
 
 uint64_t mrg_sort_tmp_bytes(uint64_t n) {
     const uint64_t ntiles = (n + TILE - 1) / TILE;
-    return sizeof(unsigned long long) * 24 * 256 + sizeof(uint32_t) * (256 * ntiles + scan_tmp(256 * ntiles)) + 256;
+    const uint64_t lsd = sizeof(unsigned long long) * 24 * 256 + sizeof(uint32_t) * (256 * ntiles + scan_tmp(256 * ntiles)) + 256;
+    const uint64_t msd = sizeof(uint32_t) * (2ull * (MSD_NB + 2) + MSD_MAX_BIG + 2 + scan_tmp(MSD_NB + 1) + n) + 256;
+    return lsd + msd + 256;  // the MSD arrays, then room for an LSD sort of one oversized bucket
+}
+
+SortRec *mrg_msd_sort(SortRec *a, SortRec *b, uint64_t n, uint32_t pbits, const SortPlan &plan, void *tmp,
+                      hipStream_t s, uint32_t *n_big) {
+    if (n_big) *n_big = 0;
+    if (n <= 1) return a;
+    uint32_t *cnt = (uint32_t *)tmp;            // [NB + 1]
+    uint32_t *off = cnt + (MSD_NB + 2);         // [NB + 1]
+    uint32_t *big = off + (MSD_NB + 2);         // [1 + MAX_BIG]
+    uint32_t *stmp = big + (MSD_MAX_BIG + 2);   // scan temp
+    uint32_t *rank = stmp + scan_tmp(MSD_NB + 1);
+    // the LSD temp (histograms, tile counts) goes after the MSD arrays
+    void *ltmp = (void *)(((uintptr_t)(rank + n) + 255) & ~(uintptr_t)255);
+    hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (MSD_NB + 2), s);
+    hipMemsetAsync(big, 0, sizeof(uint32_t), s);
+    const unsigned g = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(k_msd_count, dim3(g), dim3(256), 0, s, a, n, pbits, cnt, rank);
+    scan_rec<uint32_t>(cnt, off, MSD_NB + 1, stmp, s);  // off[NB] = n (cnt[NB] == 0)
+    hipLaunchKernelGGL(k_msd_scatter, dim3(g), dim3(256), 0, s, a, b, n, pbits, off, rank);
+    uint32_t lcap = MSD_LCAP;
+    if (const char *e = getenv("MRG_TEST_SORT_LCAP")) lcap = std::max<uint32_t>(1u, std::min<uint32_t>(MSD_LCAP, (uint32_t)atoi(e)));
+    hipLaunchKernelGGL(k_msd_leaf, dim3(MSD_NB), dim3(MSD_WG), 0, s, b, off, lcap, big);
+    uint32_t nb = 0;
+    hipMemcpyAsync(&nb, big, sizeof nb, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    if (n_big) *n_big = nb;
+    if (!nb) return b;
+    if (nb > MSD_MAX_BIG) return mrg_radix_sort(b, a, n, plan, ltmp, s, nullptr);  // skewed: all of it
+    std::vector<uint32_t> bl(nb), o(MSD_NB + 1);
+    hipMemcpyAsync(bl.data(), big + 1, sizeof(uint32_t) * nb, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(o.data(), off, sizeof(uint32_t) * (MSD_NB + 1), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    for (uint32_t bk : bl) {  // each oversized bucket by the LSD sort on its segment (a: scratch)
+        const uint64_t lo = o[bk], m = o[bk + 1] - lo;
+        SortRec *r = mrg_radix_sort(b + lo, a + lo, m, plan, ltmp, s, nullptr);
+        if (r != b + lo) hipMemcpyAsync(b + lo, r, sizeof(SortRec) * m, hipMemcpyDeviceToDevice, s);
+    }
+    return b;
 }
 
 SortRec *mrg_radix_sort(SortRec *recs, SortRec *alt, uint64_t n, const SortPlan &plan, void *tmp, hipStream_t s,

@@ -200,6 +200,12 @@ uint64_t mrg_sort_tmp_bytes(uint64_t n);
 // Stable sort by (part, k0, k1, doc) ascending.  Returns the buffer (recs or alt) with the result.
 SortRec *mrg_radix_sort(SortRec *recs, SortRec *alt, uint64_t n, const SortPlan &plan, void *tmp, hipStream_t s,
                         int *passes_run);
+// Sort by (part, k0, k1, doc) ascending, not stable (keys distinct): MSD buckets on (part: pbits
+// significant bits, leading key bits) + LDS bitonic sort per bucket; oversized buckets by the LSD
+// sort.  Returns recs or alt; *n_big = oversized buckets (more than 16: the whole array went through
+// the LSD sort).
+SortRec *mrg_msd_sort(SortRec *recs, SortRec *alt, uint64_t n, uint32_t pbits, const SortPlan &plan, void *tmp,
+                      hipStream_t s, uint32_t *n_big);
 // Stable sort of (u64 key, u32 val) pairs by key, in place in (keys, vals); kv_tmp holds 4n u64.
 void mrg_radix_sort_u64(uint64_t *keys, uint32_t *vals, uint64_t *kv_tmp, uint64_t n, void *tmp, hipStream_t s);
 

@@ -1003,9 +1003,10 @@ SortRec *sort_keys(mrg_ctx *c, KeySet ks, uint32_t R, const uint32_t *d_rank, So
     plan.use_k0 = plan.use_k1 = true;
     plan.use_doc = idx;
     plan.doc_bytes = idx ? bytes_for(c->names.size() - 1) : 0;
-    int passes = 0;
     check_sort_n(n, "key sort");
-    return mrg_radix_sort(a, b, n, plan, stmp, c->stream, &passes);
+    const uint32_t pbits = R > 1 ? 32u - (uint32_t)__builtin_clz(R - 1u) : 0u;
+    uint32_t n_big = 0;
+    return mrg_msd_sort(a, b, n, pbits, plan, stmp, c->stream, &n_big);
 }
 
 FormatArgs format_args(mrg_ctx *c, const SortRec *recs, KeySet ks, uint32_t R, int drop_last, const DocRank &dr) {

@@ -109,7 +109,7 @@ def test_c5_slice_vs_oracle(ctx):
 @pytest.fixture
 def knobs():
     keys = ["MRG_TEST_TAIL_CAP", "MRG_TEST_OVF_CAP", "MRG_TEST_AGG_OCAP", "MRG_WIDE", "MRG_TEST_LEAF_CAP",
-            "MRG_TEST_LEAF_TARGET"]
+            "MRG_TEST_LEAF_TARGET", "MRG_TEST_SORT_LCAP"]
     saved = {k: os.environ.get(k) for k in keys}
 
     def set_(**kw):
@@ -159,6 +159,25 @@ def test_aggregation_overflow_regrow_vs_oracle(ctx, corpus, knobs):
     st = ctx.stats()
     assert st["agg_launches"] >= 2 and st["overflow_keys"] > 1000, st
     assert got == O.wc(corpus, 10, O.FAST)
+
+
+@pytest.mark.parametrize("lcap", ["1", "48", "2048"])
+def test_key_sort_buckets_vs_oracle(ctx, corpus, knobs, lcap):
+    """The distinct-key sort (worker.rs:162-164): MSD buckets on (partition bits, leading key bits),
+    each bucket bitonic-sorted in LDS, a bucket above MRG_TEST_SORT_LCAP keys sorted by the LSD radix
+    sort on its own segment instead (lcap 48: some buckets; lcap 1: more than 16 oversized buckets, so
+    the whole array goes through the LSD sort).  R = 20000 has more partition
+    bits than the bucket id (buckets = partition ranges); R = 1 buckets on key bits alone."""
+    import mapreduce_rust_amd as M
+    import oracle_lib as O
+    from gpu_util import run_wc
+    knobs(MRG_TEST_SORT_LCAP=lcap, MRG_WIDE=0)
+    for R in (1, 10, 64, 20000):
+        assert run_wc(ctx, corpus, R) == O.wc(corpus, R, O.FAST), R
+    # forced internal hash collisions, and the indexer's (word, doc) keys through the same sort
+    assert run_wc(ctx, corpus, 10, flags=M.debug_hash_bits(4)) == O.wc(corpus, 10, O.FAST)
+    names = [f"data/gut-{m}.txt" for m in range(6)]
+    assert run_wc(ctx, corpus, 10, app=M.APP_INDEXER, names=names) == O.indexer(corpus, names, 10)
 
 
 def test_library_shuffle_single_rank(ctx, corpus):
