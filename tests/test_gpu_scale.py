@@ -166,13 +166,13 @@ def test_key_sort_buckets_vs_oracle(ctx, corpus, knobs, lcap):
     """The distinct-key sort (worker.rs:162-164): MSD buckets on (partition bits, leading key bits),
     each bucket bitonic-sorted in LDS, a bucket above MRG_TEST_SORT_LCAP keys sorted by the LSD radix
     sort on its own segment instead (lcap 48: some buckets; lcap 1: more than 16 oversized buckets, so
-    the whole array goes through the LSD sort).  R = 20000 has more partition
-    bits than the bucket id (buckets = partition ranges); R = 1 buckets on key bits alone."""
+    the whole array goes through the LSD sort).  R = 20000 leaves one key bit in the bucket id and R = 40000 none
+    (buckets = partitions); R = 1 buckets on key bits alone."""
     import mapreduce_rust_amd as M
     import oracle_lib as O
     from gpu_util import run_wc
     knobs(MRG_TEST_SORT_LCAP=lcap, MRG_WIDE=0)
-    for R in (1, 10, 64, 20000):
+    for R in (1, 10, 64, 20000, 40000):
         assert run_wc(ctx, corpus, R) == O.wc(corpus, R, O.FAST), R
     # forced internal hash collisions, and the indexer's (word, doc) keys through the same sort
     assert run_wc(ctx, corpus, 10, flags=M.debug_hash_bits(4)) == O.wc(corpus, 10, O.FAST)
