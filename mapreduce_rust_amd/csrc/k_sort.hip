@@ -270,8 +270,12 @@ constexpr uint32_t MSD_MAX_BIG = 16;
 
 __device__ __forceinline__ uint32_t msd_bucket(const SortRec &r, uint32_t pbits) {
     if (pbits >= (uint32_t)MSD_BITS) return r.part >> (pbits - MSD_BITS);
-    const uint32_t b0 = min((uint32_t)(r.k0 >> 56), 127u), b1 = min((uint32_t)(r.k0 >> 48) & 0xFFu, 127u),
-                   b2 = min((uint32_t)(r.k0 >> 40) & 0xFFu, 127u);
+    // bytes clamped to 7 bits, saturating: after a byte >= 0x7F every later byte counts as 0x7F
+    // (otherwise "\xc3\x86n" would get a larger code than "\xc3\x88")
+    const uint32_t c0 = (uint32_t)(r.k0 >> 56), c1 = (uint32_t)(r.k0 >> 48) & 0xFFu, c2 = (uint32_t)(r.k0 >> 40) & 0xFFu;
+    const uint32_t b0 = min(c0, 127u);
+    const uint32_t b1 = b0 == 127u ? 127u : min(c1, 127u);
+    const uint32_t b2 = b1 == 127u ? 127u : min(c2, 127u);
     const uint32_t code = (b0 << 14) | (b1 << 7) | b2;  // 21 bits, monotone in the key
     const uint32_t kb = MSD_BITS - pbits;              // key bits of the bucket id (1..16)
     return (r.part << kb) | (code >> (21 - kb));
