@@ -706,17 +706,15 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const uint32_t prev_blk =
             Ab > doc_lo ? (uint32_t)(s_lut[(lane_u32(X.e.w, 0) >> 24) & 0x7Fu] >> 4) : 1u;
         MRG_PT(1);
+        // the next block's registers are waited for HERE, before this block's tail stores are
+        // issued: vmcnt also counts stores, so a wait placed after them would wait for their
+        // acknowledgements too
+        mid();
+        MRG_PT(0);
         if (abl & 32u) {  // timing only: classification alone
-            mid();
             my_tokens += (m0 ^ m1 ^ mh ^ prev_blk) & 1u;
             return;
         }
-        // The next block's registers are waited for right before this block's first token round:
-        // vmcnt also counts stores, so that wait also waits for the previous block's tail stores
-        // (issued before the next block's loads), and a wait after this block's own stores would
-        // wait for those too.  Placed as late as that allows, the previous stores have had the
-        // classification, staging and queue phases to complete.
-        bool settled = false;
 
 #pragma unroll
         for (uint32_t j = 0; j < NSUB; ++j) {
@@ -778,11 +776,6 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             MRG_PT(2);
             uint32_t nslow = 0;
             my_tokens += (abl & 4u) ? cnt : 0u;
-            if (!settled) {
-                mid();
-                MRG_PT(0);
-                settled = true;
-            }
             wave_sync_lds();
 
             // tokens of the queue, TWO per lane per round (entries q and q + 64: two independent LDS
@@ -904,7 +897,6 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 }
             }
         }
-        if (!settled) mid();
         MRG_PT(4);
     };
 

@@ -264,7 +264,8 @@ typename TR::R *radix_sort_t(typename TR::R *a, typename TR::R *b, uint64_t n, c
 // distinct (or fully ordered afterwards by k_fix_runs for > 16-byte keys): stability is not needed.
 constexpr int MSD_BITS = 16;
 constexpr uint32_t MSD_NB = 1u << MSD_BITS;
-constexpr int MSD_WG = 512;
+constexpr int MSD_WG = 256;
+constexpr uint32_t MSD_GRID = 1024;  // leaf workgroups (they stride over the buckets)
 constexpr uint32_t MSD_LCAP = 2048;
 constexpr uint32_t MSD_MAX_BIG = 16;
 
@@ -302,43 +303,62 @@ __global__ void k_msd_scatter(const SortRec *in, SortRec *out, uint64_t n, uint3
     out[off[msd_bucket(r, pbits)] + rank[i]] = r;
 }
 
-// one workgroup per bucket: the bucket's records through LDS, bitonic-sorted (padding sorts last);
-// an oversized bucket is only listed (big[0] = how many, big[1..] = which, up to MSD_MAX_BIG)
-__global__ __launch_bounds__(MSD_WG) void k_msd_leaf(SortRec *recs, const uint32_t *off, uint32_t lcap,
-                                                    uint32_t *big) {
+// the buckets with at least 2 records, listed (list[0] = how many): the leaf workgroups share the
+// work by list position, not by bucket id (bucket ids of text keys cluster in a few ranges)
+__global__ void k_msd_list(const uint32_t *off, uint32_t *list) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool two = b < MSD_NB && off[b + 1] - off[b] >= 2u;
+    const uint64_t m = __ballot(two);
+    if (!m) return;
+    const uint32_t lane = __lane_id(), leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&list[0], (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    if (two) list[1 + base + (uint32_t)__popcll(m & mrg_lanemask_lt())] = b;
+}
+
+// workgroups stride over the bucket list: each bucket's records through LDS, bitonic-sorted
+// (padding sorts last); an oversized bucket is only listed (big[0] = how many, big[1..] = which, up
+// to MSD_MAX_BIG)
+__global__ __launch_bounds__(MSD_WG) void k_msd_leaf(SortRec *recs, const uint32_t *off, const uint32_t *list,
+                                                    uint32_t lcap, uint32_t *big) {
     __shared__ SortRec s_r[MSD_LCAP];
-    const uint32_t b = blockIdx.x, lo = off[b], m = off[b + 1] - lo;
-    if (m <= 1) return;
-    if (m > lcap) {
-        if (threadIdx.x == 0) {
-            const uint32_t k = atomicAdd(&big[0], 1u);
-            if (k < MSD_MAX_BIG) big[1 + k] = b;
-        }
-        return;
-    }
-    uint32_t P = 2;
-    while (P < m) P <<= 1;
-    for (uint32_t i = threadIdx.x; i < P; i += MSD_WG) {
-        SortRec r;
-        if (i < m) r = recs[lo + i];
-        else r = SortRec{~0ull, ~0ull, ~0u, ~0u, 0u, 0u};
-        s_r[i] = r;
-    }
-    __syncthreads();
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t t = threadIdx.x; t < P / 2; t += MSD_WG) {
-                const uint32_t i = 2 * t - (t & (j - 1)), l = i + j;
-                const SortRec x = s_r[i], y = s_r[l];
-                if (rec_less(y, x) == ((i & k) == 0)) {
-                    s_r[i] = y;
-                    s_r[l] = x;
-                }
+    const uint32_t nl = list[0];
+    for (uint32_t x = blockIdx.x; x < nl; x += gridDim.x) {
+        const uint32_t b = list[1 + x];
+        const uint32_t lo = off[b], m = off[b + 1] - lo;
+        if (m > lcap) {
+            if (threadIdx.x == 0) {
+                const uint32_t k = atomicAdd(&big[0], 1u);
+                if (k < MSD_MAX_BIG) big[1 + k] = b;
             }
-            __syncthreads();
+            continue;
         }
+        uint32_t P = 2;
+        while (P < m) P <<= 1;
+        for (uint32_t i = threadIdx.x; i < P; i += MSD_WG) {
+            SortRec r;
+            if (i < m) r = recs[lo + i];
+            else r = SortRec{~0ull, ~0ull, ~0u, ~0u, 0u, 0u};
+            s_r[i] = r;
+        }
+        __syncthreads();
+        for (uint32_t k = 2; k <= P; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t t = threadIdx.x; t < P / 2; t += MSD_WG) {
+                    const uint32_t i = 2 * t - (t & (j - 1)), l = i + j;
+                    const SortRec x = s_r[i], y = s_r[l];
+                    if (rec_less(y, x) == ((i & k) == 0)) {
+                        s_r[i] = y;
+                        s_r[l] = x;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (uint32_t i = threadIdx.x; i < m; i += MSD_WG) recs[lo + i] = s_r[i];
+        __syncthreads();  // s_r is reused by the next bucket
     }
-    for (uint32_t i = threadIdx.x; i < m; i += MSD_WG) recs[lo + i] = s_r[i];
 }
 
 __global__ void k_pack_kv(const uint64_t *k, const uint32_t *v, uint64_t n, KV64 *out) {
@@ -365,7 +385,7 @@ void mrg_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *tmp, 
 uint64_t mrg_sort_tmp_bytes(uint64_t n) {
     const uint64_t ntiles = (n + TILE - 1) / TILE;
     const uint64_t lsd = sizeof(unsigned long long) * 24 * 256 + sizeof(uint32_t) * (256 * ntiles + scan_tmp(256 * ntiles)) + 256;
-    const uint64_t msd = sizeof(uint32_t) * (2ull * (MSD_NB + 2) + MSD_MAX_BIG + 2 + scan_tmp(MSD_NB + 1) + n) + 256;
+    const uint64_t msd = sizeof(uint32_t) * (3ull * (MSD_NB + 2) + MSD_MAX_BIG + 2 + scan_tmp(MSD_NB + 1) + n) + 256;
     return lsd + msd + 256;  // the MSD arrays, then room for an LSD sort of one oversized bucket
 }
 
@@ -376,19 +396,22 @@ SortRec *mrg_msd_sort(SortRec *a, SortRec *b, uint64_t n, uint32_t pbits, const 
     uint32_t *cnt = (uint32_t *)tmp;            // [NB + 1]
     uint32_t *off = cnt + (MSD_NB + 2);         // [NB + 1]
     uint32_t *big = off + (MSD_NB + 2);         // [1 + MAX_BIG]
-    uint32_t *stmp = big + (MSD_MAX_BIG + 2);   // scan temp
+    uint32_t *list = big + (MSD_MAX_BIG + 2);   // [1 + NB]
+    uint32_t *stmp = list + (MSD_NB + 2);       // scan temp
     uint32_t *rank = stmp + scan_tmp(MSD_NB + 1);
     // the LSD temp (histograms, tile counts) goes after the MSD arrays
     void *ltmp = (void *)(((uintptr_t)(rank + n) + 255) & ~(uintptr_t)255);
     hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (MSD_NB + 2), s);
     hipMemsetAsync(big, 0, sizeof(uint32_t), s);
+    hipMemsetAsync(list, 0, sizeof(uint32_t), s);
     const unsigned g = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(k_msd_count, dim3(g), dim3(256), 0, s, a, n, pbits, cnt, rank);
     scan_rec<uint32_t>(cnt, off, MSD_NB + 1, stmp, s);  // off[NB] = n (cnt[NB] == 0)
     hipLaunchKernelGGL(k_msd_scatter, dim3(g), dim3(256), 0, s, a, b, n, pbits, off, rank);
     uint32_t lcap = MSD_LCAP;
     if (const char *e = getenv("MRG_TEST_SORT_LCAP")) lcap = std::max<uint32_t>(1u, std::min<uint32_t>(MSD_LCAP, (uint32_t)atoi(e)));
-    hipLaunchKernelGGL(k_msd_leaf, dim3(MSD_NB), dim3(MSD_WG), 0, s, b, off, lcap, big);
+    hipLaunchKernelGGL(k_msd_list, dim3(MSD_NB / 256), dim3(256), 0, s, off, list);
+    hipLaunchKernelGGL(k_msd_leaf, dim3(MSD_GRID), dim3(MSD_WG), 0, s, b, off, list, lcap, big);
     uint32_t nb = 0;
     hipMemcpyAsync(&nb, big, sizeof nb, hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
