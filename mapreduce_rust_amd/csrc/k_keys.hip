@@ -157,6 +157,7 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
         if (IDX)
             for (int k = 0; k < BA_U; ++k) asm volatile("" : "+v"(X.d[k]));
     };
+    uint64_t abl_acc = 0;  // MRG_AGG_ABLATE (timing only): what the skipped work would have consumed
     auto sum_chunk = [&](uint32_t r, uint32_t off, const Chunk &X) {
         const uint32_t n = s_rn[r];
 #pragma unroll
@@ -164,6 +165,10 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
             const bool ok = off + 64u * k + (uint32_t)lane < n;
             const uint64_t a = X.k[k].x, c = X.k[k].y;
             const uint32_t d = IDX ? X.d[k] : MRG_EMPTY_DOC;
+            if (A.ablate) {
+                abl_acc += ok ? ((A.ablate & 2u) ? (a ^ c) : (uint64_t)ba_hash(a, c, d, A.hash_bits)) : 0u;
+                continue;
+            }
             bool ovf = false;
             if (ok) ovf = !ba_add<IDX>(s_key, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
             if (__any(ovf)) overflow(ovf, a, c, d, 1);
@@ -192,6 +197,7 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
         }
     }
 
+    if (A.ablate && abl_acc == 0x9E3779B97F4A7C15ull) atomicAdd(&A.counters[CNT_OVF2], 1ull);
     // ---- 2. this bucket's slice of every map workgroup's flushed table (a few entries each)
     for (uint32_t r = wv; r < nreg; r += BA_NW) {
         const GASK uint32_t *fo = gk(A.foff) + (uint64_t)r * (MRG_NBUCKET + 1);

@@ -142,6 +142,7 @@ struct BucketArgs {
     KeySet out;
     unsigned long long *counters;
     uint32_t hash_bits;
+    uint32_t ablate;             // timing only (MRG_AGG_ABLATE): 1 = no table adds, 2 = no hash either
 };
 void mrg_launch_bucket_agg(const BucketArgs &a, bool indexer, hipStream_t s);
 // wide (sort-based) aggregation of the map records, wc only (k_keys.hip)

@@ -405,6 +405,7 @@ void bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         B.out = c->keys.ks;
         B.counters = c->d_cnt;
         B.hash_bits = hash_bits(c);
+        B.ablate = getenv("MRG_AGG_ABLATE") ? (uint32_t)atoi(getenv("MRG_AGG_ABLATE")) : 0u;
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
         mrg_launch_bucket_agg(B, idx, s);
