@@ -26,7 +26,10 @@ inline dim3 grid_for(uint64_t n, int b = 256) { return dim3((unsigned)((n + b - 
 // current one is summed, and a record that finds its key costs one 16-byte LDS read + one LDS add.
 constexpr int BA_WG = 1024;
 constexpr int BA_NW = BA_WG / 64;
-constexpr int BA_CAP = MRG_BA_CAP;
+// LDS table slots per bucket: 6144 for wc (16-byte key + 8-byte count: 144 KiB, a third of the
+// slots free at 2^20 distinct keys, so short probe chains), 4096 for the indexer (+ 4-byte doc)
+template <bool IDX>
+constexpr uint32_t ba_cap() { return IDX ? 4096u : (uint32_t)MRG_BA_CAP; }
 constexpr int BA_PROBE = 64;
 constexpr int BA_U = 8;            // records per lane per chunk
 constexpr int BA_MAXREG = 2048;    // map workgroups (regions) the per-region size table holds
@@ -55,13 +58,16 @@ struct alignas(16) BaKey {
 template <bool IDX>
 __device__ __forceinline__ bool ba_add(BaKey *key, unsigned long long *cnt, unsigned int *doc, uint64_t a,
                                        uint64_t b, uint32_t d, uint64_t c, uint32_t h) {
-    uint32_t slot = (h >> (20 - MRG_NBUCKET_LOG2)) & (BA_CAP - 1);  // the 12 bits below the bucket bits
+    constexpr uint32_t CAP = ba_cap<IDX>();
+    // 16 hash bits below the bucket bits scaled to [0, CAP)
+    uint32_t slot = (((h >> (32 - MRG_NBUCKET_LOG2 - 16)) & 0xFFFFu) * CAP) >> 16;
     BaKey kn = key[slot];
     for (int p = 0; p < BA_PROBE; ++p) {
         const BaKey k = kn;
         // the next probe slot's key is read now, beside this one's processing (a stale EMPTY there is
         // resolved by the CAS below; a filled slot never changes)
-        const uint32_t nxt = (slot + 1u + (uint32_t)p) & (BA_CAP - 1);  // triangular steps
+        uint32_t nxt = slot + 1u + (uint32_t)p;  // triangular steps (one wrap at most: p < 64 <= CAP)
+        if (nxt >= CAP) nxt -= CAP;
         kn = key[nxt];
         const bool dk = !IDX || doc[slot] == d;
         if (k.a == a && k.b == b && dk) {
@@ -92,13 +98,14 @@ __device__ __forceinline__ bool ba_add(BaKey *key, unsigned long long *cnt, unsi
 
 template <bool IDX>
 __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
+    constexpr uint32_t BA_CAP = ba_cap<IDX>();
     __shared__ BaKey s_key[BA_CAP];
     __shared__ unsigned long long s_cnt[BA_CAP];
     __shared__ unsigned int s_doc[IDX ? BA_CAP : 1];
     __shared__ uint32_t s_rn[BA_MAXREG];  // tail records of region r in this bucket
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (int i = tid; i < BA_CAP; i += BA_WG) {
+    for (int i = tid; i < (int)BA_CAP; i += BA_WG) {
         s_key[i] = BaKey{MRG_EMPTY_K0, MRG_EMPTY_K1};
         s_cnt[i] = 0;
         if (IDX) s_doc[i] = MRG_EMPTY_DOC;
@@ -237,7 +244,7 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
         }
     }
     __syncthreads();
-    for (int i0 = 0; i0 < BA_CAP; i0 += BA_WG) {
+    for (int i0 = 0; i0 < (int)BA_CAP; i0 += BA_WG) {
         const int i = i0 + tid;
         const BaKey k = s_key[i];
         const bool full = k.a != MRG_EMPTY_K0;

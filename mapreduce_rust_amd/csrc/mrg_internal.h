@@ -17,7 +17,7 @@
 // One workgroup per bucket later sums them in LDS (k_keys.hip).
 #define MRG_NBUCKET_LOG2 9
 #define MRG_NBUCKET (1 << MRG_NBUCKET_LOG2)
-#define MRG_BA_CAP 4096          // LDS table slots of the per-bucket aggregation kernel
+#define MRG_BA_CAP 6144          // LDS table slots of the per-bucket aggregation kernel (wc; indexer 4096)
 
 // counters[] slots written by the kernels
 enum {
