@@ -7,6 +7,8 @@
 // device-scope 64-bit CAS per key word, so the table is exact without locks.  Every distinct key
 // then gets its partition SipHash-1-3(key ++ 0xFF) % nReduce (worker.rs:111-115, 129) -- once per
 // key, not per token.
+#include <type_traits>
+
 #include "mrg_device.h"
 #include "mrg_internal.h"
 
@@ -26,13 +28,15 @@ inline dim3 grid_for(uint64_t n, int b = 256) { return dim3((unsigned)((n + b - 
 // current one is summed, and a record that finds its key costs one 16-byte LDS read + one LDS add.
 constexpr int BA_WG = 1024;
 constexpr int BA_NW = BA_WG / 64;
-// LDS table slots per bucket: 6144 for wc (16-byte key + 8-byte count: 144 KiB, a third of the
-// slots free at 2^20 distinct keys, so short probe chains), 4096 for the indexer (+ 4-byte doc)
-template <bool IDX>
-constexpr uint32_t ba_cap() { return IDX ? 4096u : (uint32_t)MRG_BA_CAP; }
+// LDS table slots per bucket: wc with 32-bit counts (the job has fewer than 2^32 tokens) 7680
+// (16-byte key + 4-byte count: 150 KiB), wc with 64-bit counts 6144 (144 KiB), the indexer 4096
+// (+ 4-byte doc).  About half the slots stay free at 2^20 distinct keys over 256 buckets.
+template <bool IDX, bool C32>
+constexpr uint32_t ba_cap() { return IDX ? 4096u : (C32 ? 7680u : 6144u); }
 constexpr int BA_PROBE = 64;
 constexpr int BA_U = 8;            // records per lane per chunk
-constexpr int BA_MAXREG = 2048;    // map workgroups (regions) the per-region size table holds
+template <bool C32>
+constexpr int ba_maxreg() { return C32 ? 1024 : 2048; }  // map workgroups (regions) the size table holds
 
 #define GASK __attribute__((address_space(1)))
 template <class T>
@@ -55,10 +59,10 @@ struct alignas(16) BaKey {
 // Add c to key (a, b[, d]).  Slots fill monotonically (k0, then k1, then doc, each by CAS from its
 // empty value), so a slot whose fields all equal the key is the key's slot for good: the common case
 // is one 16-byte read and one add.  A partly claimed slot is resolved by the CAS protocol.
-template <bool IDX>
-__device__ __forceinline__ bool ba_add(BaKey *key, unsigned long long *cnt, unsigned int *doc, uint64_t a,
+template <bool IDX, bool C32, class CT>
+__device__ __forceinline__ bool ba_add(BaKey *key, CT *cnt, unsigned int *doc, uint64_t a,
                                        uint64_t b, uint32_t d, uint64_t c, uint32_t h) {
-    constexpr uint32_t CAP = ba_cap<IDX>();
+    constexpr uint32_t CAP = ba_cap<IDX, C32>();
     // 16 hash bits below the bucket bits scaled to [0, CAP)
     uint32_t slot = (((h >> (32 - MRG_NBUCKET_LOG2 - 16)) & 0xFFFFu) * CAP) >> 16;
     BaKey kn = key[slot];
@@ -71,7 +75,7 @@ __device__ __forceinline__ bool ba_add(BaKey *key, unsigned long long *cnt, unsi
         kn = key[nxt];
         const bool dk = !IDX || doc[slot] == d;
         if (k.a == a && k.b == b && dk) {
-            atomicAdd(&cnt[slot], (unsigned long long)c);
+            atomicAdd(&cnt[slot], (CT)c);
             return true;
         }
         if (k.a == MRG_EMPTY_K0 || (k.a == a && (k.b == MRG_EMPTY_K1 || (IDX && k.b == b)))) {
@@ -85,7 +89,7 @@ __device__ __forceinline__ bool ba_add(BaKey *key, unsigned long long *cnt, unsi
                         ok = (z == MRG_EMPTY_DOC || z == d);
                     }
                     if (ok) {
-                        atomicAdd(&cnt[slot], (unsigned long long)c);
+                        atomicAdd(&cnt[slot], (CT)c);
                         return true;
                     }
                 }
@@ -96,13 +100,14 @@ __device__ __forceinline__ bool ba_add(BaKey *key, unsigned long long *cnt, unsi
     return false;
 }
 
-template <bool IDX>
+template <bool IDX, bool C32>
 __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
-    constexpr uint32_t BA_CAP = ba_cap<IDX>();
+    constexpr uint32_t BA_CAP = ba_cap<IDX, C32>();
+    using CT = typename std::conditional<C32, unsigned int, unsigned long long>::type;
     __shared__ BaKey s_key[BA_CAP];
-    __shared__ unsigned long long s_cnt[BA_CAP];
+    __shared__ CT s_cnt[BA_CAP];
     __shared__ unsigned int s_doc[IDX ? BA_CAP : 1];
-    __shared__ uint32_t s_rn[BA_MAXREG];  // tail records of region r in this bucket
+    __shared__ uint32_t s_rn[ba_maxreg<C32>()];  // tail records of region r in this bucket
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int i = tid; i < (int)BA_CAP; i += BA_WG) {
@@ -177,7 +182,7 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
                 continue;
             }
             bool ovf = false;
-            if (ok) ovf = !ba_add<IDX>(s_key, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
+            if (ok) ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
             if (__any(ovf)) overflow(ovf, a, c, d, 1);
         }
     };
@@ -220,7 +225,7 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
                 c = gk(A.fk1)[reg + k];
                 n2 = gk(A.fcnt)[reg + k];
                 if (IDX) d = gk(A.fdoc)[reg + k];
-                ovf = !ba_add<IDX>(s_key, s_cnt, s_doc, a, c, d, n2, ba_hash(a, c, d, A.hash_bits));
+                ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, a, c, d, n2, ba_hash(a, c, d, A.hash_bits));
             }
             if (__any(ovf)) overflow(ovf, a, c, d, n2);
         }
@@ -238,16 +243,16 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
                 a = src[(uint64_t)i * RW];
                 c = src[(uint64_t)i * RW + 1];
                 if (IDX) d = (uint32_t)src[(uint64_t)i * RW + 2];
-                ovf = !ba_add<IDX>(s_key, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
+                ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
             }
             if (__any(ovf)) overflow(ovf, a, c, d, 1);
         }
     }
     __syncthreads();
-    for (int i0 = 0; i0 < (int)BA_CAP; i0 += BA_WG) {
-        const int i = i0 + tid;
+    for (int i0 = 0; i0 < (int)BA_CAP; i0 += BA_WG) {  // BA_CAP need not be a multiple of BA_WG
+        const int i = min(i0 + tid, (int)BA_CAP - 1);
         const BaKey k = s_key[i];
-        const bool full = k.a != MRG_EMPTY_K0;
+        const bool full = i0 + tid < (int)BA_CAP && k.a != MRG_EMPTY_K0;
         const uint64_t j = mrg_wave_append(&A.counters[CNT_KEYS], full);
         if (full) {
             gk(A.out.k0)[j] = k.a;
@@ -547,9 +552,10 @@ __global__ void k_iota(uint32_t *p, uint64_t n) {
 
 }  // namespace
 
-void mrg_launch_bucket_agg(const BucketArgs &a, bool indexer, hipStream_t s) {
-    if (indexer) hipLaunchKernelGGL(k_bucket_agg<true>, dim3(MRG_NBUCKET), dim3(BA_WG), 0, s, a);
-    else hipLaunchKernelGGL(k_bucket_agg<false>, dim3(MRG_NBUCKET), dim3(BA_WG), 0, s, a);
+void mrg_launch_bucket_agg(const BucketArgs &a, bool indexer, bool count32, hipStream_t s) {
+    if (indexer) hipLaunchKernelGGL((k_bucket_agg<true, false>), dim3(MRG_NBUCKET), dim3(BA_WG), 0, s, a);
+    else if (count32) hipLaunchKernelGGL((k_bucket_agg<false, true>), dim3(MRG_NBUCKET), dim3(BA_WG), 0, s, a);
+    else hipLaunchKernelGGL((k_bucket_agg<false, false>), dim3(MRG_NBUCKET), dim3(BA_WG), 0, s, a);
 }
 
 void mrg_launch_table_clear(const TableArgs &t, bool indexer, hipStream_t s) {

@@ -15,9 +15,11 @@
 // Tail records (LDS-table misses) are bucketed by key hash into MRG_NBUCKET buckets; every
 // (bucket, map workgroup) pair owns a private region of the pool, so appending is an LDS atomic.
 // One workgroup per bucket later sums them in LDS (k_keys.hip).
-#define MRG_NBUCKET_LOG2 9
+#ifndef MRG_NBUCKET_LOG2
+#define MRG_NBUCKET_LOG2 8  // 256: half the open tail lines of 512 (map 8.1 -> 7.5 ms at C3)
+#endif
 #define MRG_NBUCKET (1 << MRG_NBUCKET_LOG2)
-#define MRG_BA_CAP 6144          // LDS table slots of the per-bucket aggregation kernel (wc; indexer 4096)
+#define MRG_BA_CAP 7680          // max LDS table slots of the per-bucket aggregation kernel (k_keys.hip ba_cap)
 
 // counters[] slots written by the kernels
 enum {
@@ -144,7 +146,8 @@ struct BucketArgs {
     uint32_t hash_bits;
     uint32_t ablate;             // timing only (MRG_AGG_ABLATE): 1 = no table adds, 2 = no hash either
 };
-void mrg_launch_bucket_agg(const BucketArgs &a, bool indexer, hipStream_t s);
+// count32: the job has fewer than 2^32 tokens (32-bit LDS counts, a larger table); nreg <= 1024 then
+void mrg_launch_bucket_agg(const BucketArgs &a, bool indexer, bool count32, hipStream_t s);
 // wide (sort-based) aggregation of the map records, wc only (k_keys.hip)
 struct SortRec;
 void mrg_launch_wide_counts(const BucketArgs &a, uint64_t *cnt, uint64_t nseg, hipStream_t s);

@@ -383,7 +383,10 @@ struct MapBufs {
 
 // Map-side records: per-bucket LDS aggregation of tail chunks + flushed map tables, exact overflow
 // through the HBM table, then the long keys.
-void bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap, LongItems li) {
+// Returns false (nothing aggregated) when far more keys miss the per-bucket tables than the overflow
+// path handles well (millions of distinct keys without the tail share that selects the wide path up
+// front): the caller then runs the wide aggregation on the same map output.
+bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap, LongItems li) {
     if (nreg > 2048) raise(MRG_EINVAL, "internal: %u map workgroups exceed the aggregation's region table", nreg);
     Pool &p = c->pool;
     hipStream_t s = c->stream;
@@ -408,12 +411,20 @@ void bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         B.ablate = getenv("MRG_AGG_ABLATE") ? (uint32_t)atoi(getenv("MRG_AGG_ABLATE")) : 0u;
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
-        mrg_launch_bucket_agg(B, idx, s);
+        // 32-bit LDS counts (larger table) when no key can reach 2^32: fewer tokens than that
+        const bool c32 = c->h_cnt[CNT_TOKENS] < 0xFFFFFFFFull && nreg <= 1024;
+        mrg_launch_bucket_agg(B, idx, c32, s);
         read_counters(c);
         const uint64_t novf = c->h_cnt[CNT_OVF2];
         if (getenv("MRG_DEBUG"))
             fprintf(stderr, "[mrgpu] bucket agg: %llu keys, %llu overflow records (cap %llu)\n",
                     (unsigned long long)c->h_cnt[CNT_KEYS], (unsigned long long)novf, (unsigned long long)ocap);
+        const char *wenv = getenv("MRG_WIDE");  // MRG_WIDE=0 pins the bucket path (tests of its overflow)
+        if (!idx && novf > env_u64("MRG_TEST_AGG_WIDE_OVF", 4ull << 20) && !(wenv && atoi(wenv) == 0)) {
+            p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
+            if (getenv("MRG_DEBUG")) fprintf(stderr, "[mrgpu] bucket agg: %llu overflow records -> wide\n", (unsigned long long)novf);
+            return false;
+        }
         if (novf > ocap) {  // overflow list too small: grow (remembered) and run again
             p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
             ocap = c->ovf_hint = novf + novf / 8 + 1024;
@@ -431,6 +442,7 @@ void bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
     }
     long_aggregate(c, li);
     finish_keys(c);
+    return true;
 }
 
 uint32_t bytes_for(uint64_t maxval) {
@@ -944,8 +956,7 @@ void job_map(mrg_ctx *c) {
     // high cardinality (most tokens missed the map-side combine): sort-based aggregation
     bool wide = !idx && c->h_cnt[CNT_REC] > (32ull << 20) && 2 * c->h_cnt[CNT_REC] > c->h_cnt[CNT_TOKENS];
     if (const char *v = getenv("MRG_WIDE")) wide = !idx && atoi(v) != 0;  // test / tuning override
-    if (wide) wide_aggregate(c, A, (uint32_t)grid, cap, li);
-    else bucket_aggregate(c, A, (uint32_t)grid, cap, li);
+    if (wide || !bucket_aggregate(c, A, (uint32_t)grid, cap, li)) wide_aggregate(c, A, (uint32_t)grid, cap, li);
     ev_rec(c, 3);
     release_map();
     c->st.ms_aggregate = ev_ms(c, 2, 3);

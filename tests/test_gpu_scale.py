@@ -109,7 +109,7 @@ def test_c5_slice_vs_oracle(ctx):
 @pytest.fixture
 def knobs():
     keys = ["MRG_TEST_TAIL_CAP", "MRG_TEST_OVF_CAP", "MRG_TEST_AGG_OCAP", "MRG_WIDE", "MRG_TEST_LEAF_CAP",
-            "MRG_TEST_LEAF_TARGET", "MRG_TEST_SORT_LCAP"]
+            "MRG_TEST_LEAF_TARGET", "MRG_TEST_SORT_LCAP", "MRG_TEST_AGG_WIDE_OVF"]
     saved = {k: os.environ.get(k) for k in keys}
 
     def set_(**kw):
@@ -178,6 +178,21 @@ def test_key_sort_buckets_vs_oracle(ctx, corpus, knobs, lcap):
     assert run_wc(ctx, corpus, 10, flags=M.debug_hash_bits(4)) == O.wc(corpus, 10, O.FAST)
     names = [f"data/gut-{m}.txt" for m in range(6)]
     assert run_wc(ctx, corpus, 10, app=M.APP_INDEXER, names=names) == O.indexer(corpus, names, 10)
+
+
+def test_bucket_overflow_falls_back_to_wide_vs_oracle(ctx, corpus, knobs):
+    """Far more keys missing the per-bucket LDS tables than the overflow path handles well (every
+    key in 16 buckets through 4-bit internal hashes; threshold lowered from 4 Mi overflow records to
+    100): the bucket aggregation gives up and the wide (sort-based) aggregation runs on the same map
+    output.  Output equals the oracle's."""
+    import mapreduce_rust_amd as M
+    import oracle_lib as O
+    from gpu_util import run_wc
+    knobs(MRG_TEST_AGG_WIDE_OVF=100)
+    for R in (1, 10):
+        got = run_wc(ctx, corpus, R, flags=M.debug_hash_bits(4))
+        assert ctx.stats()["agg_launches"] == 0  # no completed bucket aggregation: the wide path ran
+        assert got == O.wc(corpus, R, O.FAST), R
 
 
 def test_library_shuffle_single_rank(ctx, corpus):
