@@ -7,6 +7,7 @@
 // device-scope 64-bit CAS per key word, so the table is exact without locks.  Every distinct key
 // then gets its partition SipHash-1-3(key ++ 0xFF) % nReduce (worker.rs:111-115, 129) -- once per
 // key, not per token.
+#include <algorithm>
 #include <type_traits>
 
 #include "mrg_device.h"
@@ -115,7 +116,10 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
         s_cnt[i] = 0;
         if (IDX) s_doc[i] = MRG_EMPTY_DOC;
     }
-    const uint32_t b = blockIdx.x;
+    // workgroup (b, j): bucket b, hash sub-range j of A.nsub (a bucket with more distinct keys than one
+    // table holds is summed by nsub workgroups, each reading all of its records and keeping its range)
+    const uint32_t b = blockIdx.x % MRG_NBUCKET, jsub = blockIdx.x / MRG_NBUCKET, nsub = A.nsub;
+    auto mine = [&](uint32_t h) { return nsub <= 1u || (((h & 0xFFu) * nsub) >> 8) == jsub; };
     constexpr uint32_t RW = IDX ? 3u : 2u;
     const uint32_t cap = gk(A.bcap)[b];
     const uint32_t nreg = A.nreg;
@@ -182,7 +186,8 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
                 continue;
             }
             bool ovf = false;
-            if (ok) ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
+            const uint32_t h = ba_hash(a, c, d, A.hash_bits);
+            if (ok && mine(h)) ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, a, c, d, 1ull, h);
             if (__any(ovf)) overflow(ovf, a, c, d, 1);
         }
     };
@@ -225,7 +230,8 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
                 c = gk(A.fk1)[reg + k];
                 n2 = gk(A.fcnt)[reg + k];
                 if (IDX) d = gk(A.fdoc)[reg + k];
-                ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, a, c, d, n2, ba_hash(a, c, d, A.hash_bits));
+                const uint32_t h = ba_hash(a, c, d, A.hash_bits);
+                if (mine(h)) ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, a, c, d, n2, h);
             }
             if (__any(ovf)) overflow(ovf, a, c, d, n2);
         }
@@ -243,7 +249,8 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
                 a = src[(uint64_t)i * RW];
                 c = src[(uint64_t)i * RW + 1];
                 if (IDX) d = (uint32_t)src[(uint64_t)i * RW + 2];
-                ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, a, c, d, 1ull, ba_hash(a, c, d, A.hash_bits));
+                const uint32_t h = ba_hash(a, c, d, A.hash_bits);
+                if (mine(h)) ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, a, c, d, 1ull, h);
             }
             if (__any(ovf)) overflow(ovf, a, c, d, 1);
         }
@@ -254,7 +261,7 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
         const BaKey k = s_key[i];
         const bool full = i0 + tid < (int)BA_CAP && k.a != MRG_EMPTY_K0;
         const uint64_t j = mrg_wave_append(&A.counters[CNT_KEYS], full);
-        if (full) {
+        if (full && j < A.kcap) {
             gk(A.out.k0)[j] = k.a;
             gk(A.out.k1)[j] = k.b;
             gk(A.out.cnt)[j] = s_cnt[i];
@@ -553,9 +560,10 @@ __global__ void k_iota(uint32_t *p, uint64_t n) {
 }  // namespace
 
 void mrg_launch_bucket_agg(const BucketArgs &a, bool indexer, bool count32, hipStream_t s) {
-    if (indexer) hipLaunchKernelGGL((k_bucket_agg<true, false>), dim3(MRG_NBUCKET), dim3(BA_WG), 0, s, a);
-    else if (count32) hipLaunchKernelGGL((k_bucket_agg<false, true>), dim3(MRG_NBUCKET), dim3(BA_WG), 0, s, a);
-    else hipLaunchKernelGGL((k_bucket_agg<false, false>), dim3(MRG_NBUCKET), dim3(BA_WG), 0, s, a);
+    const dim3 g(MRG_NBUCKET * std::max<uint32_t>(a.nsub, 1u));
+    if (indexer) hipLaunchKernelGGL((k_bucket_agg<true, false>), g, dim3(BA_WG), 0, s, a);
+    else if (count32) hipLaunchKernelGGL((k_bucket_agg<false, true>), g, dim3(BA_WG), 0, s, a);
+    else hipLaunchKernelGGL((k_bucket_agg<false, false>), g, dim3(BA_WG), 0, s, a);
 }
 
 void mrg_launch_table_clear(const TableArgs &t, bool indexer, hipStream_t s) {

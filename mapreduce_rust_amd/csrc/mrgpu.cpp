@@ -185,6 +185,7 @@ struct mrg_ctx {
     int lds_cap = 4096;
     int map_grid = 0;
     uint64_t long_hint = 0, ovf_hint = 0;
+    uint32_t agg_nsub = 1;  // bucket-aggregation workgroups per bucket (grown when the tables overflow)
     std::vector<double> bcap_rate;  // tail records per (bucket, map workgroup) per input byte of the workgroup
     uint64_t ocap_hint = 0;         // records per bucket overflow list
     // job
@@ -394,9 +395,12 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
     uint64_t ocap = std::max<uint64_t>(c->ovf_hint, 1u << 20);
     if (const uint64_t t = env_u64("MRG_TEST_AGG_OCAP", 0)) ocap = t;  // test knob: force the regrow path
     uint32_t agg_launches = 0;
+    uint32_t nsub = c->agg_nsub;
+    if (const uint64_t t = env_u64("MRG_TEST_AGG_NSUB", 0)) nsub = (uint32_t)t;
     for (;;) {
         ++agg_launches;
-        keys_reserve(c, (uint64_t)MRG_NBUCKET * MRG_BA_CAP + ocap + li.n + 1);
+        // every workgroup (bucket, sub-range) may emit a full table of keys
+        keys_reserve(c, (uint64_t)MRG_NBUCKET * std::max<uint32_t>(nsub, 1u) * MRG_BA_CAP + ocap + li.n + 1);
         BucketArgs B{};
         B.pool = A.pool; B.rbase = A.rbase; B.bcap = A.bcap; B.bcount = A.bcount;
         B.movf = A.ovf; B.monext = A.onext; B.mocap = A.ocap;
@@ -409,18 +413,33 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         B.counters = c->d_cnt;
         B.hash_bits = hash_bits(c);
         B.ablate = getenv("MRG_AGG_ABLATE") ? (uint32_t)atoi(getenv("MRG_AGG_ABLATE")) : 0u;
+        B.nsub = nsub;
+        B.kcap = c->keys.cap;
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
         // 32-bit LDS counts (larger table) when no key can reach 2^32: fewer tokens than that
         const bool c32 = c->h_cnt[CNT_TOKENS] < 0xFFFFFFFFull && nreg <= 1024;
         mrg_launch_bucket_agg(B, idx, c32, s);
         read_counters(c);
+        if (c->h_cnt[CNT_KEYS] > c->keys.cap)
+            raise(MRG_EINVAL, "internal: bucket aggregation emitted %llu keys for %llu slots",
+                  (unsigned long long)c->h_cnt[CNT_KEYS], (unsigned long long)c->keys.cap);
         const uint64_t novf = c->h_cnt[CNT_OVF2];
         if (getenv("MRG_DEBUG"))
             fprintf(stderr, "[mrgpu] bucket agg: %llu keys, %llu overflow records (cap %llu)\n",
                     (unsigned long long)c->h_cnt[CNT_KEYS], (unsigned long long)novf, (unsigned long long)ocap);
+        // Many keys missed the tables (more distinct keys per bucket than a table holds): split every
+        // bucket over more workgroups (each reads the whole bucket and keeps one hash sub-range), up
+        // to 16; the count is remembered by the context.  Beyond that, the wide aggregation.
+        const uint64_t heavy = env_u64("MRG_TEST_AGG_WIDE_OVF", 4ull << 20);
+        if (novf > heavy && nsub < 16 && !env_u64("MRG_TEST_AGG_NSUB", 0)) {
+            p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
+            nsub = c->agg_nsub = std::min<uint32_t>(16, 2 * nsub);  // overflow counts records, not keys: double
+            if (getenv("MRG_DEBUG")) fprintf(stderr, "[mrgpu] bucket agg: %llu overflow records -> %u workgroups per bucket\n", (unsigned long long)novf, nsub);
+            continue;
+        }
         const char *wenv = getenv("MRG_WIDE");  // MRG_WIDE=0 pins the bucket path (tests of its overflow)
-        if (!idx && novf > env_u64("MRG_TEST_AGG_WIDE_OVF", 4ull << 20) && !(wenv && atoi(wenv) == 0)) {
+        if (!idx && novf > heavy && !(wenv && atoi(wenv) == 0)) {
             p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
             if (getenv("MRG_DEBUG")) fprintf(stderr, "[mrgpu] bucket agg: %llu overflow records -> wide\n", (unsigned long long)novf);
             return false;
@@ -438,6 +457,10 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
         c->st.overflow_keys = novf;
         c->st.agg_launches = agg_launches;
+        {  // the next job's workgroups per bucket: enough sub-ranges for this job's key count
+            const uint64_t per = (uint64_t)MRG_NBUCKET * 4096u;
+            c->agg_nsub = (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, (c->h_cnt[CNT_KEYS] + per - 1) / per));
+        }
         break;
     }
     long_aggregate(c, li);

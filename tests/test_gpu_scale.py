@@ -109,7 +109,7 @@ def test_c5_slice_vs_oracle(ctx):
 @pytest.fixture
 def knobs():
     keys = ["MRG_TEST_TAIL_CAP", "MRG_TEST_OVF_CAP", "MRG_TEST_AGG_OCAP", "MRG_WIDE", "MRG_TEST_LEAF_CAP",
-            "MRG_TEST_LEAF_TARGET", "MRG_TEST_SORT_LCAP", "MRG_TEST_AGG_WIDE_OVF"]
+            "MRG_TEST_LEAF_TARGET", "MRG_TEST_SORT_LCAP", "MRG_TEST_AGG_WIDE_OVF", "MRG_TEST_AGG_NSUB"]
     saved = {k: os.environ.get(k) for k in keys}
 
     def set_(**kw):
@@ -180,11 +180,27 @@ def test_key_sort_buckets_vs_oracle(ctx, corpus, knobs, lcap):
     assert run_wc(ctx, corpus, 10, app=M.APP_INDEXER, names=names) == O.indexer(corpus, names, 10)
 
 
+@pytest.mark.parametrize("nsub", ["2", "3", "16"])
+def test_bucket_subranges_vs_oracle(ctx, corpus, knobs, nsub):
+    """Every bucket summed by nsub workgroups, each reading all of the bucket's records and keeping
+    one hash sub-range (the path of buckets with more distinct keys than one LDS table holds)."""
+    import torch
+    import oracle_lib as O
+    from gpu_util import run_wc
+    n = 8 * MIB
+    t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
+    ctx.gen_zipf(t.data_ptr(), n, 0x5EED2026, 3, 1 << 18, 1.1)
+    docs = corpus + [t[:n].cpu().numpy().tobytes()]
+    knobs(MRG_TEST_AGG_NSUB=nsub, MRG_WIDE=0)
+    assert run_wc(ctx, docs, 10) == O.wc(docs, 10, O.FAST)
+
+
 def test_bucket_overflow_falls_back_to_wide_vs_oracle(ctx, corpus, knobs):
     """Far more keys missing the per-bucket LDS tables than the overflow path handles well (every
     key in 16 buckets through 4-bit internal hashes; threshold lowered from 4 Mi overflow records to
-    100): the bucket aggregation gives up and the wide (sort-based) aggregation runs on the same map
-    output.  Output equals the oracle's."""
+    100): the bucket aggregation splits buckets over up to 16 workgroups each, still overflows, and
+    gives up: the wide (sort-based) aggregation runs on the same map output.  Output equals the
+    oracle's."""
     import mapreduce_rust_amd as M
     import oracle_lib as O
     from gpu_util import run_wc
