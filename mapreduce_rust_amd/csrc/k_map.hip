@@ -647,6 +647,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
 #ifdef MRG_MAP_PROF
     const bool P = A.prof != nullptr;
     uint64_t pacc[7] = {0, 0, 0, 0, 0, 0, 0}, tl = P ? clock64() : 0;
+    const uint64_t wg_t0 = wall_clock64();  // workgroup start/end (100 MHz): load balance across CUs
 #define MRG_PT(i)                          \
     if (P) {                               \
         const uint64_t t_ = clock64();     \
@@ -1020,6 +1021,10 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
 #ifdef MRG_MAP_PROF
     if (P && lane == 0) {
         for (int i = 0; i < 7; ++i) g_add(&A.prof[i], (unsigned long long)pacc[i]);
+    }
+    if (P && tid == 0) {
+        gp(A.prof)[8 + 2 * blockIdx.x] = wg_t0;
+        gp(A.prof)[9 + 2 * blockIdx.x] = wall_clock64();
     }
 #endif
 }

@@ -901,8 +901,8 @@ void job_map(mrg_ctx *c) {
         A.ablate = getenv("MRG_ABLATE") ? (uint32_t)atoi(getenv("MRG_ABLATE")) : 0u;
         A.prof = nullptr;
         if (getenv("MRG_PROF")) {
-            M.prof = pget<unsigned long long>(p, 8);
-            HIPCHK(hipMemsetAsync(M.prof, 0, 64, s));
+            M.prof = pget<unsigned long long>(p, 8 + 2ull * grid);
+            HIPCHK(hipMemsetAsync(M.prof, 0, 8ull * (8 + 2ull * grid), s));
             A.prof = M.prof;
         }
         HIPCHK(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long) * CNT_N, s));
@@ -927,6 +927,26 @@ void job_map(mrg_ctx *c) {
             fprintf(stderr, "[mrgpu] map phase clocks (sum over waves %.3e):", tot);
             for (int i = 0; i < 7; ++i) fprintf(stderr, " %s %.1f%%", nm[i], 100.0 * (double)pr[i] / (tot > 0 ? tot : 1));
             fprintf(stderr, "\n");
+            // workgroup start/end wall clocks (100 MHz; written by -DMRG_MAP_PROF builds only)
+            std::vector<unsigned long long> wt(2ull * grid);
+            HIPCHK(hipMemcpy(wt.data(), M.prof + 8, 8ull * wt.size(), hipMemcpyDeviceToHost));
+            if (wt[1]) {
+                unsigned long long t0 = ~0ull, t1 = 0, ls = 0;
+                std::vector<double> dur(grid), end(grid);
+                for (int g = 0; g < grid; ++g) t0 = std::min(t0, wt[2 * g]);
+                for (int g = 0; g < grid; ++g) {
+                    t1 = std::max(t1, wt[2 * g + 1]);
+                    ls = std::max(ls, wt[2 * g]);
+                    dur[g] = (double)(wt[2 * g + 1] - wt[2 * g]) * 1e-5;
+                    end[g] = (double)(wt[2 * g + 1] - t0) * 1e-5;
+                }
+                std::sort(dur.begin(), dur.end());
+                std::sort(end.begin(), end.end());
+                fprintf(stderr, "[mrgpu] map workgroups (ms): span %.3f, end min %.3f med %.3f max %.3f, "
+                        "duration min %.3f med %.3f max %.3f, last start %.3f\n", (double)(t1 - t0) * 1e-5,
+                        end[0], end[grid / 2], end[grid - 1], dur[0], dur[grid / 2], dur[grid - 1],
+                        (double)(ls - t0) * 1e-5);
+            }
         }
         const uint64_t nl = c->h_cnt[CNT_LONG];
         if (c->h_cnt[CNT_OVF] == 0 && nl <= lcap) break;
