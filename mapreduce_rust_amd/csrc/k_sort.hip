@@ -255,18 +255,22 @@ typename TR::R *radix_sort_t(typename TR::R *a, typename TR::R *b, uint64_t n, c
 // ------------------------------------------------------------------ MSD bucket sort of SortRecs
 // The distinct keys of a job (~1e6) sorted by (part, k0, k1, doc) in three passes instead of up to
 // 13 LSD passes: every record takes a bucket = (part, leading key bits) and its rank inside the
-// bucket from one global atomic; the buckets' offsets are scanned; records are scattered; each bucket
-// of at most MSD_LCAP records is then sorted in LDS by one workgroup (bitonic network over whole
-// records).  The key bits of the bucket id come from the first three key bytes clamped to 7 bits
-// (monotone: every byte >= 0x7F maps to 0x7F), so text keys, whose bytes leave the top bit unused,
-// spread over the buckets.  A few oversized buckets are sorted by the LSD radix sort on their own
-// segments; many of them (a skewed key set) send the whole array through the LSD sort.  Keys are
-// distinct (or fully ordered afterwards by k_fix_runs for > 16-byte keys): stability is not needed.
-constexpr int MSD_BITS = 16;
+// bucket from one global atomic; the buckets' offsets are scanned; records are scattered; then each
+// bucket is sorted on its own: buckets of at most 64 records by ONE WAVE (rank by comparison with
+// every record of the bucket, broadcast from its lane: no LDS, no barrier -- with 2^20 bucket ids
+// most buckets of text keys are this small), larger ones of at most MSD_LCAP records by one
+// workgroup (bitonic network over whole records in LDS).  The key bits of the bucket id come from
+// the first three key bytes clamped to 7 bits (monotone: every byte >= 0x7F maps to 0x7F), so text
+// keys, whose bytes leave the top bit unused, spread over the buckets.  A few oversized buckets are
+// sorted by the LSD radix sort on their own segments; many of them (a skewed key set) send the whole
+// array through the LSD sort.  Records compare by (part, k0, k1, doc, idx): idx is unique, so the
+// order is total even for > 16-byte keys with equal prefixes (k_fix_runs orders those afterwards).
+constexpr int MSD_BITS = 20;
 constexpr uint32_t MSD_NB = 1u << MSD_BITS;
 constexpr int MSD_WG = 256;
-constexpr uint32_t MSD_GRID = 1024;  // leaf workgroups (they stride over the buckets)
+constexpr uint32_t MSD_GRID = 1024;  // leaf workgroups (they stride over the bucket lists)
 constexpr uint32_t MSD_LCAP = 2048;
+constexpr uint32_t MSD_SMALL = 64;   // buckets sorted by one wave
 constexpr uint32_t MSD_MAX_BIG = 16;
 
 __device__ __forceinline__ uint32_t msd_bucket(const SortRec &r, uint32_t pbits) {
@@ -278,7 +282,7 @@ __device__ __forceinline__ uint32_t msd_bucket(const SortRec &r, uint32_t pbits)
     const uint32_t b1 = b0 == 127u ? 127u : min(c1, 127u);
     const uint32_t b2 = b1 == 127u ? 127u : min(c2, 127u);
     const uint32_t code = (b0 << 14) | (b1 << 7) | b2;  // 21 bits, monotone in the key
-    const uint32_t kb = MSD_BITS - pbits;              // key bits of the bucket id (1..16)
+    const uint32_t kb = MSD_BITS - pbits;              // key bits of the bucket id (1..20)
     return (r.part << kb) | (code >> (21 - kb));
 }
 
@@ -286,7 +290,8 @@ __device__ __forceinline__ bool rec_less(const SortRec &a, const SortRec &b) {
     if (a.part != b.part) return a.part < b.part;
     if (a.k0 != b.k0) return a.k0 < b.k0;
     if (a.k1 != b.k1) return a.k1 < b.k1;
-    return a.doc < b.doc;
+    if (a.doc != b.doc) return a.doc < b.doc;
+    return a.idx < b.idx;
 }
 
 __global__ void k_msd_count(const SortRec *in, uint64_t n, uint32_t pbits, uint32_t *cnt, uint32_t *rank) {
@@ -303,21 +308,55 @@ __global__ void k_msd_scatter(const SortRec *in, SortRec *out, uint64_t n, uint3
     out[off[msd_bucket(r, pbits)] + rank[i]] = r;
 }
 
-// the buckets with at least 2 records, listed (list[0] = how many): the leaf workgroups share the
-// work by list position, not by bucket id (bucket ids of text keys cluster in a few ranges)
-__global__ void k_msd_list(const uint32_t *off, uint32_t *list) {
+// The buckets with at least 2 records, listed (list[0] = how many): at most `small` records in
+// list (one wave each), more in list2 (one workgroup each).  The leaf kernels share the work by list
+// position, not by bucket id (bucket ids of text keys cluster in a few ranges).
+__global__ void k_msd_list(const uint32_t *off, uint32_t small, uint32_t *list, uint32_t *list2) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool two = b < MSD_NB && off[b + 1] - off[b] >= 2u;
-    const uint64_t m = __ballot(two);
-    if (!m) return;
-    const uint32_t lane = __lane_id(), leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&list[0], (uint32_t)__popcll(m));
-    base = __shfl(base, (int)leader);
-    if (two) list[1 + base + (uint32_t)__popcll(m & mrg_lanemask_lt())] = b;
+    const uint32_t m = b < MSD_NB ? off[b + 1] - off[b] : 0u;
+    const uint32_t lane = __lane_id();
+    auto put = [&](bool pred, uint32_t *l) {
+        const uint64_t msk = __ballot(pred);
+        if (!msk) return;
+        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)msk) - 1u;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&l[0], (uint32_t)__popcll(msk));
+        base = __shfl(base, (int)leader);
+        if (pred) l[1 + base + (uint32_t)__popcll(msk & mrg_lanemask_lt())] = b;
+    };
+    put(m >= 2u && m <= small, list);
+    put(m > small, list2);
 }
 
-// workgroups stride over the bucket list: each bucket's records through LDS, bitonic-sorted
+// One wave per small bucket (m <= 64): lane i holds record i; its rank = the records of the bucket
+// that order before it (each broadcast from its lane in turn; idx makes the order total), then every
+// record is stored at its rank.
+__global__ __launch_bounds__(MSD_WG) void k_msd_leaf_small(SortRec *recs, const uint32_t *off, const uint32_t *list) {
+    const uint32_t nl = list[0];
+    const uint32_t lane = __lane_id();
+    const uint32_t nw = gridDim.x * (MSD_WG / 64);
+    for (uint32_t x = blockIdx.x * (MSD_WG / 64) + (threadIdx.x >> 6); x < nl; x += nw) {
+        const uint32_t b = list[1 + x];
+        const uint32_t lo = off[b], m = off[b + 1] - lo;
+        SortRec r{};
+        if (lane < m) r = recs[lo + lane];
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < m; ++j) {
+            SortRec o;
+            o.k0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(r.k0 >> 32), (int)j) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)r.k0, (int)j);
+            o.k1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(r.k1 >> 32), (int)j) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)r.k1, (int)j);
+            o.part = (uint32_t)__builtin_amdgcn_readlane((int)r.part, (int)j);
+            o.doc = (uint32_t)__builtin_amdgcn_readlane((int)r.doc, (int)j);
+            o.idx = (uint32_t)__builtin_amdgcn_readlane((int)r.idx, (int)j);
+            rank += rec_less(o, r) ? 1u : 0u;
+        }
+        if (lane < m) recs[lo + rank] = r;
+    }
+}
+
+// workgroups stride over the large-bucket list: each bucket's records through LDS, bitonic-sorted
 // (padding sorts last); an oversized bucket is only listed (big[0] = how many, big[1..] = which, up
 // to MSD_MAX_BIG)
 __global__ __launch_bounds__(MSD_WG) void k_msd_leaf(SortRec *recs, const uint32_t *off, const uint32_t *list,
@@ -339,7 +378,7 @@ __global__ __launch_bounds__(MSD_WG) void k_msd_leaf(SortRec *recs, const uint32
         for (uint32_t i = threadIdx.x; i < P; i += MSD_WG) {
             SortRec r;
             if (i < m) r = recs[lo + i];
-            else r = SortRec{~0ull, ~0ull, ~0u, ~0u, 0u, 0u};
+            else r = SortRec{~0ull, ~0ull, ~0u, ~0u, ~0u, 0u};
             s_r[i] = r;
         }
         __syncthreads();
@@ -385,7 +424,7 @@ void mrg_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *tmp, 
 uint64_t mrg_sort_tmp_bytes(uint64_t n) {
     const uint64_t ntiles = (n + TILE - 1) / TILE;
     const uint64_t lsd = sizeof(unsigned long long) * 24 * 256 + sizeof(uint32_t) * (256 * ntiles + scan_tmp(256 * ntiles)) + 256;
-    const uint64_t msd = sizeof(uint32_t) * (3ull * (MSD_NB + 2) + MSD_MAX_BIG + 2 + scan_tmp(MSD_NB + 1) + n) + 256;
+    const uint64_t msd = sizeof(uint32_t) * (4ull * (MSD_NB + 2) + MSD_MAX_BIG + 2 + scan_tmp(MSD_NB + 1) + n) + 256;
     return lsd + msd + 256;  // the MSD arrays, then room for an LSD sort of one oversized bucket
 }
 
@@ -396,22 +435,25 @@ SortRec *mrg_msd_sort(SortRec *a, SortRec *b, uint64_t n, uint32_t pbits, const 
     uint32_t *cnt = (uint32_t *)tmp;            // [NB + 1]
     uint32_t *off = cnt + (MSD_NB + 2);         // [NB + 1]
     uint32_t *big = off + (MSD_NB + 2);         // [1 + MAX_BIG]
-    uint32_t *list = big + (MSD_MAX_BIG + 2);   // [1 + NB]
-    uint32_t *stmp = list + (MSD_NB + 2);       // scan temp
+    uint32_t *list = big + (MSD_MAX_BIG + 2);   // [1 + NB] buckets of 2..small records
+    uint32_t *list2 = list + (MSD_NB + 2);      // [1 + NB] larger buckets
+    uint32_t *stmp = list2 + (MSD_NB + 2);      // scan temp
     uint32_t *rank = stmp + scan_tmp(MSD_NB + 1);
     // the LSD temp (histograms, tile counts) goes after the MSD arrays
     void *ltmp = (void *)(((uintptr_t)(rank + n) + 255) & ~(uintptr_t)255);
     hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (MSD_NB + 2), s);
     hipMemsetAsync(big, 0, sizeof(uint32_t), s);
     hipMemsetAsync(list, 0, sizeof(uint32_t), s);
+    hipMemsetAsync(list2, 0, sizeof(uint32_t), s);
     const unsigned g = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(k_msd_count, dim3(g), dim3(256), 0, s, a, n, pbits, cnt, rank);
     scan_rec<uint32_t>(cnt, off, MSD_NB + 1, stmp, s);  // off[NB] = n (cnt[NB] == 0)
     hipLaunchKernelGGL(k_msd_scatter, dim3(g), dim3(256), 0, s, a, b, n, pbits, off, rank);
     uint32_t lcap = MSD_LCAP;
     if (const char *e = getenv("MRG_TEST_SORT_LCAP")) lcap = std::max<uint32_t>(1u, std::min<uint32_t>(MSD_LCAP, (uint32_t)atoi(e)));
-    hipLaunchKernelGGL(k_msd_list, dim3(MSD_NB / 256), dim3(256), 0, s, off, list);
-    hipLaunchKernelGGL(k_msd_leaf, dim3(MSD_GRID), dim3(MSD_WG), 0, s, b, off, list, lcap, big);
+    hipLaunchKernelGGL(k_msd_list, dim3(MSD_NB / 256), dim3(256), 0, s, off, std::min(MSD_SMALL, lcap), list, list2);
+    hipLaunchKernelGGL(k_msd_leaf_small, dim3(MSD_GRID), dim3(MSD_WG), 0, s, b, off, list);
+    hipLaunchKernelGGL(k_msd_leaf, dim3(MSD_GRID), dim3(MSD_WG), 0, s, b, off, list2, lcap, big);
     uint32_t nb = 0;
     hipMemcpyAsync(&nb, big, sizeof nb, hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
