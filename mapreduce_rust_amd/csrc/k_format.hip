@@ -109,14 +109,14 @@ __global__ void k_wc_write(const SortRec *r, uint64_t n, KeySet ks, const uint8_
 
 // part_off[p] = byte offset of the first element with part >= p  (elements: lines or groups)
 __global__ void k_part_off(const SortRec *r, const uint64_t *pos, uint64_t n, uint32_t R, const uint64_t *gidx,
-                           uint64_t total, uint64_t *part_off) {
+                           const uint64_t *total_p, uint64_t *part_off) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > n) return;
     // element i is the first of its partition run; previous partition id (or -1)
     const int64_t prev = i == 0 ? -1 : (int64_t)r[gidx ? gidx[i - 1] : i - 1].part;
     const int64_t cur = i == n ? (int64_t)R : (int64_t)r[gidx ? gidx[i] : i].part;
     if (cur == prev) return;
-    const uint64_t off = i == n ? total : pos[i];
+    const uint64_t off = i == n ? *total_p : pos[i];
     for (int64_t p = prev + 1; p <= cur; ++p) part_off[p] = off;
 }
 
@@ -225,7 +225,7 @@ uint64_t mrg_format(const FormatArgs &f, DevPool &pool, uint8_t **out_buf, uint6
     SortRec *recs = const_cast<SortRec *>(f.recs);
     uint64_t *part_off = (uint64_t *)pool.get(sizeof(uint64_t) * (R + 1));
     uint64_t *total_d = (uint64_t *)pool.get(sizeof(uint64_t) * 2);
-    hipMemsetAsync(part_off, 0, sizeof(uint64_t) * (R + 1), s);
+    // (no memset: k_part_off writes every entry 0..R, also for n == 0)
     uint64_t *scantmp = (uint64_t *)pool.get(sizeof(uint64_t) * mrg_scan_tmp_elems(n + 1));
     if (n && f.any_long) hipLaunchKernelGGL(k_fix_runs, grid_for(n), dim3(256), 0, s, recs, n, f.ks, f.heap);
 
@@ -238,16 +238,18 @@ uint64_t mrg_format(const FormatArgs &f, DevPool &pool, uint8_t **out_buf, uint6
             mrg_scan_u64(L, O, n, scantmp, s);
         }
         hipLaunchKernelGGL(k_total, dim3(1), dim3(1), 0, s, L, O, n, total_d);
-        hipMemcpyAsync(&total, total_d, sizeof total, hipMemcpyDeviceToHost, s);
-        hipStreamSynchronize(s);
-        if (total + 16 > *out_cap) {
+        // no round trip for the byte count: the buffer is sized by a bound ("key count\n" with at most
+        // 16 short-key bytes or the long key's heap bytes, and 20 digits), the count read with part_off
+        const uint64_t bound = n * (16u + 2u + 20u) + f.heap_bytes + 16u;
+        if (bound > *out_cap) {
             if (*out_buf) pool.put(*out_buf);
-            *out_cap = total + 16;
+            *out_cap = bound;
             *out_buf = (uint8_t *)pool.get(*out_cap);
         }
         if (n) hipLaunchKernelGGL(k_wc_write, grid_for(n), dim3(256), 0, s, recs, n, f.ks, f.heap, L, O, *out_buf);
         hipLaunchKernelGGL(k_part_off, grid_for(n + 1), dim3(256), 0, s, recs, O, n, R, (const uint64_t *)nullptr,
-                           total, part_off);
+                           (const uint64_t *)total_d, part_off);
+        hipMemcpyAsync(&total, total_d, sizeof total, hipMemcpyDeviceToHost, s);
         pool.put(L);
         pool.put(O);
     } else {
@@ -290,7 +292,7 @@ uint64_t mrg_format(const FormatArgs &f, DevPool &pool, uint8_t **out_buf, uint6
                                GO, f.names, f.name_off, *out_buf);
         if (G) hipLaunchKernelGGL(k_gather_first, grid_for(G), dim3(256), 0, s, recs, H, G, first);
         hipLaunchKernelGGL(k_part_off, grid_for(G + 1), dim3(256), 0, s, first, GO, G, R, (const uint64_t *)nullptr,
-                           total, part_off);
+                           (const uint64_t *)total_d, part_off);
         pool.put(head); pool.put(E); pool.put(nl); pool.put(P);
         pool.put(H); pool.put(GL); pool.put(GO); pool.put(first);
     }

@@ -215,25 +215,59 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
     }
 
     if (A.ablate && abl_acc == 0x9E3779B97F4A7C15ull) atomicAdd(&A.counters[CNT_OVF2], 1ull);
-    // ---- 2. this bucket's slice of every map workgroup's flushed table (a few entries each)
-    for (uint32_t r = wv; r < nreg; r += BA_NW) {
-        const GASK uint32_t *fo = gk(A.foff) + (uint64_t)r * (MRG_NBUCKET + 1);
-        const uint32_t lo = fo[b], hi = fo[b + 1];
-        const uint64_t reg = (uint64_t)r * A.regcap;
-        for (uint32_t base = lo; base < hi; base += 64) {
-            const uint32_t k = base + lane;
-            bool ovf = false;
-            uint64_t a = 0, c = 0;
-            uint32_t d = MRG_EMPTY_DOC, n2 = 0;
-            if (k < hi) {
-                a = gk(A.fk0)[reg + k];
-                c = gk(A.fk1)[reg + k];
-                n2 = gk(A.fcnt)[reg + k];
-                if (IDX) d = gk(A.fdoc)[reg + k];
-                const uint32_t h = ba_hash(a, c, d, A.hash_bits);
-                if (mine(h)) ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, a, c, d, n2, h);
+    // ---- 2. this bucket's slice of every map workgroup's flushed table (a few entries each): the
+    // wave's regions (wv, wv + 16, ...) one per lane, their slices flattened over the lanes (an
+    // exclusive scan of the slice sizes, each entry finds its region by binary search), four entries
+    // per lane in flight -- two load latencies per 64 regions instead of two per region
+    {
+        const uint32_t nrw = nreg > (uint32_t)wv ? (nreg - (uint32_t)wv + BA_NW - 1) / BA_NW : 0u;
+        for (uint32_t l0 = 0; l0 < nrw; l0 += 64) {
+            const uint32_t l = l0 + (uint32_t)lane;
+            uint32_t lo = 0, cnt = 0;
+            if (l < nrw) {
+                const GASK uint32_t *fo = gk(A.foff) + (uint64_t)(wv + BA_NW * l) * (MRG_NBUCKET + 1);
+                lo = fo[b];
+                cnt = fo[b + 1] - lo;
             }
-            if (__any(ovf)) overflow(ovf, a, c, d, n2);
+            uint32_t incl = cnt;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = __shfl_up(incl, o);
+                if (lane >= o) incl += v;
+            }
+            const uint32_t excl = incl - cnt;
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            for (uint32_t e0 = 0; e0 < total; e0 += 256) {
+                uint64_t a[4], c[4];
+                uint32_t n2[4], d[4];
+                bool ok[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t e = e0 + 64u * u + (uint32_t)lane;
+                    ok[u] = e < total;
+                    uint32_t k = 0;  // last lane whose slice starts at or before e
+#pragma unroll
+                    for (int st = 32; st > 0; st >>= 1)
+                        if (__shfl(excl, (int)(k + st)) <= e) k += st;
+                    const uint32_t rl = l0 + k;
+                    const uint64_t at = (uint64_t)(wv + BA_NW * rl) * A.regcap + __shfl(lo, (int)k) + (e - __shfl(excl, (int)k));
+                    a[u] = 0; c[u] = 0; n2[u] = 0; d[u] = MRG_EMPTY_DOC;
+                    if (ok[u]) {
+                        a[u] = gk(A.fk0)[at];
+                        c[u] = gk(A.fk1)[at];
+                        n2[u] = gk(A.fcnt)[at];
+                        if (IDX) d[u] = gk(A.fdoc)[at];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    bool ovf = false;
+                    if (ok[u]) {
+                        const uint32_t h = ba_hash(a[u], c[u], d[u], A.hash_bits);
+                        if (mine(h)) ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, a[u], c[u], d[u], n2[u], h);
+                    }
+                    if (__any(ovf)) overflow(ovf, a[u], c[u], d[u], n2[u]);
+                }
+            }
         }
     }
     // ---- 3. records that did not fit their map workgroup's region: this bucket's overflow list

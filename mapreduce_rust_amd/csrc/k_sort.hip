@@ -271,6 +271,7 @@ constexpr int MSD_WG = 256;
 constexpr uint32_t MSD_GRID = 1024;  // leaf workgroups (they stride over the bucket lists)
 constexpr uint32_t MSD_LCAP = 2048;
 constexpr uint32_t MSD_SMALL = 64;   // buckets sorted by one wave
+constexpr uint32_t MSD_SMALL_GRID = 2048;  // workgroups of the one-wave leaf kernel
 constexpr uint32_t MSD_MAX_BIG = 16;
 
 __device__ __forceinline__ uint32_t msd_bucket(const SortRec &r, uint32_t pbits) {
@@ -286,6 +287,10 @@ __device__ __forceinline__ uint32_t msd_bucket(const SortRec &r, uint32_t pbits)
     return (r.part << kb) | (code >> (21 - kb));
 }
 
+__device__ __forceinline__ uint32_t uni_lane(uint32_t v, uint32_t j) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
+}
+
 __device__ __forceinline__ bool rec_less(const SortRec &a, const SortRec &b) {
     if (a.part != b.part) return a.part < b.part;
     if (a.k0 != b.k0) return a.k0 < b.k0;
@@ -294,8 +299,14 @@ __device__ __forceinline__ bool rec_less(const SortRec &a, const SortRec &b) {
     return a.idx < b.idx;
 }
 
-__global__ void k_msd_count(const SortRec *in, uint64_t n, uint32_t pbits, uint32_t *cnt, uint32_t *rank) {
+__global__ void k_msd_count(const SortRec *in, uint64_t n, uint32_t pbits, uint32_t *cnt, uint32_t *rank,
+                            uint32_t *zero0, uint32_t *zero1, uint32_t *zero2) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {  // the later kernels' counters (list lengths, oversized count): no memset launches
+        *zero0 = 0;
+        *zero1 = 0;
+        *zero2 = 0;
+    }
     if (i >= n) return;
     rank[i] = atomicAdd(&cnt[msd_bucket(in[i], pbits)], 1u);
 }
@@ -311,21 +322,33 @@ __global__ void k_msd_scatter(const SortRec *in, SortRec *out, uint64_t n, uint3
 // The buckets with at least 2 records, listed (list[0] = how many): at most `small` records in
 // list (one wave each), more in list2 (one workgroup each).  The leaf kernels share the work by list
 // position, not by bucket id (bucket ids of text keys cluster in a few ranges).
-__global__ void k_msd_list(const uint32_t *off, uint32_t small, uint32_t *list, uint32_t *list2) {
+__global__ __launch_bounds__(1024) void k_msd_list(const uint32_t *off, uint32_t small, uint32_t *list, uint32_t *list2) {
+    // 1024 buckets per workgroup: ranks inside the workgroup through LDS, one device atomic per list
+    __shared__ uint32_t s_n[2], s_base[2];
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t m = b < MSD_NB ? off[b + 1] - off[b] : 0u;
     const uint32_t lane = __lane_id();
-    auto put = [&](bool pred, uint32_t *l) {
+    if (threadIdx.x < 2) s_n[threadIdx.x] = 0;
+    __syncthreads();
+    const bool p1 = m >= 2u && m <= small, p2 = m > small;
+    uint32_t r1 = 0, r2 = 0;
+    auto rank = [&](bool pred, uint32_t k) -> uint32_t {
         const uint64_t msk = __ballot(pred);
-        if (!msk) return;
+        if (!msk) return 0;
         const uint32_t leader = (uint32_t)__ffsll((unsigned long long)msk) - 1u;
         uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&l[0], (uint32_t)__popcll(msk));
+        if (lane == leader) base = atomicAdd(&s_n[k], (uint32_t)__popcll(msk));
         base = __shfl(base, (int)leader);
-        if (pred) l[1 + base + (uint32_t)__popcll(msk & mrg_lanemask_lt())] = b;
+        return base + (uint32_t)__popcll(msk & mrg_lanemask_lt());
     };
-    put(m >= 2u && m <= small, list);
-    put(m > small, list2);
+    r1 = rank(p1, 0);
+    r2 = rank(p2, 1);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_n[0]) s_base[0] = atomicAdd(&list[0], s_n[0]);
+    if (threadIdx.x == 64 && s_n[1]) s_base[1] = atomicAdd(&list2[0], s_n[1]);
+    __syncthreads();
+    if (p1) list[1 + s_base[0] + r1] = b;
+    if (p2) list2[1 + s_base[1] + r2] = b;
 }
 
 // One wave per small bucket (m <= 64): lane i holds record i; its rank = the records of the bucket
@@ -335,22 +358,21 @@ __global__ __launch_bounds__(MSD_WG) void k_msd_leaf_small(SortRec *recs, const 
     const uint32_t nl = list[0];
     const uint32_t lane = __lane_id();
     const uint32_t nw = gridDim.x * (MSD_WG / 64);
-    for (uint32_t x = blockIdx.x * (MSD_WG / 64) + (threadIdx.x >> 6); x < nl; x += nw) {
-        const uint32_t b = list[1 + x];
-        const uint32_t lo = off[b], m = off[b + 1] - lo;
+    auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+    for (uint32_t x = uni(blockIdx.x * (MSD_WG / 64) + (threadIdx.x >> 6)); x < nl; x += nw) {
+        const uint32_t b = uni(list[1 + x]);
+        const uint32_t lo = uni(off[b]), m = uni(off[b + 1]) - lo;
         SortRec r{};
         if (lane < m) r = recs[lo + lane];
         uint32_t rank = 0;
-        for (uint32_t j = 0; j < m; ++j) {
-            SortRec o;
-            o.k0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(r.k0 >> 32), (int)j) << 32) |
-                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)r.k0, (int)j);
-            o.k1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(r.k1 >> 32), (int)j) << 32) |
-                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)r.k1, (int)j);
-            o.part = (uint32_t)__builtin_amdgcn_readlane((int)r.part, (int)j);
-            o.doc = (uint32_t)__builtin_amdgcn_readlane((int)r.doc, (int)j);
-            o.idx = (uint32_t)__builtin_amdgcn_readlane((int)r.idx, (int)j);
-            rank += rec_less(o, r) ? 1u : 0u;
+        for (uint32_t j = 0; j < m; ++j) {  // wave-uniform trip count; branch-free compare
+            const uint64_t k0 = ((uint64_t)uni_lane((uint32_t)(r.k0 >> 32), j) << 32) | uni_lane((uint32_t)r.k0, j);
+            const uint64_t k1 = ((uint64_t)uni_lane((uint32_t)(r.k1 >> 32), j) << 32) | uni_lane((uint32_t)r.k1, j);
+            const uint32_t pt = uni_lane(r.part, j), dc = uni_lane(r.doc, j), ix = uni_lane(r.idx, j);
+            const bool lt = (pt < r.part) |
+                            ((pt == r.part) & ((k0 < r.k0) | ((k0 == r.k0) & ((k1 < r.k1) | ((k1 == r.k1) &
+                            ((dc < r.doc) | ((dc == r.doc) & (ix < r.idx))))))));
+            rank += lt ? 1u : 0u;
         }
         if (lane < m) recs[lo + rank] = r;
     }
@@ -428,48 +450,71 @@ uint64_t mrg_sort_tmp_bytes(uint64_t n) {
     return lsd + msd + 256;  // the MSD arrays, then room for an LSD sort of one oversized bucket
 }
 
-SortRec *mrg_msd_sort(SortRec *a, SortRec *b, uint64_t n, uint32_t pbits, const SortPlan &plan, void *tmp,
-                      hipStream_t s, uint32_t *n_big) {
-    if (n_big) *n_big = 0;
-    if (n <= 1) return a;
-    uint32_t *cnt = (uint32_t *)tmp;            // [NB + 1]
-    uint32_t *off = cnt + (MSD_NB + 2);         // [NB + 1]
-    uint32_t *big = off + (MSD_NB + 2);         // [1 + MAX_BIG]
-    uint32_t *list = big + (MSD_MAX_BIG + 2);   // [1 + NB] buckets of 2..small records
-    uint32_t *list2 = list + (MSD_NB + 2);      // [1 + NB] larger buckets
-    uint32_t *stmp = list2 + (MSD_NB + 2);      // scan temp
-    uint32_t *rank = stmp + scan_tmp(MSD_NB + 1);
+struct MsdTmp {
+    uint32_t *cnt, *off, *big, *list, *list2, *stmp, *rank;
+    void *ltmp;
+};
+static MsdTmp msd_tmp(void *tmp, uint64_t n) {
+    MsdTmp t;
+    t.cnt = (uint32_t *)tmp;                 // [NB + 1]
+    t.off = t.cnt + (MSD_NB + 2);            // [NB + 1]
+    t.big = t.off + (MSD_NB + 2);            // [1 + MAX_BIG]
+    t.list = t.big + (MSD_MAX_BIG + 2);      // [1 + NB] buckets of 2..small records
+    t.list2 = t.list + (MSD_NB + 2);         // [1 + NB] larger buckets
+    t.stmp = t.list2 + (MSD_NB + 2);         // scan temp
+    t.rank = t.stmp + scan_tmp(MSD_NB + 1);
     // the LSD temp (histograms, tile counts) goes after the MSD arrays
-    void *ltmp = (void *)(((uintptr_t)(rank + n) + 255) & ~(uintptr_t)255);
-    hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (MSD_NB + 2), s);
-    hipMemsetAsync(big, 0, sizeof(uint32_t), s);
-    hipMemsetAsync(list, 0, sizeof(uint32_t), s);
-    hipMemsetAsync(list2, 0, sizeof(uint32_t), s);
+    t.ltmp = (void *)(((uintptr_t)(t.rank + n) + 255) & ~(uintptr_t)255);
+    return t;
+}
+
+void mrg_msd_sort_launch(SortRec *a, SortRec *b, uint64_t n, uint32_t pbits, void *tmp, hipStream_t s,
+                         uint32_t *h_nbig) {
+    *h_nbig = 0;
+    if (n <= 1) return;
+    const MsdTmp t = msd_tmp(tmp, n);
+    hipMemsetAsync(t.cnt, 0, sizeof(uint32_t) * (MSD_NB + 2), s);
     const unsigned g = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(k_msd_count, dim3(g), dim3(256), 0, s, a, n, pbits, cnt, rank);
-    scan_rec<uint32_t>(cnt, off, MSD_NB + 1, stmp, s);  // off[NB] = n (cnt[NB] == 0)
-    hipLaunchKernelGGL(k_msd_scatter, dim3(g), dim3(256), 0, s, a, b, n, pbits, off, rank);
+    hipLaunchKernelGGL(k_msd_count, dim3(g), dim3(256), 0, s, a, n, pbits, t.cnt, t.rank, t.big, t.list, t.list2);
+    scan_rec<uint32_t>(t.cnt, t.off, MSD_NB + 1, t.stmp, s);  // off[NB] = n (cnt[NB] == 0)
+    hipLaunchKernelGGL(k_msd_scatter, dim3(g), dim3(256), 0, s, a, b, n, pbits, t.off, t.rank);
     uint32_t lcap = MSD_LCAP;
     if (const char *e = getenv("MRG_TEST_SORT_LCAP")) lcap = std::max<uint32_t>(1u, std::min<uint32_t>(MSD_LCAP, (uint32_t)atoi(e)));
-    hipLaunchKernelGGL(k_msd_list, dim3(MSD_NB / 256), dim3(256), 0, s, off, std::min(MSD_SMALL, lcap), list, list2);
-    hipLaunchKernelGGL(k_msd_leaf_small, dim3(MSD_GRID), dim3(MSD_WG), 0, s, b, off, list);
-    hipLaunchKernelGGL(k_msd_leaf, dim3(MSD_GRID), dim3(MSD_WG), 0, s, b, off, list2, lcap, big);
-    uint32_t nb = 0;
-    hipMemcpyAsync(&nb, big, sizeof nb, hipMemcpyDeviceToHost, s);
-    hipStreamSynchronize(s);
-    if (n_big) *n_big = nb;
+    hipLaunchKernelGGL(k_msd_list, dim3(MSD_NB / 1024), dim3(1024), 0, s, t.off, std::min(MSD_SMALL, lcap), t.list, t.list2);
+    // small buckets: one wave each, 8 workgroups (32 waves) per CU striding over the list (the
+    // list length is on the device; a grid of n / 2 waves spent its time dispatching empty waves)
+    const uint64_t nsmall = std::min<uint64_t>(n / 2, (uint64_t)MSD_SMALL_GRID * (MSD_WG / 64));
+    hipLaunchKernelGGL(k_msd_leaf_small, dim3((unsigned)((nsmall + MSD_WG / 64 - 1) / (MSD_WG / 64))), dim3(MSD_WG), 0, s,
+                       b, t.off, t.list);
+    hipLaunchKernelGGL(k_msd_leaf, dim3(MSD_GRID), dim3(MSD_WG), 0, s, b, t.off, t.list2, lcap, t.big);
+    hipMemcpyAsync(h_nbig, t.big, sizeof(uint32_t), hipMemcpyDeviceToHost, s);  // pinned: no wait here
+}
+
+SortRec *mrg_msd_sort_finish(SortRec *a, SortRec *b, uint64_t n, const SortPlan &plan, void *tmp, hipStream_t s,
+                             uint32_t nb) {
+    if (n <= 1) return a;
     if (!nb) return b;
-    if (nb > MSD_MAX_BIG) return mrg_radix_sort(b, a, n, plan, ltmp, s, nullptr);  // skewed: all of it
+    const MsdTmp t = msd_tmp(tmp, n);
+    if (nb > MSD_MAX_BIG) return mrg_radix_sort(b, a, n, plan, t.ltmp, s, nullptr);  // skewed: all of it
     std::vector<uint32_t> bl(nb), o(MSD_NB + 1);
-    hipMemcpyAsync(bl.data(), big + 1, sizeof(uint32_t) * nb, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(o.data(), off, sizeof(uint32_t) * (MSD_NB + 1), hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(bl.data(), t.big + 1, sizeof(uint32_t) * nb, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(o.data(), t.off, sizeof(uint32_t) * (MSD_NB + 1), hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
     for (uint32_t bk : bl) {  // each oversized bucket by the LSD sort on its segment (a: scratch)
         const uint64_t lo = o[bk], m = o[bk + 1] - lo;
-        SortRec *r = mrg_radix_sort(b + lo, a + lo, m, plan, ltmp, s, nullptr);
+        SortRec *r = mrg_radix_sort(b + lo, a + lo, m, plan, t.ltmp, s, nullptr);
         if (r != b + lo) hipMemcpyAsync(b + lo, r, sizeof(SortRec) * m, hipMemcpyDeviceToDevice, s);
     }
     return b;
+}
+
+SortRec *mrg_msd_sort(SortRec *a, SortRec *b, uint64_t n, uint32_t pbits, const SortPlan &plan, void *tmp,
+                      hipStream_t s, uint32_t *n_big, uint32_t *h_pinned) {
+    mrg_msd_sort_launch(a, b, n, pbits, tmp, s, h_pinned);
+    hipStreamSynchronize(s);
+    const uint32_t nb = *h_pinned;
+    if (n_big) *n_big = nb;
+    return mrg_msd_sort_finish(a, b, n, plan, tmp, s, nb);
 }
 
 SortRec *mrg_radix_sort(SortRec *recs, SortRec *alt, uint64_t n, const SortPlan &plan, void *tmp, hipStream_t s,

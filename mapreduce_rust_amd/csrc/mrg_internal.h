@@ -211,7 +211,14 @@ SortRec *mrg_radix_sort(SortRec *recs, SortRec *alt, uint64_t n, const SortPlan 
 // sort.  Returns recs or alt; *n_big = oversized buckets (more than 16: the whole array went through
 // the LSD sort).
 SortRec *mrg_msd_sort(SortRec *recs, SortRec *alt, uint64_t n, uint32_t pbits, const SortPlan &plan, void *tmp,
-                      hipStream_t s, uint32_t *n_big);
+                      hipStream_t s, uint32_t *n_big, uint32_t *h_pinned);
+// The same in two halves, with no host wait in between: _launch enqueues the MSD passes and an async
+// copy of the oversized-bucket count into *h_nbig (pinned); once the stream has reached it, _finish
+// sorts the oversized buckets (if any) and returns recs or alt like mrg_msd_sort.
+void mrg_msd_sort_launch(SortRec *recs, SortRec *alt, uint64_t n, uint32_t pbits, void *tmp, hipStream_t s,
+                         uint32_t *h_nbig);
+SortRec *mrg_msd_sort_finish(SortRec *recs, SortRec *alt, uint64_t n, const SortPlan &plan, void *tmp, hipStream_t s,
+                             uint32_t nb);
 // Stable sort of (u64 key, u32 val) pairs by key, in place in (keys, vals); kv_tmp holds 4n u64.
 void mrg_radix_sort_u64(uint64_t *keys, uint32_t *vals, uint64_t *kv_tmp, uint64_t n, void *tmp, hipStream_t s);
 
@@ -221,6 +228,7 @@ struct FormatArgs {
     uint64_t n;
     KeySet ks;
     const uint8_t *heap;
+    uint64_t heap_bytes;        // bytes of the long-key heap (bounds the wc output before it is sized)
     uint32_t n_reduce;
     int drop_last;
     int indexer;

@@ -344,8 +344,8 @@ void long_aggregate(mrg_ctx *c, LongItems li) {
 }
 
 // Distinct-key count + partition of every key (worker.rs:129).
-void finish_keys(mrg_ctx *c) {
-    read_counters(c);
+void finish_keys(mrg_ctx *c, bool counters_fresh = false) {
+    if (!counters_fresh) read_counters(c);
     c->keys.n = c->h_cnt[CNT_KEYS];
     if (c->keys.n > c->keys.cap) raise(MRG_EINVAL, "internal: key set overflow");
     mrg_launch_partition(c->keys.ks, c->keys.heap, c->keys.n, c->R, c->stream);
@@ -415,8 +415,10 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         B.ablate = getenv("MRG_AGG_ABLATE") ? (uint32_t)atoi(getenv("MRG_AGG_ABLATE")) : 0u;
         B.nsub = nsub;
         B.kcap = c->keys.cap;
-        HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
-        HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
+        if (agg_launches > 1) {  // the map launch zeroed every counter; the map leaves these two alone
+            HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
+            HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
+        }
         // 32-bit LDS counts (larger table) when no key can reach 2^32: fewer tokens than that
         const bool c32 = c->h_cnt[CNT_TOKENS] < 0xFFFFFFFFull && nreg <= 1024;
         mrg_launch_bucket_agg(B, idx, c32, s);
@@ -463,8 +465,10 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         }
         break;
     }
+    // the counters read after the aggregation are still current unless more keys were appended
+    const bool fresh = c->st.overflow_keys == 0 && li.n == 0;
     long_aggregate(c, li);
-    finish_keys(c);
+    finish_keys(c, fresh);
     return true;
 }
 
@@ -1047,21 +1051,33 @@ DocRank doc_ranks(mrg_ctx *c) {
 }
 
 // Sort records of the keys `ks` by (partition < R, key bytes[, doc rank]) (worker.rs:162-164).
-// Returns a or b.
-SortRec *sort_keys(mrg_ctx *c, KeySet ks, uint32_t R, const uint32_t *d_rank, SortRec *a, SortRec *b, void *stmp) {
-    const uint64_t n = c->keys.n;
+// Returns a or b.  With `defer`, only the MSD passes are enqueued and b is returned: the caller
+// checks the oversized-bucket count (c->h_cnt[CNT_N], pinned) after its next stream sync and calls
+// mrg_msd_sort_finish if it is not 0 (saves a host round trip per reduce).
+SortPlan sort_plan(mrg_ctx *c, uint32_t R) {
     const bool idx = is_idx(c);
-    mrg_launch_make_sortrec(ks, n, d_rank, a, c->stream);
     SortPlan plan{};
     plan.use_part = R > 1;
     plan.part_bytes = bytes_for(R - 1);
     plan.use_k0 = plan.use_k1 = true;
     plan.use_doc = idx;
     plan.doc_bytes = idx ? bytes_for(c->names.size() - 1) : 0;
+    return plan;
+}
+
+SortRec *sort_keys(mrg_ctx *c, KeySet ks, uint32_t R, const uint32_t *d_rank, SortRec *a, SortRec *b, void *stmp,
+                   bool defer = false) {
+    const uint64_t n = c->keys.n;
+    mrg_launch_make_sortrec(ks, n, d_rank, a, c->stream);
     check_sort_n(n, "key sort");
     const uint32_t pbits = R > 1 ? 32u - (uint32_t)__builtin_clz(R - 1u) : 0u;
+    uint32_t *h_nbig = (uint32_t *)&c->h_cnt[CNT_N];
+    if (defer) {
+        mrg_msd_sort_launch(a, b, n, pbits, stmp, c->stream, h_nbig);
+        return n <= 1 ? a : b;
+    }
     uint32_t n_big = 0;
-    return mrg_msd_sort(a, b, n, pbits, plan, stmp, c->stream, &n_big);
+    return mrg_msd_sort(a, b, n, pbits, sort_plan(c, R), stmp, c->stream, &n_big, h_nbig);
 }
 
 FormatArgs format_args(mrg_ctx *c, const SortRec *recs, KeySet ks, uint32_t R, int drop_last, const DocRank &dr) {
@@ -1070,6 +1086,7 @@ FormatArgs format_args(mrg_ctx *c, const SortRec *recs, KeySet ks, uint32_t R, i
     f.n = c->keys.n;
     f.ks = ks;
     f.heap = c->keys.heap;
+    f.heap_bytes = c->keys.heap_bytes;
     f.n_reduce = R;
     f.drop_last = drop_last;
     f.indexer = is_idx(c);
@@ -1136,8 +1153,12 @@ void job_reduce(mrg_ctx *c) {
     SortRec *a = pget<SortRec>(p, n), *b = pget<SortRec>(p, n);
     void *stmp = p.get(mrg_sort_tmp_bytes(n));
     SortRec *sorted = a;
-    if (c->keys.sorted && !c->keys.any_long && !is_idx(c)) mrg_launch_make_sortrec(c->keys.ks, n, nullptr, a, s);
-    else sorted = sort_keys(c, c->keys.ks, c->R, dr.rank, a, b, stmp);
+    const bool presorted = c->keys.sorted && !c->keys.any_long && !is_idx(c);
+    // the oversized-bucket check of the key sort waits for format's own sync (add_first below is
+    // not idempotent: that path checks at once)
+    const bool defer = !presorted && !(c->extra_first && n);
+    if (presorted) mrg_launch_make_sortrec(c->keys.ks, n, nullptr, a, s);
+    else sorted = sort_keys(c, c->keys.ks, c->R, dr.rank, a, b, stmp, defer);
     // text reduce (worker.rs:169-173): lines with an empty key sort first and, since `prev` is still
     // empty when the first real key arrives, their values join that key's group
     if (c->extra_first && n) {
@@ -1148,6 +1169,12 @@ void job_reduce(mrg_ctx *c) {
     const FormatArgs f = format_args(c, sorted, c->keys.ks, c->R, compat_drop_last(c), dr);
     c->part_off.assign(c->R + 1, 0);
     c->out_bytes = mrg_format(f, p, &c->d_out, &c->out_cap, c->part_off.data(), s);
+    const uint32_t n_big = *(const uint32_t *)&c->h_cnt[CNT_N];  // written by the sort's async copy
+    if (defer && n > 1 && n_big) {  // oversized MSD buckets: sort them, format again
+        sorted = mrg_msd_sort_finish(a, b, n, sort_plan(c, c->R), stmp, s, n_big);
+        const FormatArgs f2 = format_args(c, sorted, c->keys.ks, c->R, compat_drop_last(c), dr);
+        c->out_bytes = mrg_format(f2, p, &c->d_out, &c->out_cap, c->part_off.data(), s);
+    }
     ev_rec(c, 6);
     HIPCHK(hipGetLastError());
     p.put(a); p.put(b); p.put(stmp);
@@ -1533,7 +1560,8 @@ int mrg_open(int device, mrg_ctx **out) {
         HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
         c->stream = c->own;
         HIPCHK(hipMalloc(&c->d_cnt, sizeof(unsigned long long) * CNT_N));
-        HIPCHK(hipHostMalloc(&c->h_cnt, sizeof(unsigned long long) * CNT_N, hipHostMallocDefault));
+        // CNT_N counters + pinned scratch (h_cnt[CNT_N]: the key sort's oversized-bucket count)
+        HIPCHK(hipHostMalloc(&c->h_cnt, sizeof(unsigned long long) * (CNT_N + 8), hipHostMallocDefault));
         for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
         if (const char *v = getenv("MRG_LDS_CAP")) c->lds_cap = atoi(v);
         *out = c;
