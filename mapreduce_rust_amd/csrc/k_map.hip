@@ -168,6 +168,15 @@ __device__ __forceinline__ TileInfo sub_tile(const BlkInfo &b, uint32_t j) {
     return t;
 }
 
+__device__ __forceinline__ uint32_t map_ablate(const MapArgs &A) {
+#ifdef MRG_MAP_ABLATION
+    return A.ablate;
+#else
+    (void)A;
+    return 0u;
+#endif
+}
+
 __device__ __forceinline__ void report_error(unsigned long long *counters, uint64_t pos) {
     __hip_atomic_fetch_min(gp(&counters[CNT_ERRPOS]), (unsigned long long)pos, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -406,10 +415,10 @@ __device__ __forceinline__ void emit(const MapArgs &A, LdsTable<CAP, IDX> &table
         h = key_hash(tk0, tk1, dkey, A.hash_bits);
     }
     {
-        const bool act = have && !is_long && !(A.ablate & 2u);
+        const bool act = have && !is_long && !(map_ablate(A) & 2u);
         tail = (have && !is_long) && !table.insert_wave(act, tk0, tk1, dkey, h);
     }
-    if (tail && !(A.ablate & 1u)) {
+    if (tail && !(map_ablate(A) & 1u)) {
         const uint32_t b = bucket_of(h);
         const uint64_t end = R.end[b];
         const uint64_t idx = atomicAdd(&R.cur[b], 1ull);
@@ -585,7 +594,13 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     const TailRegions tails{s_tcur, s_tend};
     uint32_t my_tokens = 0;
     // uniform job parameters used in the hot loop, read once
+    // ablation knobs (MRG_ABLATE, timing only) exist in -DMRG_MAP_ABLATION builds; in the product
+    // build abl is the constant 0, so no branch, mask or SGPR of the hot loop is spent on them
+#ifdef MRG_MAP_ABLATION
     const uint32_t abl = A.ablate;
+#else
+    constexpr uint32_t abl = 0;
+#endif
     const uint32_t hbits = A.hash_bits;
     GAS uint64_t *const pool = gp(A.pool);
     uint8_t *win = s_win[wv];
@@ -616,9 +631,15 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     struct Blk {
         uint4 v0, v1, e;
     };
+#ifdef MRG_MAP_ABLATION
     BlkInfo first_blk{};  // ablate & 8 (timing only): every block re-reads the wave's first block
+#endif
     auto load_blk = [&](const BlkInfo &b0, Blk &X) {
-        const BlkInfo &b = (A.ablate & 8u) ? first_blk : b0;  // a real block: its own base and bounds
+#ifdef MRG_MAP_ABLATION
+        const BlkInfo &b = (abl & 8u) ? first_blk : b0;  // a real block: its own base and bounds
+#else
+        const BlkInfo &b = b0;
+#endif
         const GAS uint8_t *src = gp(A.in) + (b.Ab - (uint64_t)BEHIND);
         auto ld = [&](uint32_t idx) -> uint4 {
             const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const GAS u32x4 *>(src + 16u * min(max(idx, b.v0), b.v1 - 1u)));
@@ -922,7 +943,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     };
     if (c < whi_b) {
         IA = locate_blk(A, c, dcur);
+#ifdef MRG_MAP_ABLATION
         first_blk = IA;
+#endif
         load_blk(IA, XA);
         settle(XA);
     }

@@ -1,6 +1,9 @@
 #!/bin/bash
 # Per-phase instruction counts of k_map: one PMC pass per ablation level (MRG_ABLATE) on 1 GiB of C3,
 # then the map time of each level on the full C3 input.  ABLS="32 64 4 0" by default.
+# k_map's ablation knobs exist only in the ablation build:
+#   EXTRA=-DMRG_MAP_ABLATION bash tools/build_variant.sh ablation mapreduce_rust_amd/csrc/k_map.hip
+export MRG_LIB=${MRG_LIB:-$PWD/mapreduce_rust_amd/lib_variants/ablation/libmrgpu.so}
 mkdir -p gpurun_out/abl
 export TMPDIR=/tmp
 CTRS=${CTRS:-"SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"}
