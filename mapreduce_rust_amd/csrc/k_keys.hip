@@ -29,11 +29,12 @@ inline dim3 grid_for(uint64_t n, int b = 256) { return dim3((unsigned)((n + b - 
 // current one is summed, and a record that finds its key costs one 16-byte LDS read + one LDS add.
 constexpr int BA_WG = 1024;
 constexpr int BA_NW = BA_WG / 64;
-// LDS table slots per bucket: wc with 32-bit counts (the job has fewer than 2^32 tokens) 7680
-// (16-byte key + 4-byte count: 150 KiB), wc with 64-bit counts 6144 (144 KiB), the indexer 4096
-// (+ 4-byte doc).  About half the slots stay free at 2^20 distinct keys over 256 buckets.
+// LDS table slots per bucket: wc with 32-bit counts (the job has fewer than 2^32 tokens) 7424
+// (16-byte key + 4-byte count: 145 KiB), wc with 64-bit counts 6112 (143 KiB), the indexer 4096
+// (+ 4-byte doc); the rest of the LDS holds the per-region record counts and chunk offsets.  About
+// half the slots stay free at 2^20 distinct keys over 256 buckets.
 template <bool IDX, bool C32>
-constexpr uint32_t ba_cap() { return IDX ? 4096u : (C32 ? 7680u : 6144u); }
+constexpr uint32_t ba_cap() { return IDX ? 4096u : (C32 ? 7424u : 6112u); }
 constexpr int BA_PROBE = 64;
 constexpr int BA_U = 8;            // records per lane per chunk
 template <bool C32>
@@ -108,7 +109,8 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
     __shared__ BaKey s_key[BA_CAP];
     __shared__ CT s_cnt[BA_CAP];
     __shared__ unsigned int s_doc[IDX ? BA_CAP : 1];
-    __shared__ uint32_t s_rn[ba_maxreg<C32>()];  // tail records of region r in this bucket
+    __shared__ uint32_t s_rn[ba_maxreg<C32>()];      // tail records of region r in this bucket
+    __shared__ uint32_t s_cs[ba_maxreg<C32>() + 1];  // first chunk of region r (chunks numbered region by region)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int i = tid; i < (int)BA_CAP; i += BA_WG) {
@@ -125,6 +127,24 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
     const uint32_t nreg = A.nreg;
     for (uint32_t r = tid; r < nreg; r += BA_WG) s_rn[r] = min(gk(A.bcount)[(uint64_t)r * MRG_NBUCKET + b], cap);
     __syncthreads();
+    constexpr uint32_t CH = 64u * BA_U;  // records per chunk
+    if (wv == 0) {  // chunk offsets of the regions: a wave scan, 64 regions at a time
+        uint32_t run = 0;
+        for (uint32_t r0 = 0; r0 < nreg; r0 += 64) {
+            const uint32_t r = r0 + (uint32_t)lane;
+            const uint32_t c = r < nreg ? (s_rn[r] + CH - 1u) / CH : 0u;
+            uint32_t incl = c;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = __shfl_up(incl, o);
+                if (lane >= o) incl += v;
+            }
+            if (r < nreg) s_cs[r] = run + incl - c;
+            run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+        if (lane == 0) s_cs[nreg] = run;
+    }
+    __syncthreads();
+    const uint32_t NC = s_cs[nreg];  // chunks of the bucket
 
     auto overflow = [&](bool ovf, uint64_t a, uint64_t c, uint32_t d, uint64_t n2) {
         const uint64_t j = mrg_wave_append(&A.counters[CNT_OVF2], ovf);
@@ -134,23 +154,19 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
         }
     };
 
-    // ---- 1. tail regions: wave wv takes regions wv, wv + 16, ...; chunks of 64 * BA_U records
+    // ---- 1. tail regions, as one sequence of chunks of 64 * BA_U records (region by region): wave wv
+    // takes chunks wv, wv + 16, ..., so at any time the workgroup's 16 waves read 16 neighbouring chunks
+    // (one stream of the bucket per workgroup; with a region per wave the 256 workgroups kept 4096
+    // streams open at once)
     const GASK uint64_t *pool = gk(A.pool) + A.rbase[b] * RW;
     struct Chunk {
         u64x2k k[BA_U];
         uint32_t d[IDX ? BA_U : 1];
     };
-    auto first_chunk = [&](uint32_t &r, uint32_t &off) {
-        r = (uint32_t)wv;
-        off = 0;
-        while (r < nreg && s_rn[r] == 0) r += BA_NW;
-    };
-    auto next_chunk = [&](uint32_t &r, uint32_t &off) {
-        off += 64u * BA_U;
-        while (r < nreg && off >= s_rn[r]) {
-            r += BA_NW;
-            off = 0;
-        }
+    // region and record offset of chunk k (r only moves forward: a wave's chunks increase)
+    auto chunk_pos = [&](uint32_t k, uint32_t &r) -> uint32_t {
+        while (s_cs[r + 1] <= k) ++r;
+        return (k - s_cs[r]) * CH;
     };
     // unconditional loads: an index past the region's end reads its last record (masked later)
     auto load_chunk = [&](uint32_t r, uint32_t off, Chunk &X) {
@@ -193,23 +209,25 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
     };
     {
         Chunk XA, XB;
-        uint32_t rA, oA;
-        first_chunk(rA, oA);
-        if (rA < nreg) load_chunk(rA, oA, XA);
-        while (rA < nreg) {
+        uint32_t kA = (uint32_t)wv, rA = 0, oA = 0;
+        if (kA < NC) {
+            oA = chunk_pos(kA, rA);
+            load_chunk(rA, oA, XA);
+        }
+        while (kA < NC) {
+            const uint32_t kB = kA + BA_NW;
             uint32_t rB = rA, oB = oA;
-            next_chunk(rB, oB);
+            if (kB < NC) oB = chunk_pos(kB, rB);
             settle(XA);
-            if (rB < nreg) load_chunk(rB, oB, XB);
-            else load_chunk(rA, oA, XB);  // keep the load count fixed
+            load_chunk(rB, oB, XB);  // past the end: a reload of chunk kA (fixed load count)
             sum_chunk(rA, oA, XA);
-            if (rB >= nreg) break;
+            if (kB >= NC) break;
+            kA = kB + BA_NW;
             rA = rB;
-            oA = oB;
-            next_chunk(rA, oA);
+            if (kA < NC) oA = chunk_pos(kA, rA);
+            else oA = oB;
             settle(XB);
-            if (rA < nreg) load_chunk(rA, oA, XA);
-            else load_chunk(rB, oB, XA);
+            load_chunk(rA, oA, XA);
             sum_chunk(rB, oB, XB);
         }
     }
