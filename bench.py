@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--cpu-w1-mib", type=int, default=128, help="C3 slice for the W = 1 CPU run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lds-cap", type=int, default=0)
+    ap.add_argument("--shuffle-1", action="store_true",
+                    help="N = 1 only: run the library's RCCL shuffle in a one-rank communicator every step (the "
+                         "C4 export / exchange / import path without peers; a rehearsal, not the C3 metric)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = the library's RCCL exchange over xGMI (the product); gloo = host-staged exchange "
                          "through torch.distributed, for rehearsing N > 1 with several ranks on one GPU")
@@ -142,6 +145,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
     comm = S.library_comm(ctx) if (world > 1 and a.backend == "nccl") else None
+    if world == 1 and a.shuffle_1:
+        comm = M.Comm(ctx, M.comm_id(), 1, 0)
     buf = torch.empty(shard + 64, dtype=torch.uint8, device=dev)
     for i in range(files):
         fi = rank * files + i
@@ -191,7 +196,8 @@ def main():
         if rank == 0:
             log(f"step: map {s['ms_map']:.2f} ms ({s['map_launches']} launch), agg {s['ms_aggregate']:.2f}, "
                 f"sort {s['ms_sort']:.2f}, format {s['ms_format']:.2f}"
-                + (f", exchange {s['ms_exchange']:.2f}" if world > 1 else "") + f"; wall {step_s[-1] * 1e3:.2f}")
+                + (f", exchange {s['ms_exchange']:.2f}" if comm is not None or world > 1 else "")
+                + f"; wall {step_s[-1] * 1e3:.2f}")
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -237,7 +243,7 @@ def main():
     # / the HIP-event time of the send/recv group, against (N - 1) links x 153 GB/s one way (each GPU
     # of the node has a direct link to each peer).  Max over ranks of time and bytes.
     xgmi = None
-    if comm is not None:
+    if comm is not None and world > 1:
         ex_ms = statistics.median(s["ms_exchange"] for s in stats)
         ex_b = max(statistics.median(s["exchange_sent"] for s in stats),
                    statistics.median(s["exchange_recv"] for s in stats))
@@ -266,7 +272,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": wl[a.workload], "input_bytes_per_gpu": shard, "files_per_gpu": files,
+        "config": {"workload": wl[a.workload] + (" + one-rank RCCL shuffle rehearsal" if a.shuffle_1 and world == 1 else ""), "input_bytes_per_gpu": shard, "files_per_gpu": files,
                    "file_bytes": fbytes, "n_reduce": a.reduce, "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "kernel": "k_map (tokenize + LDS combine)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

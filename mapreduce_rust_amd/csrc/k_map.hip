@@ -549,6 +549,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ unsigned long long s_tend[MRG_NBUCKET];  // end of that region
     __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
     __shared__ uint32_t s_next, s_ngen;                  // next block of the workgroup's share; list length
+    __shared__ uint32_t s_tot[2];                        // workgroup totals: tokens, tail records
     __shared__ unsigned int s_door[MRG_MAP_DOOR ? LdsTable<CAP, IDX>::DW : 1];  // admission bitmap
     static_assert(sizeof(s_q) >= CAP * sizeof(uint16_t), "flush ranks reuse the queues");
 
@@ -572,6 +573,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     if (tid == 0) {
         s_next = 0;
         s_ngen = 0;
+        s_tot[0] = 0;
+        s_tot[1] = 0;
     }
     if (tid < 128) {
         const uint32_t c = mrg_uclass((uint32_t)tid);
@@ -1031,14 +1034,21 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         gp(A.fcnt)[pos2] = s_cnt[i];
         if (IDX) gp(A.fdoc)[pos2] = d;
     }
+    // token and tail totals: waves -> LDS -> one device atomic per workgroup and counter (a wave
+    // atomic each put 8 K atomics on two counters at the very end of the launch)
     uint32_t t = my_tokens, ttl = my_tail;
     for (int off = 32; off > 0; off >>= 1) {
         t += __shfl_down(t, off);
         ttl += __shfl_down(ttl, off);
     }
     if (lane == 0) {
-        g_add(&A.counters[CNT_TOKENS], (unsigned long long)t);
-        g_add(&A.counters[CNT_REC], (unsigned long long)ttl);
+        atomicAdd(&s_tot[0], t);
+        atomicAdd(&s_tot[1], ttl);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        g_add(&A.counters[CNT_TOKENS], (unsigned long long)s_tot[0]);
+        g_add(&A.counters[CNT_REC], (unsigned long long)s_tot[1]);
     }
     MRG_PT(6);
 #ifdef MRG_MAP_PROF
