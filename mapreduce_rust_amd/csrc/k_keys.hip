@@ -202,7 +202,8 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
                 X.k[k] = u64x2k{src[(uint64_t)i * 3], src[(uint64_t)i * 3 + 1]};
                 X.d[k] = (uint32_t)src[(uint64_t)i * 3 + 2];
             } else {
-                X.k[k] = *reinterpret_cast<const GASK u64x2k *>(src + (uint64_t)i * 2);
+                // read once: non-temporal (A/B: aggregation -1.5 %)
+                X.k[k] = __builtin_nontemporal_load(reinterpret_cast<const GASK u64x2k *>(src + (uint64_t)i * 2));
             }
         }
     };
