@@ -346,8 +346,11 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
             gk(A.out.k1)[j] = k.b;
             gk(A.out.cnt)[j] = s_cnt[i];
             gk(A.out.doc)[j] = IDX ? s_doc[i] : MRG_EMPTY_DOC;
-            gk(A.out.len)[j] = mrg_short_len(k.a, k.b);
+            const uint32_t L = mrg_short_len(k.a, k.b);
+            gk(A.out.len)[j] = L;
             gk(A.out.hoff)[j] = MRG_NO_HEAP;
+            // the partition right here (worker.rs:129), instead of a k_partition pass over the keys
+            if (A.n_reduce) gk(A.out.part)[j] = (uint32_t)(mrg_siphash_short(k.a, k.b, L) % (uint64_t)A.n_reduce);
         }
     }
 }

@@ -147,6 +147,7 @@ struct BucketArgs {
     uint32_t ablate;             // timing only (MRG_AGG_ABLATE): 1 = no table adds, 2 = no hash either
     uint32_t nsub;               // workgroups per bucket, each summing one hash sub-range (1 = whole bucket)
     uint64_t kcap;               // capacity of `out` (keys beyond it are counted, not written)
+    uint32_t n_reduce;           // partition of every key written (SipHash-1-3 % n_reduce; 0 = leave to k_partition)
 };
 // count32: the job has fewer than 2^32 tokens (32-bit LDS counts, a larger table); nreg <= 1024 then
 void mrg_launch_bucket_agg(const BucketArgs &a, bool indexer, bool count32, hipStream_t s);

@@ -344,11 +344,17 @@ void long_aggregate(mrg_ctx *c, LongItems li) {
 }
 
 // Distinct-key count + partition of every key (worker.rs:129).
-void finish_keys(mrg_ctx *c, bool counters_fresh = false) {
+// Keys [0, parted) already carry their partition (the bucket aggregation computes it as it writes them).
+void finish_keys(mrg_ctx *c, bool counters_fresh = false, uint64_t parted = 0) {
     if (!counters_fresh) read_counters(c);
     c->keys.n = c->h_cnt[CNT_KEYS];
     if (c->keys.n > c->keys.cap) raise(MRG_EINVAL, "internal: key set overflow");
-    mrg_launch_partition(c->keys.ks, c->keys.heap, c->keys.n, c->R, c->stream);
+    if (parted < c->keys.n) {
+        KeySet rest = c->keys.ks;  // SoA: the same arrays from key `parted` on (the heap offsets are absolute)
+        rest.k0 += parted; rest.k1 += parted; rest.cnt += parted; rest.hoff += parted;
+        rest.doc += parted; rest.len += parted; rest.part += parted;
+        mrg_launch_partition(rest, c->keys.heap, c->keys.n - parted, c->R, c->stream);
+    }
     c->st.distinct_keys = c->keys.n;
 }
 
@@ -415,6 +421,7 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         B.ablate = getenv("MRG_AGG_ABLATE") ? (uint32_t)atoi(getenv("MRG_AGG_ABLATE")) : 0u;
         B.nsub = nsub;
         B.kcap = c->keys.cap;
+        B.n_reduce = c->R;
         if (agg_launches > 1) {  // the map launch zeroed every counter; the map leaves these two alone
             HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
             HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
@@ -465,10 +472,12 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         }
         break;
     }
-    // the counters read after the aggregation are still current unless more keys were appended
+    // the counters read after the aggregation are still current unless more keys were appended; the
+    // keys it wrote already carry their partition
     const bool fresh = c->st.overflow_keys == 0 && li.n == 0;
+    const uint64_t parted = std::min<uint64_t>(c->h_cnt[CNT_KEYS], c->keys.cap);
     long_aggregate(c, li);
-    finish_keys(c, fresh);
+    finish_keys(c, fresh, parted);
     return true;
 }
 
