@@ -1132,9 +1132,9 @@ static int map_cap_for(int app, int lds_cap) {
     return lds_cap >= 4096 ? 4096 : 2048;
 }
 
-void mrg_launch_map(const MapArgs &h, MapArgs *a, int app, int grid, int lds_cap, hipStream_t s) {
+void mrg_launch_map(const MapArgs *h, MapArgs *a, int app, int grid, int lds_cap, hipStream_t s) {
     const bool idx = app == 1;
-    (void)hipMemcpyAsync(a, &h, sizeof(MapArgs), hipMemcpyHostToDevice, s);
+    if (h) (void)hipMemcpyAsync(a, h, sizeof(MapArgs), hipMemcpyHostToDevice, s);
     if (map_cap_for(app, lds_cap) == 4096) {
         if (idx) launch_map_t<4096, true>(a, grid, s);
         else launch_map_t<4096, false>(a, grid, s);

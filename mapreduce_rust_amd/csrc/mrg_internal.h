@@ -116,7 +116,8 @@ struct LongItems {
 
 // ---- k_map.hip
 // `dev_args` is device memory for one MapArgs (the kernel reads its arguments from there)
-void mrg_launch_map(const MapArgs &a, MapArgs *dev_args, int app, int grid, int lds_cap, hipStream_t s);
+// h: the args to copy to dev_args first (nullptr: already there)
+void mrg_launch_map(const MapArgs *h, MapArgs *dev_args, int app, int grid, int lds_cap, hipStream_t s);
 uint64_t mrg_map_tiles(uint64_t doc_lo, uint64_t doc_hi);  // wave blocks (NSUB KiB) of a document (16-B grid)
 int mrg_map_cap(int app, int lds_cap);  // LDS-table entries per map workgroup actually used for lds_cap
 int mrg_map_max_grid(int app, int lds_cap, int device);

@@ -180,6 +180,10 @@ struct mrg_ctx {
     Pool pool;
     unsigned long long *d_cnt = nullptr;  // CNT_N counters
     unsigned long long *h_cnt = nullptr;  // pinned mirror
+    // pinned staging of the small per-job host tables (document offsets, region bases, map args): one
+    // bump region, reset by job_begin (after its sync), so their copies are plain async DMA
+    uint8_t *h_stage = nullptr;
+    size_t stage_used = 0;
     bool timing = false;
     hipEvent_t ev[8] = {};
     int lds_cap = 4096;
@@ -229,6 +233,21 @@ uint32_t hash_bits(const mrg_ctx *c) { return (c->flags >> 8) & 0xFFu; }
 bool is_idx(const mrg_ctx *c) { return c->app == MRG_APP_INDEXER; }
 
 void sync(mrg_ctx *c) { HIPCHK(hipStreamSynchronize(c->stream)); }
+
+constexpr size_t MRG_STAGE_BYTES = 256u << 10;
+// Host -> device copy of a small table through the pinned staging region (falls back to a pageable
+// copy when the region is used up).  Valid only between job_begin and the job's next host wait.
+void h2d(mrg_ctx *c, void *dst, const void *src, size_t n) {
+    if (!n) return;
+    if (c->h_stage && c->stage_used + n <= MRG_STAGE_BYTES) {
+        uint8_t *p = c->h_stage + c->stage_used;
+        memcpy(p, src, n);
+        c->stage_used += (n + 63) & ~(size_t)63;
+        HIPCHK(hipMemcpyAsync(dst, p, n, hipMemcpyHostToDevice, c->stream));
+    } else {
+        HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->stream));
+    }
+}
 
 void read_counters(mrg_ctx *c) {
     HIPCHK(hipMemcpyAsync(c->h_cnt, c->d_cnt, sizeof(unsigned long long) * CNT_N, hipMemcpyDeviceToHost, c->stream));
@@ -800,6 +819,7 @@ void job_begin(mrg_ctx *c, int app, uint32_t R, uint32_t flags) {
     if (app != MRG_APP_WC && app != MRG_APP_INDEXER) raise(MRG_EINVAL, "unknown app %d", app);
     if (R == 0) raise(MRG_EINVAL, "n_reduce must be > 0");
     sync(c);
+    c->stage_used = 0;  // the previous job's staged copies are done
     keys_release(c);
     c->wide.release(c->pool);
     c->job = true;
@@ -834,9 +854,9 @@ void job_map(mrg_ctx *c) {
 
     uint64_t *d_doc_off = pget<uint64_t>(p, nd + 1), *d_cb = pget<uint64_t>(p, nd + 1);
     uint32_t *d_ids = pget<uint32_t>(p, nd);
-    HIPCHK(hipMemcpyAsync(d_doc_off, c->doc_off.data(), 8ull * (nd + 1), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d_cb, cb.data(), 8ull * (nd + 1), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d_ids, ids.data(), 4ull * nd, hipMemcpyHostToDevice, s));
+    h2d(c, d_doc_off, c->doc_off.data(), 8ull * (nd + 1));
+    h2d(c, d_cb, cb.data(), 8ull * (nd + 1));
+    h2d(c, d_ids, ids.data(), 4ull * nd);
 
     if (!c->map_grid) c->map_grid = mrg_map_max_grid(c->app, c->lds_cap, c->device);
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->map_grid, n_chunks));
@@ -882,8 +902,8 @@ void job_map(mrg_ctx *c) {
         M.ovf = pget<uint64_t>(p, (uint64_t)MRG_NBUCKET * ocap * RW);
         M.onext = pget<uint32_t>(p, MRG_NBUCKET);
         HIPCHK(hipMemsetAsync(M.onext, 0, 4ull * MRG_NBUCKET, s));
-        HIPCHK(hipMemcpyAsync(M.rbase, rbase.data(), 8ull * MRG_NBUCKET, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(M.bcap, bcap32.data(), 4ull * MRG_NBUCKET, hipMemcpyHostToDevice, s));
+        h2d(c, M.rbase, rbase.data(), 8ull * MRG_NBUCKET);
+        h2d(c, M.bcap, bcap32.data(), 4ull * MRG_NBUCKET);
         A.in = c->d_in;
         A.doc_off = d_doc_off;
         A.chunk_base = d_cb;
@@ -921,15 +941,17 @@ void job_map(mrg_ctx *c) {
         HIPCHK(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long) * CNT_N, s));
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_ERRPOS], 0xFF, sizeof(unsigned long long), s));
         ev_rec(c, 0);
-        mrg_launch_map(A, M.dargs, c->app, grid, c->lds_cap, s);  // also with no tiles: writes empty flush regions
+        h2d(c, M.dargs, &A, sizeof(MapArgs));
+        mrg_launch_map(nullptr, M.dargs, c->app, grid, c->lds_cap, s);  // also with no tiles: writes empty flush regions
         ev_rec(c, 1);
         HIPCHK(hipGetLastError());
         ++launches;
-        std::vector<uint32_t> onext(MRG_NBUCKET);
-        HIPCHK(hipMemcpyAsync(onext.data(), M.onext, 4ull * MRG_NBUCKET, hipMemcpyDeviceToHost, s));
+        // overflow-list fill into pinned scratch, then the counters: one host wait for both
+        uint32_t *onext = (uint32_t *)&c->h_cnt[CNT_N + 8];
+        HIPCHK(hipMemcpyAsync(onext, M.onext, 4ull * MRG_NBUCKET, hipMemcpyDeviceToHost, s));
         read_counters(c);
         c->st.map_spill = 0;
-        for (uint32_t v : onext) c->st.map_spill += std::min<uint64_t>(v, ocap);
+        for (int b = 0; b < MRG_NBUCKET; ++b) c->st.map_spill += std::min<uint64_t>(onext[b], ocap);
         if (M.prof) {
             unsigned long long pr[8];
             HIPCHK(hipMemcpy(pr, M.prof, sizeof pr, hipMemcpyDeviceToHost));
@@ -1570,7 +1592,9 @@ int mrg_open(int device, mrg_ctx **out) {
         c->stream = c->own;
         HIPCHK(hipMalloc(&c->d_cnt, sizeof(unsigned long long) * CNT_N));
         // CNT_N counters + pinned scratch (h_cnt[CNT_N]: the key sort's oversized-bucket count)
-        HIPCHK(hipHostMalloc(&c->h_cnt, sizeof(unsigned long long) * (CNT_N + 8), hipHostMallocDefault));
+        // [CNT_N, CNT_N + 8): scratch; [CNT_N + 8, + MRG_NBUCKET / 2): the map's overflow-list fill (u32)
+        HIPCHK(hipHostMalloc(&c->h_cnt, sizeof(unsigned long long) * (CNT_N + 8 + MRG_NBUCKET / 2), hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&c->h_stage, MRG_STAGE_BYTES, hipHostMallocDefault));
         for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
         if (const char *v = getenv("MRG_LDS_CAP")) c->lds_cap = atoi(v);
         *out = c;
@@ -1585,6 +1609,7 @@ int mrg_close(mrg_ctx *c) {
         for (auto &e : c->ev) (void)hipEventDestroy(e);
         (void)hipFree(c->d_cnt);
         (void)hipHostFree(c->h_cnt);
+        if (c->h_stage) (void)hipHostFree(c->h_stage);
         if (c->own) (void)hipStreamDestroy(c->own);
         delete c;
     });
