@@ -541,3 +541,53 @@ def test_worker_text_intermediates_through_files(tmp_path, corpus):
         assert w.reduce(r)
         assert sha((tmp_path / f"mr-{r}.txt").read_bytes()) == GOLDEN["wc"]["10"][f"mr-{r}.txt"], r
     w.close()
+
+
+@pytest.mark.parametrize("G", [1, 3, 300])
+def test_export_import_many_owners(ctx, corpus, G):
+    """The export by owner (part % G) and the re-import, at 1, 3 and 300 owners (300: more owners
+    than the export kernels count in LDS, so the per-key device-atomic path runs), with long (> 16
+    byte) keys in the exchange heap: the union of the owners' partitions equals the oracle."""
+    import torch
+    import mapreduce_rust_amd as M
+    import oracle_lib as O
+    from gpu_util import to_device
+    R = 600
+    longs = (b"pneumonoultramicroscopicsilicovolcanoconiosis supercalifragilisticexpialidocious "
+             b"antidisestablishmentarianism floccinaucinihilipilification ") * 50
+    docs = [corpus[0], corpus[1] + b" " + longs, corpus[2], longs + corpus[3]]
+    shards = [docs[0:2], docs[2:4]]
+    sends = []
+    for sh in shards:
+        t, off = to_device(sh)
+        ctx.job_begin(M.APP_WC, R)
+        ctx.set_input(t.data_ptr(), off)
+        ctx.map()
+        rec, heap = ctx.export_sizes(G)
+        drec = torch.empty(max(sum(rec), 1) * 40, dtype=torch.uint8, device="cuda:0")
+        dheap = torch.empty(max(sum(heap), 1), dtype=torch.uint8, device="cuda:0")
+        ctx.export(drec.data_ptr(), dheap.data_ptr())
+        sends.append((drec.cpu(), dheap.cpu(), rec, heap))
+    exp = O.wc(docs, R, O.FAST)
+    got = [None] * R
+    for owner in range(G):
+        recs, heaps, sr, shp = [], [], [], []
+        for drec, dheap, rec, heap in sends:
+            ro = sum(rec[:owner]) * 40
+            ho = sum(heap[:owner])
+            recs.append(drec[ro:ro + rec[owner] * 40])
+            heaps.append(dheap[ho:ho + heap[owner]])
+            sr.append(rec[owner])
+            shp.append(heap[owner])
+        Rt = torch.cat(recs + [torch.zeros(40, dtype=torch.uint8)]).to("cuda:0")
+        Ht = torch.cat(heaps + [torch.zeros(1, dtype=torch.uint8)]).to("cuda:0")
+        ctx.job_begin(M.APP_WC, R)
+        ctx.import_(Rt.data_ptr(), sum(sr), Ht.data_ptr(), sum(shp), sr, shp)
+        ctx.reduce()
+        o = ctx.outputs()
+        for r in range(R):
+            if r % G == owner:
+                got[r] = o[r]
+            else:
+                assert o[r] == b"", (owner, r)
+    assert got == exp
