@@ -1396,13 +1396,17 @@ __global__ __launch_bounds__(W_WG, 1) void k_wwrite(const uint64_t *keys, const 
     lds_barrier();
     const uint32_t K = s_kst[MRG_WIDE_MAXB2];
     uint64_t dst = leaf_off[l0];
-    for (uint32_t c0 = 0; c0 < K; c0 += W_WCH) {
+    // this thread's keys of chunk c0 (keys 2t, 2t + 1): leaf by a search of the running counts, then
+    // the key and count loads.  The next chunk's are fetched before this chunk is laid out and
+    // stored, so their leaf search and load latency overlap the current chunk's work.
+    struct Two {
         uint64_t a[2], c[2], n[2];
-        uint32_t len[2] = {0, 0}, nd[2] = {0, 0}, ll[2] = {0, 0};
+    };
+    auto fetch = [&](uint32_t c0, Two &F) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const uint32_t i = c0 + 2 * tid + (uint32_t)u;   // thread t: keys 2t, 2t + 1 of the chunk
-            a[u] = c[u] = n[u] = 0;
+            const uint32_t i = c0 + 2 * tid + (uint32_t)u;
+            F.a[u] = F.c[u] = F.n[u] = 0;
             if (i < K) {
                 uint32_t lo = 0, hi = nl;   // leaf l: s_kst[l] <= i < s_kst[l + 1] (last such l)
                 while (hi - lo > 1) {
@@ -1411,11 +1415,18 @@ __global__ __launch_bounds__(W_WG, 1) void k_wwrite(const uint64_t *keys, const 
                     else hi = mid;
                 }
                 const uint64_t slot = s_lout[lo] + (i - s_kst[lo]);
-                a[u] = keys[2 * slot];
-                c[u] = keys[2 * slot + 1];
-                n[u] = ocnt[slot];
+                F.a[u] = keys[2 * slot];
+                F.c[u] = keys[2 * slot + 1];
+                F.n[u] = ocnt[slot];
             }
         }
+    };
+    Two cur, nxt;
+    if (K) fetch(0, cur);
+    for (uint32_t c0 = 0; c0 < K; c0 += W_WCH) {
+        if (c0 + W_WCH < K) fetch(c0 + W_WCH, nxt);
+        const uint64_t *a = cur.a, *c = cur.c, *n = cur.n;
+        uint32_t len[2] = {0, 0}, nd[2] = {0, 0}, ll[2] = {0, 0};
 #pragma unroll
         for (int u = 0; u < 2; ++u)
             if (c0 + 2 * tid + (uint32_t)u < K) {
@@ -1450,6 +1461,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wwrite(const uint64_t *keys, const 
         for (uint64_t x = max(e4, a4) + tid; x < end; x += W_WG) out[x] = sb[sh + (x - dst)];
         dst = end;
         lds_barrier();
+        cur = nxt;
     }
 }
 
