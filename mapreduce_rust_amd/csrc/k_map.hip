@@ -209,8 +209,9 @@ struct alignas(16) KeyPair {
 // (Measured by simulation at C3: 8-way tag groups 69.2 % hits, 2-way sets 68.1 %.)
 //
 // Admission (doorkeeper): a key may claim an empty way only on its second sighting in this
-// workgroup -- the first sets its bit in a 128 Kibit LDS bitmap (indexed by hash bits above the set
-// index; 32 Kibit for the indexer) and goes to the tail.  The table fills once and keeps its keys, so without the filter it
+// workgroup -- the first sets its two bits in a 128 Kibit LDS Bloom filter (positions from the hash
+// bits above the set index and from a remix of the hash; 32 Kibit for the indexer) and goes to the
+// tail.  The table fills once and keeps its keys, so without the filter it
 // fills with whatever the first few thousand tokens hold, singletons included; with it, mostly with
 // repeated (frequent) keys.  Exactness is untouched: a token either adds to its key's slot or is
 // appended to the tail, and both are summed.
@@ -237,9 +238,14 @@ struct LdsTable {
     __device__ __forceinline__ bool admitted(uint32_t h) {
         if (!MRG_MAP_DOOR) return true;
         if (MRG_MAP_DOOR_LEVELS == 1) {
+            // a two-position Bloom filter: hash bits 11.. and a multiplicative remix of the hash
+            // (fewer false "seen before" while the table fills: simulated on the C3 stream, hits
+            // 72.2 -> 72.9 %); both atomics in flight together, and only on the claim path
             const uint32_t di = (h >> 11) & (DW * 32u - 1u);
-            const uint32_t bit = 1u << (di & 31u);
-            return (atomicOr(&door[di >> 5], bit) & bit) != 0u;
+            const uint32_t dj = ((h * 0x9E3779B1u) >> 15) & (DW * 32u - 1u);
+            const uint32_t bi = 1u << (di & 31u), bj = 1u << (dj & 31u);
+            const uint32_t oi = atomicOr(&door[di >> 5], bi), oj = atomicOr(&door[dj >> 5], bj);
+            return (oi & bi) != 0u && (oj & bj) != 0u;
         }
         const uint32_t di = (h >> 11) & (DW * 16u - 1u);
         const uint32_t lo = 1u << (2u * (di & 15u)), hi = lo << 1;
