@@ -1273,7 +1273,9 @@ void export_sizes(mrg_ctx *c, uint32_t n_owners, uint64_t *h_rec, uint64_t *h_he
     if (h_heap) memcpy(h_heap, c->exp_heap.data(), 8ull * n_owners);
 }
 
-void export_pack(mrg_ctx *c, void *d_rec, void *d_heap) {
+// wait = false: the caller consumes the packed records on the context's stream (the library's own
+// exchange): no host wait here
+void export_pack(mrg_ctx *c, void *d_rec, void *d_heap, bool wait = true) {
     need_job(c);
     if (!c->n_owners) raise(MRG_EINVAL, "call mrg_job_export_sizes first");
     Pool &p = c->pool;
@@ -1290,8 +1292,8 @@ void export_pack(mrg_ctx *c, void *d_rec, void *d_heap) {
     HIPCHK(hipMemsetAsync(cur, 0, 16ull * G, s));
     mrg_launch_export_pack(c->keys.ks, c->keys.heap, c->keys.n, G, d_base, d_base + G, cur, cur + G, (XRec *)d_rec,
                            (uint8_t *)d_heap, s);
-    sync(c);
-    p.put(d_base);
+    if (wait) sync(c);
+    p.put(d_base);  // later users of these blocks run after the pack on the same stream
     p.put(cur);
 }
 
@@ -1377,7 +1379,7 @@ void job_shuffle(mrg_ctx *c, mrg_comm *m) {
     }
     uint8_t *srec = pget<uint8_t>(p, sro[G] * MRG_XREC_BYTES + 16), *sheap = pget<uint8_t>(p, sho[G] + 16);
     uint8_t *rrec = pget<uint8_t>(p, rro[G] * MRG_XREC_BYTES + 16), *rheap = pget<uint8_t>(p, rho[G] + 16);
-    export_pack(c, srec, sheap);
+    export_pack(c, srec, sheap, false);
     const uint64_t X = MRG_XREC_BYTES;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     HIPCHK(hipEventCreate(&e0));
@@ -1399,15 +1401,14 @@ void job_shuffle(mrg_ctx *c, mrg_comm *m) {
     }
     NCCLCHK(ncclGroupEnd());
     HIPCHK(hipEventRecord(e1, s));
-    HIPCHK(hipEventSynchronize(e1));
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    p.put(srec);
+    p.put(srec);  // stream-ordered reuse only (see export_pack)
     p.put(sheap);
     const mrg_stats keep = c->st;
-    job_import(c, rrec, rro[G], rheap, rho[G], seg_rec.data(), seg_heap.data(), G);
+    job_import(c, rrec, rro[G], rheap, rho[G], seg_rec.data(), seg_heap.data(), G);  // ends with a host wait
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));  // e1 is done: the import waited for the stream
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     p.put(rrec);
     p.put(rheap);
     // the import's aggregation time is the reduce side's; the map-side stats stay those of the map
