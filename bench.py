@@ -257,7 +257,8 @@ def main():
                 "note": "libmrgpu RCCL send/recv group: max-over-ranks peer bytes / HIP-event time (median step)"}
 
     wl = {"zipf": ("C3: wc, Zipf(%.2f) ASCII text, vocab %d" % (a.zipf_s, a.vocab)) if world == 1 else
-          ("C4: wc, Zipf(%.2f) text sharded over %d GPUs, RCCL shuffle" % (a.zipf_s, world)),
+          ("C4: wc, Zipf(%.2f) text sharded over %d GPUs, %s shuffle"
+           % (a.zipf_s, world, "RCCL" if a.backend == "nccl" else "gloo (host-staged rehearsal)")),
           "unique": "C5: near-unique 12-char keys (1% repeats)" + ("" if world == 1 else ", %d GPUs" % world)}
     line = {
         "metric": "word-count input GB/s (whole node) at 1/2/4/8 MI355X + % of HBM roofline",
