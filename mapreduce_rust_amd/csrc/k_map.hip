@@ -232,6 +232,7 @@ struct LdsTable {
     KeyPair *key;
     unsigned int *cnt, *doc;
     unsigned int *door;
+    unsigned int *fill;  // slots claimed so far (never decreases: a claimed slot keeps its key)
 
     // seen before in this workgroup?  (records this sighting; collisions only admit early).  With
     // two levels, entries are 2-bit: admitted from the third sighting on.
@@ -271,6 +272,7 @@ struct LdsTable {
                 key[s].b = b;
                 if (IDX) doc[s] = d;
                 atomicAdd(&cnt[s], 1u);
+                atomicAdd(fill, 1u);
                 return true;
             }
             if (old == a) return false;  // being claimed by the same k0: miss (safe)
@@ -343,7 +345,7 @@ struct TailRegions {
 template <int CAP, bool IDX>
 __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint32_t hbits, LdsTable<CAP, IDX> &T,
                                            TailRegions R, GAS uint64_t *pool, bool ha, uint64_t a0, uint64_t a1,
-                                           bool hb, uint64_t b0, uint64_t b1, uint32_t docid) {
+                                           bool hb, uint64_t b0, uint64_t b1, uint32_t docid, bool may_claim) {
     constexpr uint32_t NS = LdsTable<CAP, IDX>::NS;
     const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
     const uint32_t hA = key_hash(a0, a1, dkey, hbits), hB = key_hash(b0, b1, dkey, hbits);
@@ -363,12 +365,16 @@ __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint3
         if (hitA) atomicAdd(&T.cnt[mA0 ? sA : sA + 1], 1u);
         if (hitB) atomicAdd(&T.cnt[mB0 ? sB : sB + 1], 1u);
     }
-    const bool eA0 = kA0.a == MRG_EMPTY_K0, eA1 = kA1.a == MRG_EMPTY_K0;
-    const bool eB0 = kB0.a == MRG_EMPTY_K0, eB1 = kB1.a == MRG_EMPTY_K0;
-    const bool nA = actA && !hitA && (eA0 || eA1), nB = actB && !hitB && (eB0 || eB1);
-    if (__any(nA || nB)) {
-        if (nA) hitA = T.claim(sA, eA0, eA1, a0, a1, dkey, hA);
-        if (nB) hitB = T.claim(sB, eB0, eB1, b0, b1, dkey, hB);
+    // empty ways exist only until the table has filled (wave-uniform: a stale count only means
+    // an unneeded test)
+    if (may_claim) {
+        const bool eA0 = kA0.a == MRG_EMPTY_K0, eA1 = kA1.a == MRG_EMPTY_K0;
+        const bool eB0 = kB0.a == MRG_EMPTY_K0, eB1 = kB1.a == MRG_EMPTY_K0;
+        const bool nA = actA && !hitA && (eA0 || eA1), nB = actB && !hitB && (eB0 || eB1);
+        if (__any(nA || nB)) {
+            if (nA) hitA = T.claim(sA, eA0, eA1, a0, a1, dkey, hA);
+            if (nB) hitB = T.claim(sB, eB0, eB1, b0, b1, dkey, hB);
+        }
     }
     const bool tA = ha && !hitA && !(abl & 1u), tB = hb && !hitB && !(abl & 1u);
     // both appends in one region (a lane adds 0 to the other token's cursor): one LDS round trip
@@ -556,6 +562,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
     __shared__ uint32_t s_next, s_ngen;                  // next block of the workgroup's share; list length
     __shared__ uint32_t s_tot[2];                        // workgroup totals: tokens, tail records
+    __shared__ unsigned int s_fill;                      // table slots claimed
     __shared__ unsigned int s_door[MRG_MAP_DOOR ? LdsTable<CAP, IDX>::DW : 1];  // admission bitmap
     static_assert(sizeof(s_q) >= CAP * sizeof(uint16_t), "flush ranks reuse the queues");
 
@@ -581,6 +588,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         s_ngen = 0;
         s_tot[0] = 0;
         s_tot[1] = 0;
+        s_fill = 0;
     }
     if (tid < 128) {
         const uint32_t c = mrg_uclass((uint32_t)tid);
@@ -599,7 +607,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const uint32_t zm = zmask(L, j), gm = zmask(g, j);
         s_sel[L * 17u + g][j] = ((0x00010203u + (gm & 0x01010101u)) & ~zm) | (0x0C0C0C0Cu & zm);
     }
-    LdsTable<CAP, IDX> table{s_key, s_cnt, s_doc, s_door};
+    LdsTable<CAP, IDX> table{s_key, s_cnt, s_doc, s_door, &s_fill};
     const TailRegions tails{s_tcur, s_tend};
     uint32_t my_tokens = 0;
     // uniform job parameters used in the hot loop, read once
@@ -806,6 +814,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const uint32_t total = (abl & 68u) ? 0u : lane_u32(incl, 63);
             MRG_PT(2);
             uint32_t nslow = 0;
+            const bool may_claim = __builtin_amdgcn_readfirstlane(*(volatile unsigned int *)&s_fill) < (uint32_t)CAP;
             my_tokens += (abl & 4u) ? cnt : 0u;
             wave_sync_lds();
 
@@ -826,8 +835,10 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 const uint32_t first = (uint32_t)__builtin_ctz(w | 0x80000000u);
                 const uint32_t last = 31u - (uint32_t)__builtin_clz(w | 1u);
                 const uint32_t span = last - first + 1u;
-                fast = act && ended && w != 0u && span <= 16u;
-                slow = act && (!ended || (w != 0u && span > 16u));
+                // bitwise on purpose: lane masks combined by SALU, no per-lane selects
+                const bool wz = w == 0u, big = span > 16u;
+                fast = act & ended & !wz & !big;
+                slow = act & (!ended | (!wz & big));
                 // deleted bytes inside the token ("don't"): one 1-byte gap is folded into the selectors
                 // below (key bytes from the gap on come from one window byte later); tokens with more
                 // gaps squeeze them out afterwards
@@ -899,7 +910,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                     nslow += na + (uint32_t)__builtin_popcountll(mb);
                 }
                 my_tokens += (fa ? 1u : 0u) + (fb ? 1u : 0u);
-                emit_fast2(A, abl, hbits, table, tails, pool, fa, a0, a1, fb, b0, b1, docid);
+                emit_fast2(A, abl, hbits, table, tails, pool, fa, a0, a1, fb, b0, b1, docid, may_claim);
             }
             // deferred slow tokens: the exact per-codepoint walker, one token per lane (forward
             // reads only: the staged bytes are [At, whi))

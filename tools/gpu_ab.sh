@@ -12,6 +12,6 @@ m = [float(re.search(r"map ([0-9.]+) ms", l).group(1)) for l in lines if "step: 
 a = [float(re.search(r"agg ([0-9.]+)", l).group(1)) for l in lines if "step: map" in l]
 so = [float(re.search(r"sort ([0-9.]+)", l).group(1)) for l in lines if "step: map" in l]
 j = json.loads(lines[-1])
-print(f"{sys.argv[1]:22s} map median {statistics.median(m):.3f} ms  agg median {statistics.median(a):.3f}  sort {statistics.median(so):.3f}  value {j['value']}  tail {j['job']['map_records']}")
+print(f"{sys.argv[1]:22s} map median {statistics.median(m):.3f} ms  agg median {statistics.median(a):.3f}  sort {statistics.median(so):.3f}  value {j['value']}  tail {j['job']['map_records']}  tokens {j['job']['tokens']}")
 PY
 done
