@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--cpu-slice-mib", type=int, default=1024, help="C3 slice for the W = cores CPU run")
     ap.add_argument("--cpu-w1-mib", type=int, default=128, help="C3 slice for the W = 1 CPU run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end leg (files on disk -> mrg_run_job)")
     ap.add_argument("--lds-cap", type=int, default=0)
     ap.add_argument("--shuffle-1", action="store_true",
                     help="N = 1 only: run the library's RCCL shuffle in a one-rank communicator every step (the "
@@ -118,6 +119,60 @@ def cpu_baseline(slice_files, w1_bytes, n_reduce):
                       f"map tasks, nReduce {n_reduce}, W = {W} worker threads (the host cores given to this job) "
                       f"running the reference's task structure (oracle/oracle.c restatement; no Rust toolchain)",
             "runs": runs}
+
+
+def end_to_end(buf, files, fbytes, n_reduce):
+    """SURVEY §8(d) end-to-end leg: the benchmark's own input written to local disk as data/gut-{m}.txt
+    files, then the whole job through mrg_run_job (the reference's read -> map -> reduce -> mr-{r}.txt
+    path, worker.rs:65-77, 167-179): file reads through pinned staging overlapped with the H2D copies,
+    the job, the D2H of the output and the mr-{r}.txt writes.  The files were just written, so they are
+    read from the page cache.  Also the C1 latency (the bundled 6-file corpus, nReduce 10)."""
+    d = tempfile.mkdtemp(prefix="mrg_e2e_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        paths = []
+        host = torch.empty(fbytes, dtype=torch.uint8, pin_memory=True)
+        for i in range(files):
+            host.copy_(buf[i * fbytes:(i + 1) * fbytes])
+            pth = os.path.join(d, f"gut-{i}.txt")
+            with open(pth, "wb") as f:
+                f.write(host.numpy().tobytes())
+            paths.append(pth)
+        del host
+        out = os.path.join(d, "out")
+        os.makedirs(out)
+        runs = []
+        for _ in range(2):  # the first run also faults in the library's host-side setup
+            t0 = time.perf_counter()
+            st = M.native.run_job(paths, n_reduce, M.APP_WC, out)
+            runs.append((time.perf_counter() - t0, st))
+        wall, st = min(runs, key=lambda x: x[0])
+        n = files * fbytes
+        c1 = [gzip.open(os.path.join(ROOT, "tests", "golden", "corpus", f"gut-{m}.txt.gz")).read() for m in range(6)]
+        c1p = []
+        for m, b in enumerate(c1):
+            pth = os.path.join(d, f"c1-{m}.txt")
+            with open(pth, "wb") as f:
+                f.write(b)
+            c1p.append(pth)
+        lat = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            M.native.run_job(c1p, 10, M.APP_WC, out)
+            lat.append((time.perf_counter() - t0) * 1e3)
+        res = {"end_to_end_gbs": round(n / wall / 1e9, 3), "ms": round(wall * 1e3, 1),
+               "phases_ms": {k: round(st[k], 1) for k in ("ms_open", "ms_read", "ms_map", "ms_shuffle", "ms_reduce",
+                                                          "ms_write")},
+               "input_bytes": n, "output_bytes": st["output_bytes"],
+               "read_gbs": round(n / (st["ms_read"] / 1e3) / 1e9, 2) if st["ms_read"] > 0 else None,
+               "c1_latency_ms": round(statistics.median(lat), 2),
+               "note": "mrg_run_job over the C3 input as %d files on local disk (page cache: written just before), "
+                       "nReduce %d: open + read/H2D + map + reduce + D2H + mr-{r}.txt writes; best of 2 runs; "
+                       "C1 = bundled corpus, median of 5" % (files, n_reduce)}
+        log(f"end-to-end: {res['end_to_end_gbs']} GB/s ({res['ms']} ms: {res['phases_ms']}), C1 {res['c1_latency_ms']} ms")
+        return res
+    finally:
+        import shutil
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def main():
@@ -290,6 +345,8 @@ def main():
         "job": {"tokens": st["tokens"], "map_records": st["map_records"], "distinct_keys": st["distinct_keys"],
                 "output_bytes": out_bytes, "map_launches": [s["map_launches"] for s in stats]},
     }
+    if world == 1 and not a.no_e2e and a.workload == "zipf":
+        line["end_to_end"] = end_to_end(buf, files, fbytes, a.reduce)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "zipf":
         n = min(a.cpu_slice_mib * MIB, shard)
         host = buf[:n].cpu().numpy().tobytes()

@@ -56,14 +56,19 @@ extern "C" {
    A test knob that forces hash collisions so the full-string tie-break paths are exercised. */
 #define MRG_FLAG_DEBUG_HASH_BITS(n) (((uint32_t)(n) & 0xFFu) << 8)
 
-/* Exchange record (mrg_job_export / mrg_job_import / mrg_parts): 40 bytes, little-endian.
- *   u64 k0, k1   first 16 key bytes, big-endian packed, zero padded (keys never contain NUL)
- *   u64 count    occurrences (wc) / 1 (indexer)
- *   u32 doc      global document id (indexer), 0xFFFFFFFF for wc
- *   u32 len      key length in bytes
- *   u64 heap     byte offset of the full key in the heap buffer if len > 16, else ~0
- * The heap holds the bytes of keys longer than 16 bytes. */
-#define MRG_XREC_BYTES 40
+/* Exchange record (mrg_job_export / mrg_job_import / mrg_parts): 24 bytes, little-endian.
+ *   short key (len <= 16):
+ *     u64 k0, k1   the key bytes, big-endian packed, zero padded (keys never contain NUL)
+ *     u32 v        wc: occurrences (a key counted more than 0xFFFFFFFF times is sent as several records,
+ *                  which the receiver sums); indexer: global document id
+ *     u32 len      key length in bytes
+ *   long key (len > 16):
+ *     u64 heap     byte offset of the key bytes in the sender's heap segment
+ *     u64 count    occurrences (wc) / 1 (indexer)
+ *     u32 v        global document id (indexer), 0xFFFFFFFF (wc)
+ *     u32 len      key length in bytes
+ * The heap holds the bytes of keys longer than 16 bytes.  (Format 2; format 1 had 40-byte records.) */
+#define MRG_XREC_BYTES 24
 
 typedef struct mrg_ctx mrg_ctx;
 typedef struct mrg_parts mrg_parts;
@@ -88,6 +93,10 @@ typedef struct {
     uint64_t map_spill;        /* map records that overflowed their tail region into a bucket's shared
                                   overflow list (last map launch) */
 } mrg_stats;
+
+/* ABI history: 1 = round-1 layout; 2 = mrg_run_job's last argument is n_gpus (was a device index);
+ * 3 = 24-byte exchange records (were 40), mrg_run_get_stats.  mrg_version() names the ABI it implements. */
+#define MRG_ABI_VERSION 3
 
 const char *mrg_last_error(void);
 const char *mrg_version(void);
@@ -194,9 +203,28 @@ int mrg_reduce_text(mrg_ctx *ctx, const uint8_t *const *h_files, const uint64_t 
  * coordinator.rs:137-176), the shuffle is mrg_job_shuffle, GPU g reduces and writes out_dir/mr-{r}.txt
  * for r % n_gpus == g (the reduce task ids, coordinator.rs:178-215).  With MRG_FLAG_FINAL_TXT also
  * out_dir/final.txt: each GPU sorts the lines it holds, the host merges the n_gpus sorted runs.
- * Indexer document names are the file paths as given (the reference opens "data/gut-{m}.txt"). */
+ * Indexer document names are the file paths as given (the reference opens "data/gut-{m}.txt").
+ * Files are read by several host threads per GPU through pinned staging, overlapped with the copies
+ * to the device.  Every phase runs on all GPUs and is joined before the next, and the exchange agrees
+ * on every rank's status before each transfer: a failure on any GPU fails the call, never hangs it.
+ * (ABI 2 changed the last argument from a device index to n_gpus.) */
 int mrg_run_job(const char *const *files, size_t n_files, uint32_t n_reduce, int app, const char *out_dir,
                 uint32_t flags, int n_gpus);
+
+/* Wall-clock phases of the last mrg_run_job on the calling thread (host clock, milliseconds). */
+typedef struct {
+    double ms_total;        /* the whole call */
+    double ms_open;         /* contexts + communicators */
+    double ms_read;         /* input files -> device (read + H2D, overlapped; slowest GPU) */
+    double ms_map;          /* map + aggregation after the read (slowest GPU) */
+    double ms_shuffle;      /* the exchange (0 without a communicator) */
+    double ms_reduce;       /* sort + format + D2H of the output (+ final.txt) */
+    double ms_write;        /* mr-{r}.txt (+ final.txt) files */
+    uint64_t input_bytes;
+    uint64_t output_bytes;  /* bytes of all mr-{r}.txt */
+    int n_gpus;
+} mrg_run_stats;
+int mrg_run_get_stats(mrg_run_stats *out);
 
 /* Free host memory returned by the library (mrg_reduce / mrg_map_text / mrg_reduce_text output). */
 void mrg_free(void *p);

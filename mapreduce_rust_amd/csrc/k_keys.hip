@@ -387,7 +387,10 @@ __device__ __forceinline__ void table_add(const TableArgs &T, uint64_t a, uint64
                 }
             }
         }
-        slot = (slot + 1u) & (T.cap - 1);
+        // triangular steps (+1, +2, +3, ...: every slot of the power-of-two table is reached): no
+        // primary clusters, so few probes even when the hash values crowd into part of the table
+        // (the collision test knob truncates them to 20 bits while the table has more slots)
+        slot = (slot + probe + 1u) & (T.cap - 1);
     }
 }
 
@@ -398,11 +401,20 @@ __global__ void k_table_insert(TableArgs T, const uint64_t *k0, const uint64_t *
     table_add(T, k0[i], k1[i], idx ? doc[i] : MRG_EMPTY_DOC, cnt[i], idx);
 }
 
+// short exchange records (include/mrgpu.h): v = count (wc) / doc id (indexer)
 __global__ void k_table_insert_x(TableArgs T, const XRec *x, uint64_t n, bool idx) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const XRec r = x[i];
     if (r.len > 16u) return;  // long keys take the fingerprint-sort path
+    table_add(T, r.a, r.b, idx ? r.v : MRG_EMPTY_DOC, idx ? 1ull : (uint64_t)r.v, idx);
+}
+
+__global__ void k_table_insert_l(TableArgs T, const LRec *x, uint64_t n, bool idx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const LRec r = x[i];
+    if (r.len > 16u) return;
     table_add(T, r.k0, r.k1, idx ? r.doc : MRG_EMPTY_DOC, r.cnt, idx);
 }
 
@@ -571,17 +583,41 @@ __global__ void k_long_emit(const uint32_t *rep, const uint64_t *k0, const uint6
     out.hoff[j] = hoff[i];
 }
 
-// received exchange records with long keys -> long items over the received heap
+// segment (sender) of record i: the first s with i < seg_rec_end[s] (binary search)
+__device__ __forceinline__ uint32_t seg_of(const uint64_t *seg_rec_end, uint32_t n_segs, uint64_t i) {
+    uint32_t lo = 0, hi = n_segs - 1u;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (i < seg_rec_end[mid]) hi = mid;
+        else lo = mid + 1u;
+    }
+    return lo;
+}
+
+// received exchange records with long keys -> long items over the received heap (long form: a = heap
+// offset in the sender's segment, b = count, v = doc)
 __global__ void k_x_split_long(const XRec *x, uint64_t n, const uint64_t *seg_rec_end, const uint64_t *seg_heap_base,
+                               uint32_t n_segs, LongItems li, unsigned long long *counter, bool idx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool lng = i < n && x[i].len > 16u;
+    const uint64_t j = mrg_wave_append(counter, lng);
+    if (!lng) return;
+    const XRec r = x[i];
+    li.start[j] = seg_heap_base[seg_of(seg_rec_end, n_segs, i)] + r.a;
+    li.rawlen[j] = r.len;
+    li.doc[j] = idx ? r.v : MRG_EMPTY_DOC;
+    li.cnt[j] = idx ? 1ull : r.b;
+}
+
+// the same for the text reduce's line records (key bytes addressed in their file's segment)
+__global__ void k_l_split_long(const LRec *x, uint64_t n, const uint64_t *seg_rec_end, const uint64_t *seg_heap_base,
                                uint32_t n_segs, LongItems li, unsigned long long *counter) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool lng = i < n && x[i].len > 16u;
     const uint64_t j = mrg_wave_append(counter, lng);
     if (!lng) return;
-    uint32_t sgi = 0;  // segment (sender) of record i
-    while (sgi + 1 < n_segs && i >= seg_rec_end[sgi]) ++sgi;
-    const XRec r = x[i];
-    li.start[j] = seg_heap_base[sgi] + r.heap;
+    const LRec r = x[i];
+    li.start[j] = seg_heap_base[seg_of(seg_rec_end, n_segs, i)] + r.heap;
     li.rawlen[j] = r.len;
     li.doc[j] = r.doc;
     li.cnt[j] = r.cnt;
@@ -595,8 +631,9 @@ constexpr int EXP_WG = 1024;
 constexpr uint32_t EXP_MAXO = 256;
 
 __global__ __launch_bounds__(EXP_WG) void k_export_count(KeySet ks, uint64_t n, uint32_t n_owners,
-                                                         unsigned long long *rec_cnt, unsigned long long *heap_cnt) {
-    __shared__ uint32_t s_rc[EXP_MAXO];
+                                                         unsigned long long *rec_cnt, unsigned long long *heap_cnt,
+                                                         bool idx, uint64_t vmax) {
+    __shared__ unsigned long long s_rc[EXP_MAXO];
     __shared__ unsigned long long s_hc[EXP_MAXO];
     const bool lds = n_owners <= EXP_MAXO;
     if (lds)
@@ -609,11 +646,12 @@ __global__ __launch_bounds__(EXP_WG) void k_export_count(KeySet ks, uint64_t n, 
     if (i < n) {
         const uint32_t o = ks.part[i] % n_owners;
         const uint32_t len = ks.len[i];
+        const unsigned long long nr = mrg_xrec_per_key(ks.cnt[i], len, idx, vmax);
         if (lds) {
-            atomicAdd(&s_rc[o], 1u);
+            atomicAdd(&s_rc[o], nr);
             if (len > 16u) atomicAdd(&s_hc[o], (unsigned long long)len);
         } else {
-            atomicAdd(&rec_cnt[o], 1ull);
+            atomicAdd(&rec_cnt[o], nr);
             if (len > 16u) atomicAdd(&heap_cnt[o], (unsigned long long)len);
         }
     }
@@ -628,8 +666,8 @@ __global__ __launch_bounds__(EXP_WG) void k_export_count(KeySet ks, uint64_t n, 
 __global__ __launch_bounds__(EXP_WG) void k_export_pack(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t n_owners,
                                                         const uint64_t *rec_base, const uint64_t *heap_base,
                                                         unsigned long long *rec_cur, unsigned long long *heap_cur,
-                                                        XRec *out, uint8_t *out_heap) {
-    __shared__ uint32_t s_rc[EXP_MAXO];
+                                                        XRec *out, uint8_t *out_heap, bool idx, uint64_t vmax) {
+    __shared__ unsigned long long s_rc[EXP_MAXO];
     __shared__ unsigned long long s_hc[EXP_MAXO], s_rb[EXP_MAXO], s_hb[EXP_MAXO];
     const bool lds = n_owners <= EXP_MAXO;
     if (lds)
@@ -641,15 +679,18 @@ __global__ __launch_bounds__(EXP_WG) void k_export_pack(KeySet ks, const uint8_t
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool act = i < n;
     uint32_t o = 0, len = 0;
+    uint64_t cnt = 0, nr = 0;
     unsigned long long lr = 0, lh = 0;  // this key's rank / heap offset inside the workgroup's range
     if (act) {
         o = ks.part[i] % n_owners;
         len = ks.len[i];
+        cnt = ks.cnt[i];
+        nr = mrg_xrec_per_key(cnt, len, idx, vmax);
         if (lds) {
-            lr = atomicAdd(&s_rc[o], 1u);
+            lr = atomicAdd(&s_rc[o], (unsigned long long)nr);
             if (len > 16u) lh = atomicAdd(&s_hc[o], (unsigned long long)len);
         } else {
-            lr = atomicAdd(&rec_cur[o], 1ull);
+            lr = atomicAdd(&rec_cur[o], (unsigned long long)nr);
             if (len > 16u) lh = atomicAdd(&heap_cur[o], (unsigned long long)len);
         }
     }
@@ -668,19 +709,30 @@ __global__ __launch_bounds__(EXP_WG) void k_export_pack(KeySet ks, const uint8_t
     if (!act) return;
     const uint64_t slot = rec_base[o] + lr;
     XRec r;
-    r.k0 = ks.k0[i];
-    r.k1 = ks.k1[i];
-    r.cnt = ks.cnt[i];
-    r.doc = ks.doc[i];
     r.len = len;
-    r.heap = MRG_NO_HEAP;
-    if (len > 16u) {  // heap offset relative to the owner's segment
+    if (len > 16u) {  // long form: heap offset relative to the owner's segment, 64-bit count
         const uint8_t *src = heap + ks.hoff[i];
         uint8_t *dst = out_heap + heap_base[o] + lh;
         for (uint32_t b = 0; b < len; ++b) dst[b] = src[b];
-        r.heap = lh;
+        r.a = lh;
+        r.b = idx ? 1ull : cnt;
+        r.v = idx ? ks.doc[i] : MRG_EMPTY_DOC;
+        out[slot] = r;
+        return;
     }
-    out[slot] = r;
+    r.a = ks.k0[i];
+    r.b = ks.k1[i];
+    if (idx) {
+        r.v = ks.doc[i];
+        out[slot] = r;
+        return;
+    }
+    for (uint64_t k = 0; k < nr; ++k) {  // counts above 32 bits: several records, summed by the receiver
+        const uint64_t c = cnt > vmax ? vmax : cnt;
+        cnt -= c;
+        r.v = (uint32_t)c;
+        out[slot + k] = r;
+    }
 }
 
 __global__ void k_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, SortRec *out) {
@@ -727,6 +779,10 @@ void mrg_launch_table_insert_x(const TableArgs &t, const XRec *x, uint64_t n, bo
     if (!n) return;
     hipLaunchKernelGGL(k_table_insert_x, grid_for(n), dim3(256), 0, s, t, x, n, indexer);
 }
+void mrg_launch_table_insert_l(const TableArgs &t, const LRec *x, uint64_t n, bool indexer, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_table_insert_l, grid_for(n), dim3(256), 0, s, t, x, n, indexer);
+}
 void mrg_launch_table_compact(const TableArgs &t, bool indexer, KeySet out, unsigned long long *counter,
                               hipStream_t s) {
     hipLaunchKernelGGL(k_table_compact, grid_for(t.cap, TC_WG), dim3(TC_WG), 0, s, t, indexer, out, counter);
@@ -752,22 +808,30 @@ void mrg_launch_long_emit(const uint32_t *rep, const uint64_t *cnt_in, const uin
                        (const unsigned long long *)acc, out, counter, indexer);
 }
 void mrg_launch_x_split_long(const XRec *x, uint64_t n, const uint64_t *seg_rec_end, const uint64_t *seg_heap_base,
-                             uint32_t n_segs, LongItems li, unsigned long long *counter, hipStream_t s) {
+                             uint32_t n_segs, LongItems li, unsigned long long *counter, bool indexer, hipStream_t s) {
     if (!n) return;
     hipLaunchKernelGGL(k_x_split_long, grid_for(n), dim3(256), 0, s, x, n, seg_rec_end, seg_heap_base, n_segs, li,
+                       counter, indexer);
+}
+void mrg_launch_l_split_long(const LRec *x, uint64_t n, const uint64_t *seg_rec_end, const uint64_t *seg_heap_base,
+                             uint32_t n_segs, LongItems li, unsigned long long *counter, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_l_split_long, grid_for(n), dim3(256), 0, s, x, n, seg_rec_end, seg_heap_base, n_segs, li,
                        counter);
 }
 void mrg_launch_export_count(KeySet ks, uint64_t n, uint32_t n_owners, unsigned long long *rec_cnt,
-                             unsigned long long *heap_cnt, hipStream_t s) {
+                             unsigned long long *heap_cnt, bool indexer, uint64_t vmax, hipStream_t s) {
     if (!n) return;
-    hipLaunchKernelGGL(k_export_count, grid_for(n, EXP_WG), dim3(EXP_WG), 0, s, ks, n, n_owners, rec_cnt, heap_cnt);
+    hipLaunchKernelGGL(k_export_count, grid_for(n, EXP_WG), dim3(EXP_WG), 0, s, ks, n, n_owners, rec_cnt, heap_cnt,
+                       indexer, vmax);
 }
 void mrg_launch_export_pack(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t n_owners,
                             const uint64_t *rec_base, const uint64_t *heap_base, unsigned long long *rec_cur,
-                            unsigned long long *heap_cur, XRec *out, uint8_t *out_heap, hipStream_t s) {
+                            unsigned long long *heap_cur, XRec *out, uint8_t *out_heap, bool indexer, uint64_t vmax,
+                            hipStream_t s) {
     if (!n) return;
     hipLaunchKernelGGL(k_export_pack, grid_for(n, EXP_WG), dim3(EXP_WG), 0, s, ks, heap, n, n_owners, rec_base,
-                       heap_base, rec_cur, heap_cur, out, out_heap);
+                       heap_base, rec_cur, heap_cur, out, out_heap, indexer, vmax);
 }
 void mrg_launch_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, void *recs, hipStream_t s) {
     if (!n) return;

@@ -237,7 +237,7 @@ __global__ void k_utf8_check(const uint8_t *in, uint64_t n, unsigned long long *
 // reference's map never writes one): both are reported in err[1].  Lines with an empty key are
 // counted in nempty (the reduce loop folds them into the next group, see mrgpu.cpp).
 __global__ void k_text_lines(const uint8_t *in, const uint64_t *fo, const uint64_t *fe, uint32_t nf, uint64_t nseg,
-                             const uint64_t *base, uint64_t *cnt, XRec *out, unsigned long long *err,
+                             const uint64_t *base, uint64_t *cnt, LRec *out, unsigned long long *err,
                              unsigned long long *nempty) {
     const uint64_t seg = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (seg >= nseg) return;
@@ -284,7 +284,7 @@ __global__ void k_text_lines(const uint8_t *in, const uint64_t *fo, const uint64
             continue;
         }
         if (out) {
-            XRec x;
+            LRec x;
             x.k0 = k0;
             x.k1 = k1;
             x.cnt = 1;
@@ -326,7 +326,7 @@ void mrg_launch_utf8_check(const uint8_t *in, uint64_t n, unsigned long long *er
     if (n) hipLaunchKernelGGL(k_utf8_check, grid_for(n), dim3(256), 0, s, in, n, err);
 }
 void mrg_launch_text_lines(const uint8_t *in, const uint64_t *fo, const uint64_t *fe, uint32_t nf, uint64_t nseg,
-                           const uint64_t *base, uint64_t *cnt, XRec *out, unsigned long long *err,
+                           const uint64_t *base, uint64_t *cnt, LRec *out, unsigned long long *err,
                            unsigned long long *nempty, hipStream_t s) {
     if (nseg)
         hipLaunchKernelGGL(k_text_lines, grid_for(nseg), dim3(256), 0, s, in, fo, fe, nf, nseg, base, cnt, out, err,

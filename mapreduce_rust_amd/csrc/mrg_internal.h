@@ -95,13 +95,30 @@ struct TableArgs {
     uint32_t hash_bits;
 };
 
-// Exchange record, MRG_XREC_BYTES = 40 (include/mrgpu.h)
+// Exchange record, MRG_XREC_BYTES = 24 (include/mrgpu.h).  Short form (len <= 16): a, b = the packed
+// key, v = count (wc; a count above MRG_XREC_VMAX goes out as several records, which the receiver
+// sums) or the doc id (indexer).  Long form (len > 16): a = heap offset of the key bytes in the
+// sender's heap segment, b = count (wc) / 1 (indexer), v = doc id (indexer) / MRG_EMPTY_DOC (wc).
 struct XRec {
+    uint64_t a, b;
+    uint32_t v, len;
+};
+static_assert(sizeof(XRec) == 24, "XRec layout");
+#define MRG_XREC_VMAX 0xFFFFFFFFull
+// Records per key of the export: short wc keys carry at most vmax (MRG_XREC_VMAX; smaller only as a
+// test knob) of their count per record
+__host__ __device__ inline uint64_t mrg_xrec_per_key(uint64_t cnt, uint32_t len, bool indexer, uint64_t vmax) {
+    return (indexer || len > 16u || cnt <= vmax) ? 1ull : (cnt + vmax - 1u) / vmax;
+}
+
+// Line record of the text reduce (k_text.hip -> mrg_reduce_text): one "key value" line of an
+// intermediate file; keys longer than 16 bytes are addressed in place in the file buffer.
+struct LRec {
     uint64_t k0, k1, cnt;
     uint32_t doc, len;
     uint64_t heap;
 };
-static_assert(sizeof(XRec) == 40, "XRec layout");
+static_assert(sizeof(LRec) == 40, "LRec layout");
 
 // Long items: keys > 16 bytes, as raw byte ranges of `base` (input text or a received heap).
 struct LongItems {
@@ -166,6 +183,7 @@ void mrg_launch_table_clear(const TableArgs &t, bool indexer, hipStream_t s);
 void mrg_launch_table_insert(const TableArgs &t, const uint64_t *k0, const uint64_t *k1, const uint32_t *cnt32,
                              const uint32_t *doc, uint64_t n, bool indexer, hipStream_t s);
 void mrg_launch_table_insert_x(const TableArgs &t, const XRec *x, uint64_t n, bool indexer, hipStream_t s);
+void mrg_launch_table_insert_l(const TableArgs &t, const LRec *x, uint64_t n, bool indexer, hipStream_t s);
 void mrg_launch_table_compact(const TableArgs &t, bool indexer, KeySet out, unsigned long long *counter,
                               hipStream_t s);
 void mrg_launch_partition(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t n_reduce, hipStream_t s);
@@ -177,12 +195,15 @@ void mrg_launch_long_emit(const uint32_t *rep, const uint64_t *cnt_in, const uin
                           unsigned long long *acc, KeySet out, unsigned long long *counter, bool indexer,
                           hipStream_t s);
 void mrg_launch_x_split_long(const XRec *x, uint64_t n, const uint64_t *seg_rec_end, const uint64_t *seg_heap_base,
+                             uint32_t n_segs, LongItems li, unsigned long long *counter, bool indexer, hipStream_t s);
+void mrg_launch_l_split_long(const LRec *x, uint64_t n, const uint64_t *seg_rec_end, const uint64_t *seg_heap_base,
                              uint32_t n_segs, LongItems li, unsigned long long *counter, hipStream_t s);
 void mrg_launch_export_count(KeySet ks, uint64_t n, uint32_t n_owners, unsigned long long *rec_cnt,
-                             unsigned long long *heap_cnt, hipStream_t s);
+                             unsigned long long *heap_cnt, bool indexer, uint64_t vmax, hipStream_t s);
 void mrg_launch_export_pack(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t n_owners,
                             const uint64_t *rec_base, const uint64_t *heap_base, unsigned long long *rec_cur,
-                            unsigned long long *heap_cur, XRec *out, uint8_t *out_heap, hipStream_t s);
+                            unsigned long long *heap_cur, XRec *out, uint8_t *out_heap, bool indexer, uint64_t vmax,
+                            hipStream_t s);
 void mrg_launch_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, void *recs, hipStream_t s);
 void mrg_launch_fill_u32(uint32_t *p, uint32_t v, uint64_t n, hipStream_t s);
 void mrg_launch_fill_u64(uint64_t *p, uint64_t v, uint64_t n, hipStream_t s);
@@ -264,7 +285,7 @@ void mrg_launch_text_write(const uint8_t *in, const TextTok *t, const uint32_t *
                            uint8_t *out, hipStream_t s);
 void mrg_launch_utf8_check(const uint8_t *in, uint64_t n, unsigned long long *err, hipStream_t s);
 void mrg_launch_text_lines(const uint8_t *in, const uint64_t *fo, const uint64_t *fe, uint32_t nf, uint64_t nseg,
-                           const uint64_t *base, uint64_t *cnt, XRec *out, unsigned long long *err,
+                           const uint64_t *base, uint64_t *cnt, LRec *out, unsigned long long *err,
                            unsigned long long *nempty, hipStream_t s);
 void mrg_launch_add_first(const SortRec *r, KeySet ks, uint64_t v, hipStream_t s);
 

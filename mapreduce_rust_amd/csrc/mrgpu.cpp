@@ -14,8 +14,15 @@
 
 #include <rccl/rccl.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -23,6 +30,8 @@
 
 #include "mrg_internal.h"
 #include "mrgpu.h"
+
+static_assert(sizeof(XRec) == MRG_XREC_BYTES, "exchange record layout (include/mrgpu.h)");
 
 namespace {
 
@@ -205,6 +214,7 @@ struct mrg_ctx {
     bool mapped = false;
     uint32_t n_owners = 0;
     std::vector<uint64_t> exp_rec, exp_heap;
+    uint64_t xrec_vmax = MRG_XREC_VMAX;  // count per short export record (test knob MRG_TEST_XREC_VMAX)
     uint8_t *d_out = nullptr;
     uint64_t out_cap = 0, out_bytes = 0;
     std::vector<uint64_t> part_off;
@@ -219,6 +229,11 @@ struct mrg_ctx {
 struct mrg_comm {
     ncclComm_t comm = nullptr;
     int n = 0, rank = 0, device = 0;
+    // preallocated at init, so the exchange never allocates before a collective that its peers are
+    // already waiting in: the counts message [3 * n send | 3 * n receive] and the status word
+    uint64_t *d_counts = nullptr;
+    int *d_flag = nullptr;
+    std::atomic<bool> aborted{false};  // ncclCommAbort was called (by this rank or by mrg_run_job's watchdog)
 };
 
 struct mrg_parts {
@@ -297,7 +312,8 @@ uint64_t pow2_at_least(uint64_t x) {
 struct ShortSrc {
     const uint64_t *k0 = nullptr, *k1 = nullptr;
     const uint32_t *cnt = nullptr, *doc = nullptr;
-    const XRec *x = nullptr;
+    const XRec *x = nullptr;   // exchange records (short form only; long ones take the long path)
+    const LRec *lx = nullptr;  // text-reduce line records
     uint64_t n = 0;
 };
 
@@ -317,6 +333,7 @@ void table_aggregate(mrg_ctx *c, const ShortSrc &src) {
         T.hash_bits = hash_bits(c);
         mrg_launch_table_clear(T, idx, s);
         if (src.x) mrg_launch_table_insert_x(T, src.x, src.n, idx, s);
+        else if (src.lx) mrg_launch_table_insert_l(T, src.lx, src.n, idx, s);
         else mrg_launch_table_insert(T, src.k0, src.k1, src.cnt, src.doc, src.n, idx, s);
         mrg_launch_table_compact(T, idx, c->keys.ks, &c->d_cnt[CNT_KEYS], s);
         p.put(T.tk0); p.put(T.tk1); p.put(T.tcnt); p.put(T.tdoc);
@@ -469,6 +486,8 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         const char *wenv = getenv("MRG_WIDE");  // MRG_WIDE=0 pins the bucket path (tests of its overflow)
         if (!idx && novf > heavy && !(wenv && atoi(wenv) == 0)) {
             p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
+            c->agg_nsub = 1;  // the next job starts from one workgroup per bucket (a low-cardinality job
+                              // would otherwise stream every bucket 16 times)
             if (getenv("MRG_DEBUG")) fprintf(stderr, "[mrgpu] bucket agg: %llu overflow records -> wide\n", (unsigned long long)novf);
             return false;
         }
@@ -842,6 +861,8 @@ void job_begin(mrg_ctx *c, int app, uint32_t R, uint32_t flags) {
 void job_map(mrg_ctx *c) {
     need_job(c);
     if (c->doc_off.empty()) raise(MRG_EINVAL, "no input: call mrg_job_set_input first");
+    c->wide.release(c->pool);  // a second map of the same job replaces the first one's keys
+    c->mapped = c->reduced = false;
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     const uint32_t nd = (uint32_t)c->doc_off.size() - 1;
@@ -1261,7 +1282,8 @@ void export_sizes(mrg_ctx *c, uint32_t n_owners, uint64_t *h_rec, uint64_t *h_he
     hipStream_t s = c->stream;
     unsigned long long *d = pget<unsigned long long>(p, 2ull * n_owners);
     HIPCHK(hipMemsetAsync(d, 0, 16ull * n_owners, s));
-    mrg_launch_export_count(c->keys.ks, c->keys.n, n_owners, d, d + n_owners, s);
+    c->xrec_vmax = std::max<uint64_t>(1, std::min<uint64_t>(MRG_XREC_VMAX, env_u64("MRG_TEST_XREC_VMAX", MRG_XREC_VMAX)));
+    mrg_launch_export_count(c->keys.ks, c->keys.n, n_owners, d, d + n_owners, is_idx(c), c->xrec_vmax, s);
     std::vector<uint64_t> h(2ull * n_owners);
     HIPCHK(hipMemcpyAsync(h.data(), d, 16ull * n_owners, hipMemcpyDeviceToHost, s));
     sync(c);
@@ -1291,15 +1313,18 @@ void export_pack(mrg_ctx *c, void *d_rec, void *d_heap, bool wait = true) {
     HIPCHK(hipMemcpyAsync(d_base, base.data(), 16ull * G, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(cur, 0, 16ull * G, s));
     mrg_launch_export_pack(c->keys.ks, c->keys.heap, c->keys.n, G, d_base, d_base + G, cur, cur + G, (XRec *)d_rec,
-                           (uint8_t *)d_heap, s);
+                           (uint8_t *)d_heap, is_idx(c), c->xrec_vmax, s);
     if (wait) sync(c);
     p.put(d_base);  // later users of these blocks run after the pack on the same stream
     p.put(cur);
 }
 
-void job_import(mrg_ctx *c, const void *d_rec, uint64_t n_rec, const void *d_heap, uint64_t heap_bytes,
-                const uint64_t *seg_recs, const uint64_t *seg_heap, uint32_t n_segs) {
+// Received records -> the job's keys: exchange records (xr, include/mrgpu.h) or the text reduce's
+// line records (lr, k_text.hip).
+void import_recs(mrg_ctx *c, const XRec *xr, const LRec *lr, uint64_t n_rec, const void *d_heap, uint64_t heap_bytes,
+                 const uint64_t *seg_recs, const uint64_t *seg_heap, uint32_t n_segs) {
     need_job(c);
+    c->wide.release(c->pool);  // the imported records replace the job's keys, whatever path the map took
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     std::vector<uint64_t> rec_end, heap_base;
@@ -1328,11 +1353,13 @@ void job_import(mrg_ctx *c, const void *d_rec, uint64_t n_rec, const void *d_hea
     li.cnt = pget<uint64_t>(p, n_rec);
     li.verbatim = 1;  // the exchange heap holds exact key bytes
     HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_LONG], 0, 8, s));
-    mrg_launch_x_split_long((const XRec *)d_rec, n_rec, d_seg, d_seg + n_segs, n_segs, li, &c->d_cnt[CNT_LONG], s);
+    if (xr) mrg_launch_x_split_long(xr, n_rec, d_seg, d_seg + n_segs, n_segs, li, &c->d_cnt[CNT_LONG], is_idx(c), s);
+    else mrg_launch_l_split_long(lr, n_rec, d_seg, d_seg + n_segs, n_segs, li, &c->d_cnt[CNT_LONG], s);
     read_counters(c);
     li.n = c->h_cnt[CNT_LONG];
     ShortSrc src;
-    src.x = (const XRec *)d_rec;
+    src.x = xr;
+    src.lx = lr;
     src.n = n_rec;
     ev_rec(c, 2);
     aggregate(c, src, li);
@@ -1344,73 +1371,186 @@ void job_import(mrg_ctx *c, const void *d_rec, uint64_t n_rec, const void *d_hea
     c->reduced = false;
 }
 
+void job_import(mrg_ctx *c, const void *d_rec, uint64_t n_rec, const void *d_heap, uint64_t heap_bytes,
+                const uint64_t *seg_recs, const uint64_t *seg_heap, uint32_t n_segs) {
+    import_recs(c, (const XRec *)d_rec, nullptr, n_rec, d_heap, heap_bytes, seg_recs, seg_heap, n_segs);
+}
+
+// A communicator shell with its preallocated exchange buffers (the RCCL communicator is added by
+// the caller).
+mrg_comm *comm_alloc(int device, int n, int rank) {
+    HIPCHK(hipSetDevice(device));
+    mrg_comm *m = new mrg_comm();
+    m->n = n;
+    m->rank = rank;
+    m->device = device;
+    if (hipMalloc(&m->d_counts, 48ull * (uint64_t)n) != hipSuccess || hipMalloc(&m->d_flag, 64) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(m->d_counts);
+        delete m;
+        raise(MRG_ENOMEM, "communicator buffers: device allocation failed");
+    }
+    return m;
+}
+
+void comm_free(mrg_comm *m) {
+    if (!m) return;
+    (void)hipSetDevice(m->device);
+    (void)hipFree(m->d_counts);
+    (void)hipFree(m->d_flag);
+    delete m;
+}
+
+// Test knob: MRG_TEST_FAIL="<stage>[:<rank>]" raises an injected failure at that stage (on that rank
+// only, or on every rank), so the failure paths of the multi-GPU plan can be exercised.
+void test_fail(const char *stage, int rank) {
+    const char *v = getenv("MRG_TEST_FAIL");
+    if (!v || !*v) return;
+    const char *colon = strchr(v, ':');
+    const size_t n = colon ? (size_t)(colon - v) : strlen(v);
+    if (n == strlen(stage) && !strncmp(v, stage, n) && (!colon || atoi(colon + 1) == rank))
+        raise(MRG_EINVAL, "injected failure at stage '%s' on rank %d (MRG_TEST_FAIL)", stage, rank);
+}
+
+// An RCCL call of the exchange: on failure the communicator is aborted (its peers' pending operations
+// then fail instead of waiting forever) and the call raises MRG_ECOMM.
+void nccl_or_abort(mrg_comm *m, ncclResult_t r, const char *what) {
+    if (r == ncclSuccess) return;
+    if (!m->aborted.exchange(true)) (void)ncclCommAbort(m->comm);
+    raise(MRG_ECOMM, "%s: %s (communicator aborted)", what, ncclGetErrorString(r));
+}
+
+void check_not_aborted(mrg_comm *m) {
+    if (m->aborted.load()) raise(MRG_ECOMM, "the communicator was aborted (another rank of the job failed)");
+}
+
+// Max of `flag` over the ranks (one RCCL all-reduce into the preallocated status word): every rank
+// learns whether any rank failed, so all of them leave the exchange together.
+int agree(mrg_ctx *c, mrg_comm *m, int flag) {
+    check_not_aborted(m);
+    HIPCHK(hipMemcpyAsync(m->d_flag, &flag, sizeof flag, hipMemcpyHostToDevice, c->stream));
+    nccl_or_abort(m, ncclAllReduce(m->d_flag, m->d_flag, 1, ncclInt, ncclMax, m->comm, c->stream), "ncclAllReduce");
+    int any = 0;
+    HIPCHK(hipMemcpyAsync(&any, m->d_flag, sizeof any, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    check_not_aborted(m);
+    return any;
+}
+
 // The shuffle: the reference's map -> reduce hand-off through mr-{m}-{r}.txt files
 // (worker.rs:117-140 -> 79-109) as one exchange over RCCL.  Owner of partition r = r % G.
+//
+// Failure protocol: every rank reaches every collective of the exchange.  A rank whose local step
+// fails (export, buffer allocation) still takes part, with a failure status: the per-destination
+// counts message carries it (the first collective), and one status all-reduce precedes the data
+// transfer; every rank then raises together (the failing rank its own error, the others MRG_ECOMM).
+// An RCCL error aborts the communicator.
 void job_shuffle(mrg_ctx *c, mrg_comm *m) {
-    need_job(c);
-    if (!m || !m->comm) raise(MRG_EINVAL, "null communicator");
+    if (!c || !m || !m->comm) raise(MRG_EINVAL, "null context or communicator");
     if (m->device != c->device) raise(MRG_EINVAL, "communicator is on device %d, context on %d", m->device, c->device);
-    if (!c->mapped) raise(MRG_EINVAL, "shuffle before map");
+    check_not_aborted(m);
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     const uint32_t G = (uint32_t)m->n;
     const uint32_t me = (uint32_t)m->rank;
-    export_sizes(c, G, nullptr, nullptr);
-    // per-destination (records, heap bytes) -> all-to-all -> per-source
-    std::vector<uint64_t> sc(2ull * G), rc(2ull * G);
-    for (uint32_t o = 0; o < G; ++o) {
-        sc[2 * o] = c->exp_rec[o];
-        sc[2 * o + 1] = c->exp_heap[o];
-    }
-    uint64_t *d_c = pget<uint64_t>(p, 4ull * G);
-    HIPCHK(hipMemcpyAsync(d_c, sc.data(), 16ull * G, hipMemcpyHostToDevice, s));
-    NCCLCHK(ncclAllToAll(d_c, d_c + 2 * G, 2, ncclUint64, m->comm, s));
-    HIPCHK(hipMemcpyAsync(rc.data(), d_c + 2 * G, 16ull * G, hipMemcpyDeviceToHost, s));
-    sync(c);
-    p.put(d_c);
-    std::vector<uint64_t> sro(G + 1, 0), sho(G + 1, 0), rro(G + 1, 0), rho(G + 1, 0), seg_rec(G), seg_heap(G);
-    for (uint32_t o = 0; o < G; ++o) {
-        sro[o + 1] = sro[o] + sc[2 * o];
-        sho[o + 1] = sho[o] + sc[2 * o + 1];
-        rro[o + 1] = rro[o] + rc[2 * o];
-        rho[o + 1] = rho[o] + rc[2 * o + 1];
-        seg_rec[o] = rc[2 * o];
-        seg_heap[o] = rc[2 * o + 1];
-    }
-    uint8_t *srec = pget<uint8_t>(p, sro[G] * MRG_XREC_BYTES + 16), *sheap = pget<uint8_t>(p, sho[G] + 16);
-    uint8_t *rrec = pget<uint8_t>(p, rro[G] * MRG_XREC_BYTES + 16), *rheap = pget<uint8_t>(p, rho[G] + 16);
-    export_pack(c, srec, sheap, false);
     const uint64_t X = MRG_XREC_BYTES;
+    uint8_t *srec = nullptr, *sheap = nullptr, *rrec = nullptr, *rheap = nullptr;
+    auto release = [&]() {
+        p.put(srec); p.put(sheap); p.put(rrec); p.put(rheap);
+        srec = sheap = rrec = rheap = nullptr;
+    };
+    MrgError mine{MRG_OK, ""};
+    // ---- local: export sizes and pack (the pack runs on the stream, no host wait)
+    std::vector<uint64_t> sc(3ull * G, 0), rc(3ull * G, 0);  // per peer: records, heap bytes, status
+    std::vector<uint64_t> sro(G + 1, 0), sho(G + 1, 0);
+    try {
+        need_job(c);
+        if (!c->mapped) raise(MRG_EINVAL, "shuffle before map");
+        test_fail("export", (int)me);
+        export_sizes(c, G, nullptr, nullptr);
+        for (uint32_t o = 0; o < G; ++o) {
+            sc[3 * o] = c->exp_rec[o];
+            sc[3 * o + 1] = c->exp_heap[o];
+            sro[o + 1] = sro[o] + sc[3 * o];
+            sho[o + 1] = sho[o] + sc[3 * o + 1];
+        }
+        srec = pget<uint8_t>(p, sro[G] * X + 16);
+        sheap = pget<uint8_t>(p, sho[G] + 16);
+        export_pack(c, srec, sheap, false);
+    } catch (const MrgError &e) {
+        mine = e;
+        std::fill(sc.begin(), sc.end(), 0);
+    }
+    for (uint32_t o = 0; o < G; ++o) sc[3 * o + 2] = mine.code ? 1u : 0u;
+    // ---- collective 1: the counts all-to-all (with every rank's status)
+    HIPCHK(hipMemcpyAsync(m->d_counts, sc.data(), 24ull * G, hipMemcpyHostToDevice, s));
+    nccl_or_abort(m, ncclAllToAll(m->d_counts, m->d_counts + 3 * G, 3, ncclUint64, m->comm, s), "ncclAllToAll");
+    HIPCHK(hipMemcpyAsync(rc.data(), m->d_counts + 3 * G, 24ull * G, hipMemcpyDeviceToHost, s));
+    sync(c);
+    check_not_aborted(m);
+    int failed_peer = -1;
+    for (uint32_t o = 0; o < G; ++o)
+        if (rc[3 * o + 2] && failed_peer < 0) failed_peer = (int)o;
+    if (mine.code || failed_peer >= 0) {
+        release();
+        if (mine.code) throw mine;
+        raise(MRG_ECOMM, "rank %d of the exchange failed before sending", failed_peer);
+    }
+    // ---- local: receive buffers
+    std::vector<uint64_t> rro(G + 1, 0), rho(G + 1, 0), seg_rec(G), seg_heap(G);
+    for (uint32_t o = 0; o < G; ++o) {
+        rro[o + 1] = rro[o] + rc[3 * o];
+        rho[o + 1] = rho[o] + rc[3 * o + 1];
+        seg_rec[o] = rc[3 * o];
+        seg_heap[o] = rc[3 * o + 1];
+    }
+    try {
+        test_fail("recv", (int)me);
+        rrec = pget<uint8_t>(p, rro[G] * X + 16);
+        rheap = pget<uint8_t>(p, rho[G] + 16);
+    } catch (const MrgError &e) {
+        mine = e;
+    }
+    // ---- collective 2: everyone ready to transfer?
+    if (agree(c, m, mine.code ? 1 : 0)) {
+        release();
+        if (mine.code) throw mine;
+        raise(MRG_ECOMM, "another rank of the exchange could not allocate its receive buffers");
+    }
+    // ---- collective 3: own slice by a device copy; peers by one send/recv group (each peer pair has
+    // its own xGMI link)
     hipEvent_t e0 = nullptr, e1 = nullptr;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipEventRecord(e0, s));
-    // own slice: a device copy; peers: one send/recv group (each peer pair has its own xGMI link)
-    if (sc[2 * me]) HIPCHK(hipMemcpyAsync(rrec + rro[me] * X, srec + sro[me] * X, sc[2 * me] * X, hipMemcpyDeviceToDevice, s));
-    if (sc[2 * me + 1]) HIPCHK(hipMemcpyAsync(rheap + rho[me], sheap + sho[me], sc[2 * me + 1], hipMemcpyDeviceToDevice, s));
+    if (sc[3 * me]) HIPCHK(hipMemcpyAsync(rrec + rro[me] * X, srec + sro[me] * X, sc[3 * me] * X, hipMemcpyDeviceToDevice, s));
+    if (sc[3 * me + 1]) HIPCHK(hipMemcpyAsync(rheap + rho[me], sheap + sho[me], sc[3 * me + 1], hipMemcpyDeviceToDevice, s));
     uint64_t sent = 0, recv = 0;
-    NCCLCHK(ncclGroupStart());
+    nccl_or_abort(m, ncclGroupStart(), "ncclGroupStart");
     for (uint32_t o = 0; o < G; ++o) {
         if (o == me) continue;
-        if (sc[2 * o]) NCCLCHK(ncclSend(srec + sro[o] * X, sc[2 * o] * X, ncclUint8, (int)o, m->comm, s));
-        if (sc[2 * o + 1]) NCCLCHK(ncclSend(sheap + sho[o], sc[2 * o + 1], ncclUint8, (int)o, m->comm, s));
-        if (rc[2 * o]) NCCLCHK(ncclRecv(rrec + rro[o] * X, rc[2 * o] * X, ncclUint8, (int)o, m->comm, s));
-        if (rc[2 * o + 1]) NCCLCHK(ncclRecv(rheap + rho[o], rc[2 * o + 1], ncclUint8, (int)o, m->comm, s));
-        sent += sc[2 * o] * X + sc[2 * o + 1];
-        recv += rc[2 * o] * X + rc[2 * o + 1];
+        if (sc[3 * o]) nccl_or_abort(m, ncclSend(srec + sro[o] * X, sc[3 * o] * X, ncclUint8, (int)o, m->comm, s), "ncclSend");
+        if (sc[3 * o + 1]) nccl_or_abort(m, ncclSend(sheap + sho[o], sc[3 * o + 1], ncclUint8, (int)o, m->comm, s), "ncclSend");
+        if (rc[3 * o]) nccl_or_abort(m, ncclRecv(rrec + rro[o] * X, rc[3 * o] * X, ncclUint8, (int)o, m->comm, s), "ncclRecv");
+        if (rc[3 * o + 1]) nccl_or_abort(m, ncclRecv(rheap + rho[o], rc[3 * o + 1], ncclUint8, (int)o, m->comm, s), "ncclRecv");
+        sent += sc[3 * o] * X + sc[3 * o + 1];
+        recv += rc[3 * o] * X + rc[3 * o + 1];
     }
-    NCCLCHK(ncclGroupEnd());
+    nccl_or_abort(m, ncclGroupEnd(), "ncclGroupEnd");
     HIPCHK(hipEventRecord(e1, s));
-    p.put(srec);  // stream-ordered reuse only (see export_pack)
+    HIPCHK(hipEventSynchronize(e1));
+    check_not_aborted(m);  // a watchdog abort ends a transfer early: its buffers are not to be used
+    p.put(srec);
     p.put(sheap);
+    srec = sheap = nullptr;
+    // ---- local: re-aggregate what arrived (no collective after this point)
     const mrg_stats keep = c->st;
     job_import(c, rrec, rro[G], rheap, rho[G], seg_rec.data(), seg_heap.data(), G);  // ends with a host wait
     float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, e0, e1));  // e1 is done: the import waited for the stream
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    p.put(rrec);
-    p.put(rheap);
+    release();
     // the import's aggregation time is the reduce side's; the map-side stats stay those of the map
     const double agg_import = c->st.ms_aggregate;
     c->st = keep;
@@ -1552,7 +1692,7 @@ void text_reduce(mrg_ctx *c, const uint8_t *const *files, const uint64_t *sizes,
               (unsigned long long)at);
     }
     const uint64_t N = fb[k];
-    XRec *x = pget<XRec>(p, std::max<uint64_t>(N, 1));
+    LRec *x = pget<LRec>(p, std::max<uint64_t>(N, 1));
     if (k) mrg_launch_text_lines(d, dfo, dfe, nf, nseg, base, cnt, x, err, err + 2, s);  // also counts empty keys
     HIPCHK(hipMemcpyAsync(&herr[2], err + 2, 8, hipMemcpyDeviceToHost, s));
     sync(c);
@@ -1561,7 +1701,7 @@ void text_reduce(mrg_ctx *c, const uint8_t *const *files, const uint64_t *sizes,
         seg_rec[i] = fb[i + 1] - fb[i];
         seg_heap[i] = fo[i + 1] - fo[i];  // heap segment of file i = its slot in the buffer
     }
-    job_import(c, x, N, d, k ? total : 0, seg_rec.data(), seg_heap.data(), nf);
+    import_recs(c, nullptr, x, N, d, k ? total : 0, seg_rec.data(), seg_heap.data(), nf);
     c->extra_first = herr[2];
     job_reduce(c);
     out.resize(c->out_bytes);
@@ -1578,7 +1718,7 @@ void text_reduce(mrg_ctx *c, const uint8_t *const *files, const uint64_t *sizes,
 extern "C" {
 
 const char *mrg_last_error(void) { return g_err.c_str(); }
-const char *mrg_version(void) { return "mrgpu 0.1 (gfx950)"; }
+const char *mrg_version(void) { return "mrgpu 0.3 (gfx950, abi 3)"; }
 
 int mrg_open(int device, mrg_ctx **out) {
     return guard([&] {
@@ -1891,15 +2031,14 @@ int mrg_comm_init(mrg_ctx *c, const uint8_t id[MRG_COMM_ID_BYTES], int n_ranks, 
         HIPCHK(hipSetDevice(c->device));
         ncclUniqueId u;
         memcpy(&u, id, sizeof u);
-        mrg_comm *m = new mrg_comm();
+        // the buffers first: a rank that fails here has not joined, and its peers' init fails or
+        // waits for it (the caller's concern: mrg_run_job creates its communicators in one call)
+        mrg_comm *m = comm_alloc(c->device, n_ranks, rank);
         const ncclResult_t r = ncclCommInitRank(&m->comm, n_ranks, u, rank);
         if (r != ncclSuccess) {
-            delete m;
+            comm_free(m);
             raise(MRG_ECOMM, "ncclCommInitRank(%d of %d): %s", rank, n_ranks, ncclGetErrorString(r));
         }
-        m->n = n_ranks;
-        m->rank = rank;
-        m->device = c->device;
         *out = m;
     });
 }
@@ -1907,15 +2046,14 @@ int mrg_comm_init(mrg_ctx *c, const uint8_t id[MRG_COMM_ID_BYTES], int n_ranks, 
 int mrg_comm_destroy(mrg_comm *m) {
     return guard([&] {
         if (!m) return;
-        if (m->comm) {
+        ncclResult_t r = ncclSuccess;
+        if (m->comm && !m->aborted.load()) {
             (void)hipSetDevice(m->device);
-            const ncclResult_t r = ncclCommDestroy(m->comm);
-            m->comm = nullptr;
-            delete m;
-            if (r != ncclSuccess) raise(MRG_ECOMM, "ncclCommDestroy: %s", ncclGetErrorString(r));
-            return;
+            r = ncclCommDestroy(m->comm);
         }
-        delete m;
+        m->comm = nullptr;
+        comm_free(m);
+        if (r != ncclSuccess) raise(MRG_ECOMM, "ncclCommDestroy: %s", ncclGetErrorString(r));
     });
 }
 
@@ -1927,17 +2065,12 @@ int mrg_job_shuffle(mrg_ctx *c, mrg_comm *m) {
 
 namespace {
 
-void read_file(const char *path, std::vector<uint8_t> &data) {
-    FILE *f = fopen(path, "rb");  // worker.rs:73 File::open(..).unwrap()
-    if (!f) raise(MRG_EIO, "cannot open %s", path);
-    fseek(f, 0, SEEK_END);
-    const long sz = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    data.resize(sz > 0 ? (size_t)sz : 0);
-    const size_t got = sz > 0 ? fread(data.data(), 1, (size_t)sz, f) : 0;
-    fclose(f);
-    if (sz < 0 || got != (size_t)sz) raise(MRG_EIO, "short read on %s", path);
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
 }
+
+thread_local mrg_run_stats g_run{};
 
 void write_file(const std::string &path, const uint8_t *p, uint64_t n) {
     FILE *f = fopen(path.c_str(), "wb");  // worker.rs:167-168 File::create("mr-{r}.txt")
@@ -1947,107 +2080,332 @@ void write_file(const std::string &path, const uint8_t *p, uint64_t n) {
     if (w != n || cl != 0) raise(MRG_EIO, "short write on %s", path.c_str());
 }
 
-// k-way merge of G byte-sorted line runs (each GPU's final.txt lines): LC_ALL=C `sort` order
-std::vector<uint8_t> merge_sorted_lines(const std::vector<std::vector<uint8_t>> &runs) {
-    struct Cur { const uint8_t *p, *e; };
+// k-way merge of G byte-sorted line runs (each GPU's final.txt lines): LC_ALL=C `sort` order.  A run
+// may lack its final newline (its last line then ends at the run's end); each cursor's line end is
+// found once per line.
+std::vector<uint8_t> merge_sorted_lines(const std::vector<std::pair<const uint8_t *, uint64_t>> &runs) {
+    struct Cur { const uint8_t *p, *e, *le; };  // le = end of the current line (its '\n' or e)
     std::vector<Cur> cur;
     uint64_t total = 0;
+    auto line_end = [](const uint8_t *p, const uint8_t *e) {
+        const uint8_t *q = (const uint8_t *)memchr(p, '\n', (size_t)(e - p));
+        return q ? q : e;
+    };
     for (auto &r : runs) {
-        cur.push_back({r.data(), r.data() + r.size()});
-        total += r.size();
+        if (!r.second) continue;
+        cur.push_back({r.first, r.first + r.second, line_end(r.first, r.first + r.second)});
+        total += r.second;
     }
-    auto line_end = [](const Cur &c) { return (const uint8_t *)memchr(c.p, '\n', (size_t)(c.e - c.p)); };
     std::vector<uint8_t> out;
-    out.reserve(total);
-    for (;;) {
-        int best = -1;
-        const uint8_t *be = nullptr;
-        for (int i = 0; i < (int)cur.size(); ++i) {
-            if (cur[i].p >= cur[i].e) continue;
-            const uint8_t *e = line_end(cur[i]);
-            if (!e) e = cur[i].e;
-            if (best < 0) { best = i; be = e; continue; }
-            const size_t la = (size_t)(e - cur[i].p), lb = (size_t)(be - cur[best].p);
+    out.reserve(total + runs.size());
+    while (!cur.empty()) {
+        size_t best = 0;
+        for (size_t i = 1; i < cur.size(); ++i) {
+            const size_t la = (size_t)(cur[i].le - cur[i].p), lb = (size_t)(cur[best].le - cur[best].p);
             const int cm = memcmp(cur[i].p, cur[best].p, std::min(la, lb));
-            if (cm < 0 || (cm == 0 && la < lb)) { best = i; be = e; }
+            if (cm < 0 || (cm == 0 && la < lb)) best = i;
         }
-        if (best < 0) break;
-        const uint8_t *stop = be < cur[best].e ? be + 1 : be;
-        out.insert(out.end(), cur[best].p, stop);
-        cur[best].p = stop;
+        Cur &c = cur[best];
+        out.insert(out.end(), c.p, c.le);
+        out.push_back('\n');  // every output line ends with a newline, also a run's unterminated last one
+        c.p = c.le < c.e ? c.le + 1 : c.e;
+        if (c.p >= c.e) cur.erase(cur.begin() + (ptrdiff_t)best);
+        else c.le = line_end(c.p, c.e);
     }
     return out;
 }
 
-// One GPU of mrg_run_job: rank g of G (GPU g), one host thread.
-void run_rank(int g, int G, const ncclUniqueId *uid, const char *const *files, size_t n_files, uint32_t R, int app,
-              const char *out_dir, uint32_t flags, std::vector<uint8_t> &final_out) {
-    mrg_ctx *c = nullptr;
-    if (mrg_open(g, &c) != MRG_OK) raise(MRG_EHIP, "GPU %d: %s", g, mrg_last_error());
-    struct Closer { mrg_ctx *c; mrg_comm *m; ~Closer() { mrg_comm_destroy(m); mrg_close(c); } } closer{c, nullptr};
-    if (G > 1 || uid) {
-        if (mrg_comm_init(c, (const uint8_t *)uid, G, g, &closer.m) != MRG_OK) raise(MRG_ECOMM, "%s", mrg_last_error());
+// ---- input files -> device: worker.rs:65-77 reads each file whole (read_to_string).  Here the
+// files of a GPU are read in chunks by several host threads into pinned staging buffers (two per
+// thread), each chunk copied to the device buffer while the thread reads the next one, so disk /
+// page-cache reads and the PCIe copies overlap.
+struct FileChunk {
+    uint32_t file;   // index in the rank's file list
+    uint64_t off, n; // bytes [off, off + n) of the file
+    uint64_t dst;    // offset in the device buffer
+};
+
+constexpr uint64_t MRG_READ_CHUNK = 32ull << 20;
+
+void read_files_to_device(int device, const std::vector<const char *> &paths, const std::vector<uint64_t> &doc_off,
+                          uint8_t *d, int n_threads) {
+    std::vector<FileChunk> chunks;
+    for (uint32_t i = 0; i < paths.size(); ++i) {
+        const uint64_t sz = doc_off[i + 1] - doc_off[i];
+        for (uint64_t o = 0; o < sz; o += MRG_READ_CHUNK)
+            chunks.push_back({i, o, std::min<uint64_t>(MRG_READ_CHUNK, sz - o), doc_off[i] + o});
     }
-    // map shard: files m with m % G == g (static plan for coordinator.rs:137-176)
-    int status = MRG_OK;
-    std::string err;
+    if (chunks.empty()) return;
+    n_threads = std::max(1, std::min<int>(n_threads, (int)chunks.size()));
+    uint64_t pin_bytes = 0;  // staging buffers sized to the largest chunk (small inputs: small buffers)
+    for (auto &ch : chunks) pin_bytes = std::max(pin_bytes, ch.n);
+    std::atomic<size_t> next{0};
+    std::atomic<int> fail{0};
+    std::vector<int> rc(n_threads, MRG_OK);
+    std::vector<std::string> msg(n_threads);
+    auto reader = [&](int t) {
+        rc[t] = guard([&] {
+            HIPCHK(hipSetDevice(device));
+            hipStream_t st = nullptr;
+            uint8_t *pin[2] = {nullptr, nullptr};
+            hipEvent_t ev[2] = {nullptr, nullptr};
+            std::vector<int> fds(paths.size(), -1);
+            struct Res {  // released on every exit path
+                hipStream_t &st; uint8_t **pin; hipEvent_t *ev; std::vector<int> &fds;
+                ~Res() {
+                    if (st) (void)hipStreamSynchronize(st);
+                    for (int k = 0; k < 2; ++k) { if (ev[k]) (void)hipEventDestroy(ev[k]); if (pin[k]) (void)hipHostFree(pin[k]); }
+                    if (st) (void)hipStreamDestroy(st);
+                    for (int fd : fds) if (fd >= 0) close(fd);
+                }
+            } res{st, pin, ev, fds};
+            HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            for (int k = 0; k < 2; ++k) {
+                HIPCHK(hipHostMalloc(&pin[k], pin_bytes, hipHostMallocDefault));
+                HIPCHK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+            }
+            bool used[2] = {false, false};
+            for (int k = 0;; k ^= 1) {
+                if (fail.load()) return;
+                const size_t ci = next.fetch_add(1);
+                if (ci >= chunks.size()) break;
+                const FileChunk &ch = chunks[ci];
+                if (used[k]) HIPCHK(hipEventSynchronize(ev[k]));  // the copy out of this buffer is done
+                int &fd = fds[ch.file];
+                if (fd < 0) {
+                    fd = open(paths[ch.file], O_RDONLY);  // worker.rs:73 File::open(..).unwrap()
+                    if (fd < 0) raise(MRG_EIO, "cannot open %s", paths[ch.file]);
+                }
+                uint64_t got = 0;
+                while (got < ch.n) {
+                    const ssize_t r = pread(fd, pin[k] + got, (size_t)(ch.n - got), (off_t)(ch.off + got));
+                    if (r <= 0) raise(MRG_EIO, "short read on %s", paths[ch.file]);
+                    got += (uint64_t)r;
+                }
+                HIPCHK(hipMemcpyAsync(d + ch.dst, pin[k], ch.n, hipMemcpyHostToDevice, st));
+                HIPCHK(hipEventRecord(ev[k], st));
+                used[k] = true;
+            }
+            HIPCHK(hipStreamSynchronize(st));
+        });
+        if (rc[t]) {
+            msg[t] = g_err;
+            fail.store(1);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < n_threads; ++t) th.emplace_back(reader, t);
+    reader(0);
+    for (auto &x : th) x.join();
+    for (int t = 0; t < n_threads; ++t)
+        if (rc[t]) raise(rc[t], "%s", msg[t].c_str());
+}
+
+// One GPU of mrg_run_job.
+struct RankState {
+    int g = 0, device = 0;
+    mrg_ctx *c = nullptr;
+    mrg_comm *m = nullptr;
     uint8_t *d = nullptr;
-    try {
+    uint64_t in_bytes = 0;
+    std::vector<uint8_t> out, fin;
+};
+
+// Runs fn on every rank, one host thread each, and returns when all have returned; the per-rank
+// status codes and messages are left in rc / msg.  In a phase with collectives (`watch`), a rank
+// that failed outside the exchange's own status protocol (an RCCL error) can leave its peers
+// waiting for it: once a rank has failed and the others have not finished within the grace period
+// (MRG_ABORT_GRACE_MS, default 10 s), every communicator is aborted, so the waiting RCCL operations
+// fail and their threads return.
+template <class F>
+void run_ranks(std::vector<RankState> &rs, bool watch, F &&fn, std::vector<int> &rc, std::vector<std::string> &msg) {
+    const int G = (int)rs.size();
+    rc.assign(G, MRG_OK);
+    msg.assign(G, std::string());
+    std::mutex mu;
+    std::condition_variable cv;
+    int done = 0, failed = 0;
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; ++g)
+        th.emplace_back([&, g] {
+            const int r = guard([&] {
+                HIPCHK(hipSetDevice(rs[g].device));
+                fn(rs[g]);
+            });
+            std::lock_guard<std::mutex> lk(mu);
+            rc[g] = r;
+            if (r) {
+                msg[g] = g_err;
+                ++failed;
+            }
+            ++done;
+            cv.notify_all();
+        });
+    const uint64_t grace_ms = env_u64("MRG_ABORT_GRACE_MS", 10000);
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        Clock::time_point first_fail{};
+        bool aborted = false;
+        while (done < G) {
+            cv.wait_for(lk, std::chrono::milliseconds(50));
+            if (!watch || aborted || !failed || done >= G) continue;
+            if (first_fail == Clock::time_point{}) first_fail = Clock::now();
+            if (ms_since(first_fail) < (double)grace_ms) continue;
+            aborted = true;
+            for (auto &r : rs)
+                if (r.m && r.m->comm && !r.m->aborted.exchange(true)) (void)ncclCommAbort(r.m->comm);
+        }
+    }
+    for (auto &t : th) t.join();
+}
+
+// The first failure that is not an echo (MRG_ECOMM) of another rank's, else the first failure.
+void raise_first(const std::vector<int> &rc, const std::vector<std::string> &msg, const std::vector<RankState> &rs) {
+    for (size_t g = 0; g < rc.size(); ++g)
+        if (rc[g] && rc[g] != MRG_ECOMM) raise(rc[g], "GPU %d: %s", rs[g].device, msg[g].c_str());
+    for (size_t g = 0; g < rc.size(); ++g)
+        if (rc[g]) raise(rc[g], "GPU %d: %s", rs[g].device, msg[g].c_str());
+}
+
+void release_ranks(std::vector<RankState> &rs) {
+    for (auto &r : rs) {
+        if (r.d && r.c) {
+            (void)hipSetDevice(r.device);
+            r.c->pool.put(r.d);
+        }
+        if (r.m) (void)mrg_comm_destroy(r.m);
+        if (r.c) (void)mrg_close(r.c);
+        r = RankState{};
+    }
+}
+
+// The whole job on GPUs devices[0..G): the static plan for the coordinator's task assignment
+// (coordinator.rs:137-215) and the workers' map-then-reduce loop (mrworker.rs:43-149).  Phases, each
+// on all GPUs at once and joined before the next: open contexts -> create the communicators (one
+// ncclCommInitAll) -> read + map -> exchange -> reduce + write.  A failure in any phase fails the job
+// there: before the communicators exist nothing collective has started, and the exchange agrees on
+// every rank's status before each of its transfers, so no GPU thread is left waiting for another.
+void run_job(const char *const *files, size_t n_files, uint32_t R, int app, const char *out_dir, uint32_t flags,
+             const std::vector<int> &devices) {
+    const Clock::time_point t_all = Clock::now();
+    g_run = mrg_run_stats{};
+    const int G = (int)devices.size();
+    g_run.n_gpus = G;
+    std::vector<const char *> names(files, files + n_files);
+    check_names(names.data(), (uint32_t)n_files);
+    std::vector<RankState> rs(G);
+    struct Guard { std::vector<RankState> &rs; ~Guard() { release_ranks(rs); } } release{rs};
+    std::vector<int> rc;
+    std::vector<std::string> msg;
+    // ---- contexts (worker processes)
+    Clock::time_point t0 = Clock::now();
+    for (int g = 0; g < G; ++g) {
+        rs[g].g = g;
+        rs[g].device = devices[g];
+        test_fail("open", g);
+        if (mrg_open(devices[g], &rs[g].c) != MRG_OK) raise(MRG_EHIP, "GPU %d: %s", devices[g], mrg_last_error());
+    }
+    // ---- communicators: all of them in one call (nothing to wait for if one cannot be made)
+    const bool comm = G > 1 || env_u64("MRG_TEST_FORCE_COMM", 0);
+    if (comm) {
+        test_fail("comm", 0);
+        std::vector<ncclComm_t> cs(G, nullptr);
+        const ncclResult_t r = ncclCommInitAll(cs.data(), G, devices.data());
+        if (r != ncclSuccess) raise(MRG_ECOMM, "ncclCommInitAll over %d GPUs: %s", G, ncclGetErrorString(r));
+        for (int g = 0; g < G; ++g) {
+            try {
+                rs[g].m = comm_alloc(devices[g], G, g);
+            } catch (...) {
+                for (int k = g; k < G; ++k) { (void)hipSetDevice(devices[k]); (void)ncclCommDestroy(cs[k]); }
+                throw;
+            }
+            rs[g].m->comm = cs[g];
+        }
+    }
+    g_run.ms_open = ms_since(t0);
+    // ---- map phase: GPU g reads and maps files m with m % G == g (coordinator.rs:137-176)
+    const int readers = (int)std::max<uint64_t>(1, env_u64("MRG_READ_THREADS", std::max(1, std::min(8, 16 / G))));
+    std::vector<double> t_read(G, 0.0);
+    t0 = Clock::now();
+    run_ranks(rs, false, [&](RankState &r) {
+        mrg_ctx *c = r.c;
+        test_fail("map", r.g);
+        const Clock::time_point tr = Clock::now();
         job_begin(c, app, R, flags);
-        std::vector<const char *> nm(files, files + n_files);
-        check_names(nm.data(), (uint32_t)n_files);
         c->names.assign(files, files + n_files);
+        std::vector<const char *> mine;
         std::vector<uint64_t> off(1, 0);
         std::vector<uint32_t> ids;
-        std::vector<std::vector<uint8_t>> data;
-        for (size_t m = (size_t)g; m < n_files; m += (size_t)G) {
-            data.emplace_back();
-            read_file(files[m], data.back());
-            off.push_back(off.back() + data.back().size());
+        for (size_t m = (size_t)r.g; m < n_files; m += (size_t)G) {
+            struct stat sb;
+            if (stat(files[m], &sb) != 0) raise(MRG_EIO, "cannot open %s", files[m]);  // worker.rs:73
+            mine.push_back(files[m]);
+            off.push_back(off.back() + (uint64_t)sb.st_size);
             ids.push_back((uint32_t)m);
         }
-        d = pget<uint8_t>(c->pool, off.back() + 64);
-        for (size_t i = 0; i < data.size(); ++i)
-            if (!data[i].empty())
-                HIPCHK(hipMemcpyAsync(d + off[i], data[i].data(), data[i].size(), hipMemcpyHostToDevice, c->stream));
-        sync(c);
-        data.clear();
-        c->d_in = d;
+        r.in_bytes = off.back();
+        r.d = pget<uint8_t>(c->pool, off.back() + 64);
+        read_files_to_device(c->device, mine, off, r.d, readers);
+        t_read[r.g] = ms_since(tr);
+        c->d_in = r.d;
         c->doc_off = off;
         c->doc_ids = ids;
         job_map(c);
-    } catch (const MrgError &e) {
-        status = e.code;
-        err = e.msg;
+    }, rc, msg);
+    raise_first(rc, msg, rs);
+    g_run.ms_map = ms_since(t0);
+    for (int g = 0; g < G; ++g) {
+        g_run.ms_read = std::max(g_run.ms_read, t_read[g]);
+        g_run.input_bytes += rs[g].in_bytes;
     }
-    if (closer.m) {  // every rank learns whether any map failed before entering the exchange
-        int *flag = pget<int>(c->pool, 1);
-        int h = status ? 1 : 0;
-        HIPCHK(hipMemcpyAsync(flag, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
-        NCCLCHK(ncclAllReduce(flag, flag, 1, ncclInt, ncclMax, closer.m->comm, c->stream));
-        HIPCHK(hipMemcpyAsync(&h, flag, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    g_run.ms_map -= g_run.ms_read;
+    // ---- exchange (RCCL over xGMI)
+    if (comm) {
+        t0 = Clock::now();
+        run_ranks(rs, true, [&](RankState &r) { job_shuffle(r.c, r.m); }, rc, msg);
+        raise_first(rc, msg, rs);
+        g_run.ms_shuffle = ms_since(t0);
+    }
+    // ---- reduce phase: GPU g formats the partitions r % G == g (coordinator.rs:178-215)
+    t0 = Clock::now();
+    run_ranks(rs, false, [&](RankState &r) {
+        mrg_ctx *c = r.c;
+        test_fail("reduce", r.g);
+        job_reduce(c);
+        r.out.resize(c->out_bytes);
+        if (c->out_bytes) HIPCHK(hipMemcpyAsync(r.out.data(), c->d_out, c->out_bytes, hipMemcpyDeviceToHost, c->stream));
+        if (flags & MRG_FLAG_FINAL_TXT) {  // run.sh:16-20 generate_output: this GPU's lines, sorted on the device
+            job_final(c);
+            r.fin.resize(c->final_bytes);
+            if (c->final_bytes)
+                HIPCHK(hipMemcpyAsync(r.fin.data(), c->d_final, c->final_bytes, hipMemcpyDeviceToHost, c->stream));
+        }
         sync(c);
-        c->pool.put(flag);
-        if (h && !status) raise(MRG_ECOMM, "another GPU of the job failed");
+    }, rc, msg);
+    raise_first(rc, msg, rs);
+    g_run.ms_reduce = ms_since(t0);
+    // ---- writes: mr-{r}.txt by the GPU that owns r (worker.rs:167-179), then final.txt
+    t0 = Clock::now();
+    run_ranks(rs, false, [&](RankState &r) {
+        test_fail("write", r.g);
+        for (uint32_t p = (uint32_t)r.g; p < R; p += (uint32_t)G) {
+            const uint64_t a = r.c->part_off[p], b = r.c->part_off[p + 1];
+            write_file(std::string(out_dir) + "/mr-" + std::to_string(p) + ".txt", r.out.data() + a, b - a);
+        }
+    }, rc, msg);
+    raise_first(rc, msg, rs);
+    for (auto &r : rs) g_run.output_bytes += r.out.size();
+    if (flags & MRG_FLAG_FINAL_TXT) {
+        std::vector<std::pair<const uint8_t *, uint64_t>> runs;
+        for (auto &r : rs) runs.push_back({r.fin.data(), r.fin.size()});
+        if (G == 1) write_file(std::string(out_dir) + "/final.txt", rs[0].fin.data(), rs[0].fin.size());
+        else {
+            const std::vector<uint8_t> all = merge_sorted_lines(runs);
+            write_file(std::string(out_dir) + "/final.txt", all.data(), all.size());
+        }
     }
-    if (status) throw MrgError{status, err};
-    if (closer.m) job_shuffle(c, closer.m);
-    job_reduce(c);
-    std::vector<uint8_t> out(c->out_bytes);
-    if (c->out_bytes) HIPCHK(hipMemcpyAsync(out.data(), c->d_out, c->out_bytes, hipMemcpyDeviceToHost, c->stream));
-    sync(c);
-    for (uint32_t r = (uint32_t)g; r < R; r += (uint32_t)G) {  // reduce tasks of this GPU (coordinator.rs:178-215)
-        const uint64_t a = c->part_off[r], b = c->part_off[r + 1];
-        write_file(std::string(out_dir) + "/mr-" + std::to_string(r) + ".txt", out.data() + a, b - a);
-    }
-    if (flags & MRG_FLAG_FINAL_TXT) {  // run.sh:16-20 generate_output: this GPU's lines, sorted on the device
-        job_final(c);
-        final_out.resize(c->final_bytes);
-        if (c->final_bytes)
-            HIPCHK(hipMemcpyAsync(final_out.data(), c->d_final, c->final_bytes, hipMemcpyDeviceToHost, c->stream));
-        sync(c);
-    }
-    c->pool.put(d);
+    g_run.ms_write = ms_since(t0);
+    g_run.ms_total = ms_since(t_all);
 }
 
 }  // namespace
@@ -2062,31 +2420,33 @@ int mrg_run_job(const char *const *files, size_t n_files, uint32_t n_reduce, int
         int ndev = 0;
         HIPCHK(hipGetDeviceCount(&ndev));
         if (n_gpus < 1 || n_gpus > ndev) raise(MRG_EINVAL, "n_gpus %d: %d devices visible", n_gpus, ndev);
-        const int G = n_gpus;
-        std::vector<std::vector<uint8_t>> fin(G);
-        if (G == 1 && !env_u64("MRG_TEST_FORCE_COMM", 0)) {  // one GPU: no communicator needed
-            run_rank(0, 1, nullptr, files, n_files, n_reduce, app, out_dir, flags, fin[0]);
-        } else {
-            ncclUniqueId uid;
-            NCCLCHK(ncclGetUniqueId(&uid));
-            std::vector<int> rc(G, MRG_OK);
-            std::vector<std::string> msg(G);
-            std::vector<std::thread> th;
-            for (int g = 0; g < G; ++g)
-                th.emplace_back([&, g] {
-                    rc[g] = guard([&] { run_rank(g, G, &uid, files, n_files, n_reduce, app, out_dir, flags, fin[g]); });
-                    if (rc[g]) msg[g] = g_err;
-                });
-            for (auto &t : th) t.join();
-            for (int g = 0; g < G; ++g)  // the first rank's own failure, not the others' ECOMM echo of it
-                if (rc[g] && rc[g] != MRG_ECOMM) raise(rc[g], "GPU %d: %s", g, msg[g].c_str());
-            for (int g = 0; g < G; ++g)
-                if (rc[g]) raise(rc[g], "GPU %d: %s", g, msg[g].c_str());
-        }
-        if (flags & MRG_FLAG_FINAL_TXT) {
-            const std::vector<uint8_t> all = G == 1 ? fin[0] : merge_sorted_lines(fin);
-            write_file(std::string(out_dir) + "/final.txt", all.data(), all.size());
-        }
+        std::vector<int> devs(n_gpus);
+        for (int g = 0; g < n_gpus; ++g) devs[g] = g;
+        run_job(files, n_files, n_reduce, app, out_dir, flags, devs);
+    });
+}
+
+int mrg_run_get_stats(mrg_run_stats *out) {
+    return guard([&] {
+        if (!out) raise(MRG_EINVAL, "null argument");
+        *out = g_run;
+    });
+}
+
+// Test entry (not in include/mrgpu.h): the k-way merge of sorted line runs that builds a multi-GPU
+// final.txt, callable without a GPU.  *out (free with mrg_free) receives the merged bytes.
+int mrg_test_merge_sorted_lines(const uint8_t *const *runs, const uint64_t *sizes, size_t k, uint8_t **out,
+                                uint64_t *out_len) {
+    return guard([&] {
+        if (!out || !out_len || (k && (!runs || !sizes))) raise(MRG_EINVAL, "null argument");
+        std::vector<std::pair<const uint8_t *, uint64_t>> v;
+        for (size_t i = 0; i < k; ++i) v.push_back({runs[i], sizes[i]});
+        const std::vector<uint8_t> m = merge_sorted_lines(v);
+        uint8_t *o = (uint8_t *)malloc(m.size() + 1);
+        if (!o) raise(MRG_ENOMEM, "host allocation failed");
+        if (!m.empty()) memcpy(o, m.data(), m.size());
+        *out = o;
+        *out_len = m.size();
     });
 }
 

@@ -13,7 +13,8 @@ APP_WC = 0
 APP_INDEXER = 1
 FLAG_NO_COMPAT_DROP_LAST = 0x1
 FLAG_FINAL_TXT = 0x2
-XREC_BYTES = 40
+XREC_BYTES = 24  # include/mrgpu.h MRG_XREC_BYTES (ABI 3)
+ABI_VERSION = 3
 
 OK, EINVAL, EUTF8, EHIP, ENOMEM, EIO, ECOMM = 0, -1, -2, -3, -4, -5, -6
 _CODES = {EINVAL: "EINVAL", EUTF8: "EUTF8", EHIP: "EHIP", ENOMEM: "ENOMEM", EIO: "EIO", ECOMM: "ECOMM"}
@@ -60,6 +61,16 @@ class Stats(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+class RunStats(C.Structure):
+    """mrg_run_stats: wall-clock phases of the last mrg_run_job on this thread."""
+    _fields_ = [("ms_total", C.c_double), ("ms_open", C.c_double), ("ms_read", C.c_double), ("ms_map", C.c_double),
+                ("ms_shuffle", C.c_double), ("ms_reduce", C.c_double), ("ms_write", C.c_double),
+                ("input_bytes", C.c_uint64), ("output_bytes", C.c_uint64), ("n_gpus", C.c_int)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
 _lib = None
 _vp = C.c_void_p
 _u8p = C.POINTER(C.c_uint8)
@@ -97,6 +108,7 @@ _SIGS = {
                                   C.POINTER(C.c_size_t)]),
     "mrg_run_job": (C.c_int, [C.POINTER(C.c_char_p), C.c_size_t, C.c_uint32, C.c_int, C.c_char_p, C.c_uint32,
                               C.c_int]),
+    "mrg_run_get_stats": (C.c_int, [C.POINTER(RunStats)]),
     "mrg_comm_get_id": (C.c_int, [_vp]),
     "mrg_comm_init": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.POINTER(_vp)]),
     "mrg_comm_destroy": (C.c_int, [_vp]),
@@ -325,8 +337,26 @@ class Context:
 
 
 def run_job(files, n_reduce, app=APP_WC, out_dir=".", flags=0, n_gpus=1):
+    """mrg_run_job: the whole job over files on disk; returns its phase timings (mrg_run_get_stats)."""
     arr = (C.c_char_p * max(len(files), 1))(*[f.encode() for f in files])
     _check(load().mrg_run_job(arr, len(files), n_reduce, app, out_dir.encode(), flags, n_gpus))
+    st = RunStats()
+    _check(load().mrg_run_get_stats(C.byref(st)))
+    return st.as_dict()
+
+
+def merge_sorted_lines(runs):
+    """The host k-way merge of per-GPU sorted final.txt runs (test entry, no GPU needed)."""
+    L = load()
+    f = L.mrg_test_merge_sorted_lines
+    f.restype = C.c_int
+    f.argtypes = [C.POINTER(C.c_char_p), _u64p, C.c_size_t, C.POINTER(_vp), _u64p]
+    arr = (C.c_char_p * max(len(runs), 1))(*runs)
+    out, n = _vp(), C.c_uint64()
+    _check(f(arr, _u64arr([len(r) for r in runs]), len(runs), C.byref(out), C.byref(n)))
+    data = C.string_at(out, n.value) if n.value else b""
+    L.mrg_free(out)
+    return data
 
 
 def comm_id():

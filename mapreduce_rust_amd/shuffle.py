@@ -5,7 +5,7 @@ The reference coordinator hands out map tasks (input files) and reduce tasks (pa
 (src/mr/worker.rs:117-140, 79-109).  Here the plan is static: rank g maps its shard of the input
 files, and owns every partition r with r % G == g.  After the map each rank packs its per-key
 records by owner (mrg_job_export), one all-to-all of the per-owner counts tells every rank how much
-it receives, and the 40-byte exchange records and the long-key heap bytes follow.  The receiving
+it receives, and the 24-byte exchange records and the long-key heap bytes follow.  The receiving
 rank re-aggregates (mrg_job_import: the same key can arrive from every rank) and reduces its
 partitions.  There is exactly one data-path collective, the exchange itself.
 
@@ -20,7 +20,7 @@ import torch.distributed as dist
 
 from . import native
 
-XREC = 40
+XREC = native.XREC_BYTES
 
 # Per-exchange record of the data all-to-alls (device runs only): start/end events on the current
 # stream around the two data collectives, and the bytes this rank sent to / received from peers
@@ -38,27 +38,44 @@ def shard_files(n_files, rank, world):
     return list(range(rank, n_files, world))
 
 
-def alltoall_exchange(send_rec, send_heap, rec_counts, heap_counts, group=None):
-    """Exchange per-owner slices.  send_rec: uint8 tensor of sum(rec_counts) * 40 bytes ordered by
-    owner; send_heap: uint8 tensor of sum(heap_counts) bytes ordered by owner.
+def alltoall_exchange(send_rec, send_heap, rec_counts, heap_counts, group=None, status=0):
+    """Exchange per-owner slices.  send_rec: uint8 tensor of sum(rec_counts) * XREC bytes ordered by
+    owner; send_heap: uint8 tensor of sum(heap_counts) bytes ordered by owner.  `status` != 0 says this
+    rank failed before the exchange: the counts all-to-all carries every rank's status, and every
+    rank raises if any failed (no rank is left waiting in the data all-to-alls).
     Returns (recv_rec, recv_heap, recv_rec_counts, recv_heap_counts), ordered by sender."""
     world = dist.get_world_size(group)
     dev = send_rec.device
     if dev.type == "cuda" and dist.get_backend(group) == "gloo":
         # gloo moves host tensors only: stage through host memory (rehearsal of N > 1 on one GPU;
         # the product path is RCCL, which exchanges device buffers directly)
-        rr, rh, r_rec, r_heap = alltoall_exchange(send_rec.cpu(), send_heap.cpu(), rec_counts, heap_counts, group)
+        rr, rh, r_rec, r_heap = alltoall_exchange(send_rec.cpu(), send_heap.cpu(), rec_counts, heap_counts, group,
+                                                  status)
         return rr.to(dev), rh.to(dev), r_rec, r_heap
-    counts = torch.tensor(list(rec_counts) + list(heap_counts), dtype=torch.int64, device=dev)
-    # [rec_0..rec_{G-1}, heap_0..heap_{G-1}] -> per destination (rec_o, heap_o) pairs
-    send_c = counts.view(2, world).t().contiguous().view(-1)
+    counts = torch.tensor(list(rec_counts) + list(heap_counts) + [1 if status else 0] * world, dtype=torch.int64,
+                          device=dev)
+    # [rec_0..rec_{G-1}, heap_0..heap_{G-1}, status x G] -> per destination (rec_o, heap_o, status) triples
+    send_c = counts.view(3, world).t().contiguous().view(-1)
     recv_c = torch.empty_like(send_c)
-    dist.all_to_all_single(recv_c, send_c, [2] * world, [2] * world, group=group)
-    rc = recv_c.view(world, 2).cpu().tolist()
-    r_rec = [int(a) for a, _ in rc]
-    r_heap = [int(b) for _, b in rc]
-    recv_rec = torch.empty(max(sum(r_rec), 1) * XREC, dtype=torch.uint8, device=dev)
-    recv_heap = torch.empty(max(sum(r_heap), 1), dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(recv_c, send_c, [3] * world, [3] * world, group=group)
+    rc = recv_c.view(world, 3).cpu().tolist()
+    failed = [o for o, (_, _, st) in enumerate(rc) if st]
+    if failed:
+        raise native.MrgError(native.ECOMM, "rank %d of the exchange failed before sending" % failed[0])
+    r_rec = [int(a) for a, _, _ in rc]
+    r_heap = [int(b) for _, b, _ in rc]
+    err = None
+    try:  # receive buffers; then every rank agrees that all of them have theirs
+        recv_rec = torch.empty(max(sum(r_rec), 1) * XREC, dtype=torch.uint8, device=dev)
+        recv_heap = torch.empty(max(sum(r_heap), 1), dtype=torch.uint8, device=dev)
+    except RuntimeError as e:
+        err = e
+    flag = torch.tensor([1 if err else 0], dtype=torch.int64, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    if err is not None:
+        raise err
+    if flag.item():
+        raise native.MrgError(native.ECOMM, "another rank of the exchange could not allocate its receive buffers")
     timed = dev.type == "cuda"
     if timed:
         me = dist.get_rank(group)
@@ -93,16 +110,30 @@ def shuffle(ctx, world, device, group=None):
     torch.distributed.  The context's kernels run on its own stream, torch's buffers and collectives
     on torch's current stream: the current stream is drained before the export writes into torch
     buffers and before the import reads what the collectives wrote (the export itself returns only
-    after its kernels are done)."""
+    after its kernels are done).  A rank whose export fails still takes part in the counts exchange
+    (with a failure status), so every rank raises instead of waiting for it."""
     dev = torch.device(device)
     cuda = dev.type == "cuda"
-    rec, heap = ctx.export_sizes(world)
-    send_rec = torch.empty(max(sum(rec), 1) * XREC, dtype=torch.uint8, device=dev)
-    send_heap = torch.empty(max(sum(heap), 1), dtype=torch.uint8, device=dev)
-    if cuda:
-        torch.cuda.current_stream(dev).synchronize()
-    ctx.export(send_rec.data_ptr(), send_heap.data_ptr())
-    recv_rec, recv_heap, r_rec, r_heap = alltoall_exchange(send_rec, send_heap, rec, heap, group)
+    err = None
+    try:
+        rec, heap = ctx.export_sizes(world)
+        send_rec = torch.empty(max(sum(rec), 1) * XREC, dtype=torch.uint8, device=dev)
+        send_heap = torch.empty(max(sum(heap), 1), dtype=torch.uint8, device=dev)
+        if cuda:
+            torch.cuda.current_stream(dev).synchronize()
+        ctx.export(send_rec.data_ptr(), send_heap.data_ptr())
+    except (native.MrgError, RuntimeError) as e:  # RuntimeError: a torch allocation
+        err = e
+        rec, heap = [0] * world, [0] * world
+        send_rec = torch.empty(1, dtype=torch.uint8, device=dev)
+        send_heap = torch.empty(1, dtype=torch.uint8, device=dev)
+    try:
+        recv_rec, recv_heap, r_rec, r_heap = alltoall_exchange(send_rec, send_heap, rec, heap, group,
+                                                               status=1 if err else 0)
+    except native.MrgError:
+        if err is not None:
+            raise err
+        raise
     if cuda:
         torch.cuda.current_stream(dev).synchronize()
     ctx.import_(recv_rec.data_ptr(), sum(r_rec), recv_heap.data_ptr(), sum(r_heap), r_rec, r_heap)

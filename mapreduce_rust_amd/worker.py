@@ -7,7 +7,7 @@ Same task structure and file conventions as the reference:
 intermediates="text" (default, wc): mr-{m}-{r}.txt byte-identical to the reference's ("key 1" per
 token in input order, mrg_map_text / mrg_reduce_text), so GPU and reference CPU workers can take
 each other's tasks.  intermediates="records": the engine's combined form, mr-{m}-{r}.rec (per-key
-counts as 40-byte exchange records + long-key heap, include/mrgpu.h; little-endian u64 n_records,
+counts as 24-byte exchange records + long-key heap, include/mrgpu.h; little-endian u64 n_records,
 u64 heap_bytes, records, heap) -- far smaller, and the only form for the indexer.  mr-{r}.txt is
 byte-identical to the reference's either way.  A map task and a reduce task may run in different
 processes, as in the reference (the files in the working directory are the hand-off).

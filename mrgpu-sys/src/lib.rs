@@ -23,7 +23,8 @@ pub const MRG_FLAG_FINAL_TXT: u32 = 0x2;
 pub const fn mrg_flag_debug_hash_bits(n: u32) -> u32 {
     (n & 0xFF) << 8
 }
-pub const MRG_XREC_BYTES: usize = 40;
+pub const MRG_XREC_BYTES: usize = 24;
+pub const MRG_ABI_VERSION: u32 = 3;
 pub const MRG_COMM_ID_BYTES: usize = 128;
 
 #[repr(C)]
@@ -59,6 +60,21 @@ pub struct mrg_stats {
     pub exchange_sent: u64,
     pub exchange_recv: u64,
     pub map_spill: u64,
+}
+
+#[repr(C)]
+#[derive(Debug, Default, Clone, Copy)]
+pub struct mrg_run_stats {
+    pub ms_total: f64,
+    pub ms_open: f64,
+    pub ms_read: f64,
+    pub ms_map: f64,
+    pub ms_shuffle: f64,
+    pub ms_reduce: f64,
+    pub ms_write: f64,
+    pub input_bytes: u64,
+    pub output_bytes: u64,
+    pub n_gpus: c_int,
 }
 
 extern "C" {
@@ -108,6 +124,7 @@ extern "C" {
 
     pub fn mrg_run_job(files: *const *const c_char, n_files: usize, n_reduce: u32, app: c_int,
                        out_dir: *const c_char, flags: u32, n_gpus: c_int) -> c_int;
+    pub fn mrg_run_get_stats(out: *mut mrg_run_stats) -> c_int;
     pub fn mrg_free(p: *mut c_void);
 
     pub fn mrg_gen_zipf(ctx: *mut mrg_ctx, d_dst: *mut u8, n_bytes: u64, seed: u64, file_index: u64, vocab: u32,
@@ -173,6 +190,53 @@ impl Ctx {
         Ok(Parts(p))
     }
 
+    /// Start a device-resident job (`mrg_job_begin`).
+    pub fn job_begin(&self, app: c_int, n_reduce: u32, flags: u32) -> Result<(), Error> {
+        check(unsafe { mrg_job_begin(self.0, app, n_reduce, flags) })
+    }
+
+    /// Input already in device memory: documents back to back from `d_bytes` (16-byte aligned),
+    /// document i = bytes [doc_off[i], doc_off[i + 1]) (`mrg_job_set_input`).
+    ///
+    /// # Safety
+    /// `d_bytes` must be a device allocation on this context's device holding `doc_off[n]` bytes, and
+    /// stay valid until the next `job_begin`.
+    pub unsafe fn job_set_input(&self, d_bytes: *const u8, doc_off: &[u64], doc_ids: Option<&[u32]>)
+                                -> Result<(), Error> {
+        let n = doc_off.len().saturating_sub(1) as u32;
+        let ids = doc_ids.map_or(std::ptr::null(), |v| v.as_ptr());
+        check(mrg_job_set_input(self.0, d_bytes, doc_off.as_ptr(), n, ids))
+    }
+
+    /// Map + combine + partition (`mrg_job_map`; wc.rs:6-13, worker.rs:111-131).
+    pub fn job_map(&self) -> Result<(), Error> {
+        check(unsafe { mrg_job_map(self.0) })
+    }
+
+    /// The exchange with the other ranks of `comm` (`mrg_job_shuffle`, RCCL over xGMI).
+    pub fn shuffle(&self, comm: &Comm) -> Result<(), Error> {
+        check(unsafe { mrg_job_shuffle(self.0, comm.0) })
+    }
+
+    /// Sort + group + reduce + format (`mrg_job_reduce`); then the bytes of every `mr-{r}.txt`,
+    /// concatenated in r order, with the partition offsets (n_reduce + 1 of them).
+    pub fn job_reduce(&self, n_reduce: u32) -> Result<(Vec<u8>, Vec<u64>), Error> {
+        let mut total = 0u64;
+        check(unsafe { mrg_job_reduce(self.0, &mut total) })?;
+        let mut off = vec![0u64; n_reduce as usize + 1];
+        check(unsafe { mrg_job_output(self.0, std::ptr::null_mut(), off.as_mut_ptr()) })?;
+        let mut out = vec![0u8; total as usize];
+        check(unsafe { mrg_job_copy_output(self.0, out.as_mut_ptr(), total) })?;
+        Ok((out, off))
+    }
+
+    /// Counters and stage times of the last job (`mrg_get_stats`).
+    pub fn stats(&self) -> Result<mrg_stats, Error> {
+        let mut st = mrg_stats::default();
+        check(unsafe { mrg_get_stats(self.0, &mut st) })?;
+        Ok(st)
+    }
+
     /// `Worker::reduce` (src/mr/worker.rs:157-193): the exact bytes of `mr-{r}.txt`.
     pub fn reduce(&self, app: c_int, r: u32, parts: &[Parts], n_reduce: u32, doc_names: &[&str])
                   -> Result<Vec<u8>, Error> {
@@ -190,11 +254,40 @@ impl Ctx {
     }
 }
 
-/// The whole job over `n_gpus` GPUs (mrcoordinator + workers): out_dir/mr-{r}.txt (+ final.txt).
+/// One rank's membership of an RCCL communicator (one process or thread per GPU).
+pub struct Comm(*mut mrg_comm);
+impl Drop for Comm {
+    fn drop(&mut self) {
+        unsafe { mrg_comm_destroy(self.0) };
+    }
+}
+unsafe impl Send for Comm {}
+
+impl Comm {
+    /// A fresh communicator id, made by one rank and handed to the others out of band.
+    pub fn new_id() -> Result<[u8; MRG_COMM_ID_BYTES], Error> {
+        let mut id = [0u8; MRG_COMM_ID_BYTES];
+        check(unsafe { mrg_comm_get_id(id.as_mut_ptr()) })?;
+        Ok(id)
+    }
+
+    /// Join as `rank` of `n_ranks` on `ctx`'s device (collective: every rank calls it concurrently).
+    pub fn init(ctx: &Ctx, id: &[u8; MRG_COMM_ID_BYTES], n_ranks: i32, rank: i32) -> Result<Comm, Error> {
+        let mut m = std::ptr::null_mut();
+        check(unsafe { mrg_comm_init(ctx.0, id.as_ptr(), n_ranks, rank, &mut m) })?;
+        Ok(Comm(m))
+    }
+}
+
+/// The whole job over `n_gpus` GPUs (mrcoordinator + workers): out_dir/mr-{r}.txt (+ final.txt);
+/// returns the call's phase timings.
 pub fn run_job(files: &[&str], n_reduce: u32, app: c_int, out_dir: &str, flags: u32, n_gpus: i32)
-               -> Result<(), Error> {
+               -> Result<mrg_run_stats, Error> {
     let cs: Vec<CString> = files.iter().map(|f| CString::new(*f).unwrap()).collect();
     let ps: Vec<*const c_char> = cs.iter().map(|c| c.as_ptr()).collect();
     let od = CString::new(out_dir).unwrap();
-    check(unsafe { mrg_run_job(ps.as_ptr(), ps.len(), n_reduce, app, od.as_ptr(), flags, n_gpus) })
+    check(unsafe { mrg_run_job(ps.as_ptr(), ps.len(), n_reduce, app, od.as_ptr(), flags, n_gpus) })?;
+    let mut st = mrg_run_stats::default();
+    check(unsafe { mrg_run_get_stats(&mut st) })?;
+    Ok(st)
 }

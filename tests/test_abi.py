@@ -48,9 +48,40 @@ def test_no_gpu_is_a_clean_error():
 
 def test_record_layout_constant():
     src = open(os.path.join(ROOT, "include", "mrgpu.h")).read()
-    assert "#define MRG_XREC_BYTES 40" in src
+    assert "#define MRG_XREC_BYTES 24" in src and "#define MRG_ABI_VERSION 3" in src
     from mapreduce_rust_amd import native, shuffle
-    assert native.XREC_BYTES == shuffle.XREC == 40
+    assert native.XREC_BYTES == shuffle.XREC == 24 and native.ABI_VERSION == 3
+    assert b"abi 3" in native.load().mrg_version()
+    rs = open(os.path.join(ROOT, "mrgpu-sys", "src", "lib.rs")).read()
+    assert "pub const MRG_XREC_BYTES: usize = 24;" in rs and "pub const MRG_ABI_VERSION: u32 = 3;" in rs
+
+
+def test_merge_sorted_lines_host():
+    """The host k-way merge of the GPUs' sorted final.txt runs (mrgpu.cpp merge_sorted_lines, the
+    multi-GPU half of run.sh:16-20 `cat mr-* | sort`): equals sorted() of all lines, byte order (C
+    locale), with runs lacking a final newline, equal prefixes, duplicates across runs and empty runs."""
+    import random
+    from mapreduce_rust_amd import native
+    rng = random.Random(7)
+    alpha = [b"a", b"b", b"ab", b"abc", b"z", b"\xc3\xa9", b"_", b"0"]
+    for trial in range(200):
+        lines = [b"".join(rng.choice(alpha) for _ in range(rng.randint(1, 4))) + b" " + str(rng.randint(1, 99)).encode()
+                 for _ in range(rng.randint(0, 40))]
+        k = rng.randint(1, 9)
+        runs = [[] for _ in range(k)]
+        for ln in lines:
+            runs[rng.randrange(k)].append(ln)
+        blobs = []
+        for r in runs:
+            r.sort()
+            b = b"".join(x + b"\n" for x in r)
+            if b and rng.random() < 0.3:
+                b = b[:-1]  # no final newline
+            blobs.append(b)
+        got = native.merge_sorted_lines(blobs)
+        assert got == b"".join(x + b"\n" for x in sorted(lines)), trial
+    assert native.merge_sorted_lines([]) == b"" and native.merge_sorted_lines([b"", b""]) == b""
+    assert native.merge_sorted_lines([b"ab 1\nb 2", b"a 3\nab 0\n"]) == b"a 3\nab 0\nab 1\nb 2\n"
 
 
 def test_rust_ffi_crate_declares_the_header():

@@ -14,6 +14,7 @@ pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLDEN = json.load(open(os.path.join(HERE, "golden", "golden.json")))
+X = 24  # exchange record bytes (include/mrgpu.h MRG_XREC_BYTES)
 
 
 def sha(b):
@@ -187,7 +188,7 @@ def test_two_owner_exchange_on_one_gpu(ctx, corpus):
         ctx.set_input(t.data_ptr(), off)
         ctx.map()
         rec, heap = ctx.export_sizes(2)
-        drec = torch.empty(max(sum(rec), 1) * 40, dtype=torch.uint8, device="cuda:0")
+        drec = torch.empty(max(sum(rec), 1) * X, dtype=torch.uint8, device="cuda:0")
         dheap = torch.empty(max(sum(heap), 1), dtype=torch.uint8, device="cuda:0")
         ctx.export(drec.data_ptr(), dheap.data_ptr())
         sends.append((drec.cpu(), dheap.cpu(), rec, heap))
@@ -195,9 +196,9 @@ def test_two_owner_exchange_on_one_gpu(ctx, corpus):
     for owner in range(2):
         recs, heaps, sr, sh = [], [], [], []
         for drec, dheap, rec, heap in sends:
-            ro = sum(rec[:owner]) * 40
+            ro = sum(rec[:owner]) * X
             ho = sum(heap[:owner])
-            recs.append(drec[ro:ro + rec[owner] * 40])
+            recs.append(drec[ro:ro + rec[owner] * X])
             heaps.append(dheap[ho:ho + heap[owner]])
             sr.append(rec[owner])
             sh.append(heap[owner])
@@ -564,7 +565,7 @@ def test_export_import_many_owners(ctx, corpus, G):
         ctx.set_input(t.data_ptr(), off)
         ctx.map()
         rec, heap = ctx.export_sizes(G)
-        drec = torch.empty(max(sum(rec), 1) * 40, dtype=torch.uint8, device="cuda:0")
+        drec = torch.empty(max(sum(rec), 1) * X, dtype=torch.uint8, device="cuda:0")
         dheap = torch.empty(max(sum(heap), 1), dtype=torch.uint8, device="cuda:0")
         ctx.export(drec.data_ptr(), dheap.data_ptr())
         sends.append((drec.cpu(), dheap.cpu(), rec, heap))
@@ -573,13 +574,13 @@ def test_export_import_many_owners(ctx, corpus, G):
     for owner in range(G):
         recs, heaps, sr, shp = [], [], [], []
         for drec, dheap, rec, heap in sends:
-            ro = sum(rec[:owner]) * 40
+            ro = sum(rec[:owner]) * X
             ho = sum(heap[:owner])
-            recs.append(drec[ro:ro + rec[owner] * 40])
+            recs.append(drec[ro:ro + rec[owner] * X])
             heaps.append(dheap[ho:ho + heap[owner]])
             sr.append(rec[owner])
             shp.append(heap[owner])
-        Rt = torch.cat(recs + [torch.zeros(40, dtype=torch.uint8)]).to("cuda:0")
+        Rt = torch.cat(recs + [torch.zeros(X, dtype=torch.uint8)]).to("cuda:0")
         Ht = torch.cat(heaps + [torch.zeros(1, dtype=torch.uint8)]).to("cuda:0")
         ctx.job_begin(M.APP_WC, R)
         ctx.import_(Rt.data_ptr(), sum(sr), Ht.data_ptr(), sum(shp), sr, shp)

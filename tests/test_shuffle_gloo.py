@@ -2,8 +2,8 @@
 
 World size 2 (and 3).  Each rank plays the part of one GPU: it tokenizes its shard of the bundled
 corpus with the oracle (test infrastructure), packs its per-key counts into exchange records exactly
-as mrg_job_export lays them out (include/mrgpu.h: 40-byte records ordered by owner r % G, long keys
-in a heap addressed per sender segment), runs the real alltoall_exchange, unpacks what it received
+as mrg_job_export lays them out (include/mrgpu.h: 24-byte records ordered by owner r % G, short keys
+packed in the record, long keys in a heap addressed per sender segment), runs the real alltoall_exchange, unpacks what it received
 the way mrg_job_import does, and reduces the partitions it owns.  The union of all ranks' outputs
 must equal the single-process oracle job byte for byte (golden digests of SURVEY.md §8(c)).
 """
@@ -36,16 +36,24 @@ def pack(counts, n_reduce, n_owners, key_hash):
     rc, hc = [], []
     for o in range(n_owners):
         seg = bytearray()
+        n = 0
         for k, c in by_owner[o]:
-            pre = k[:16].ljust(16, b"\0")
+            if len(k) > 16:  # long form: heap offset, 64-bit count
+                recs += struct.pack("<QQII", len(seg), c, 0xFFFFFFFF, len(k))
+                seg += k
+                n += 1
+                continue
+            pre = k.ljust(16, b"\0")
             k0 = int.from_bytes(pre[:8], "big")
             k1 = int.from_bytes(pre[8:], "big")
-            hoff = 0xFFFFFFFFFFFFFFFF
-            if len(k) > 16:
-                hoff = len(seg)
-                seg += k
-            recs += struct.pack("<QQQIIQ", k0, k1, c, 0xFFFFFFFF, len(k), hoff)
-        rc.append(len(by_owner[o]))
+            while True:  # short form: the count in 32 bits, larger counts over several records
+                part = min(c, 0xFFFFFFFF)
+                recs += struct.pack("<QQII", k0, k1, part, len(k))
+                n += 1
+                c -= part
+                if c == 0:
+                    break
+        rc.append(n)
         hc.append(len(seg))
         heap += seg
     return bytes(recs), bytes(heap), rc, hc
@@ -58,11 +66,13 @@ def unpack(recv_rec, recv_heap, r_rec, r_heap):
     i = 0
     for n, hb in zip(r_rec, r_heap):
         for _ in range(n):
-            k0, k1, c, _doc, ln, hoff = struct.unpack_from("<QQQIIQ", recv_rec, i * 40)
+            a, b, v, ln = struct.unpack_from("<QQII", recv_rec, i * 24)
             if ln > 16:
-                k = bytes(recv_heap[hbase + hoff:hbase + hoff + ln])
+                k = bytes(recv_heap[hbase + a:hbase + a + ln])
+                c = b
             else:
-                k = (k0.to_bytes(8, "big") + k1.to_bytes(8, "big"))[:ln]
+                k = (a.to_bytes(8, "big") + b.to_bytes(8, "big"))[:ln]
+                c = v
             out[k] = out.get(k, 0) + c
             i += 1
         hbase += hb
