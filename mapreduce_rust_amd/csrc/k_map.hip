@@ -1,4 +1,4 @@
-// k_map.hip -- the map kernel: tokenize + local combine (MI355X / gfx950), v7.
+// k_map.hip -- the map kernel: tokenize + local combine (MI355X / gfx950).
 //
 // Replaces wc::map (src/app/wc.rs:6-13) -- delete every codepoint outside \w ∪ \s, split on
 // White_Space -- fused with the per-token part of write_key_value_to_file (src/mr/worker.rs:127-131).
@@ -6,29 +6,34 @@
 // SipHash(key) % R is a pure function of the key.  Also validates UTF-8 like read_to_string
 // (worker.rs:75): the first invalid byte offset is reported and the job fails with MRG_EUTF8.
 //
-// Layout: documents back to back in one HBM buffer; each document is cut into 1 KiB
-// tiles on a 16-byte-aligned grid.  One 16-wave workgroup per CU walks the tiles; every WAVE works
-// on a tile of its own (no workgroup barrier in the main loop) with the next two tiles' loads in
-// flight in registers.  The 16 waves share the workgroup's LDS combine table.
+// Layout: documents back to back in one HBM buffer; each document is cut into 2 KiB
+// blocks (two 1 KiB tiles) on a 16-byte-aligned grid.  One 16-wave workgroup per CU owns an equal
+// share of the blocks; its waves take the next block from an LDS counter (no workgroup barrier in
+// the main loop), with the next block's three 16-byte loads per lane in flight in registers (A/B
+// register sets).  The 16 waves share the workgroup's LDS combine table.
 //
 // ASCII tiles (wave-uniform test) take the fast path, written for few instructions per byte:
-//   1. lane l classifies its 16-byte segment through a 128-entry u16 LDS LUT into W16 (\w) and S16
-//      (White_Space) masks; token starts = non-space bytes after a space (the neighbour lane's last
-//      class arrives by DPP wave_shr); a DPP prefix sum gives every start a queue slot;
-//   2. each lane stores its 2-segment mask window (W and S of segments g, g+1) -- a consumer lane
-//      reads ONE 8-byte word to find its token's raw length (first space: ffbl), the \w span
-//      (bfe + ffbl/ffbh) and whether a deleted byte sits inside the token ("don't");
-//   3. per token (one per lane per round): 5 LDS dwords -> v_perm with a length-masked selector gives
-//      the big-endian packed key (k0, k1) in 4 instructions; interior deletions are squeezed out by
-//      128-bit shifts (one per gap); tokens that run past the 2-segment window or the staged halo
-//      take the exact per-codepoint walker.
-// Non-ASCII tiles use the per-codepoint walker for every token (UTF-8 decode + class table).
-// Keys of <= 16 bytes go to the workgroup's LDS hash table (exact: the packed key IS the identity)
-// of 8-slot tagged groups; a miss is appended to one of 512 hash buckets in HBM, into the region
-// this workgroup owns in that bucket (an LDS cursor per bucket: no HBM atomics).  Keys > 16 bytes
-// become long-token records (start, raw length, doc) resolved by the collision-safe fingerprint
-// sort (k_keys.hip).  At the end the LDS table is flushed, sorted by bucket, into the workgroup's
-// flush region.
+//   1. lane l classifies its two 16-byte segments through a 128-entry byte LUT (32 dwords, one per
+//      LDS bank) into W16 (\w) and S16 (White_Space) masks; the first halo segment by 16 lanes and
+//      two ballots; token starts = non-space bytes after a space (the neighbour lane's last class by
+//      DPP wave_shr); a DPP prefix sum gives every start a queue slot;
+//   2. per tile each lane stores its 2-segment mask window (W and S of segments g, g+1) -- a consumer
+//      lane reads ONE 8-byte word to find its token's raw length (first space), the \w span and
+//      whether a deleted byte sits inside the token ("don't");
+//   3. TWO tokens per lane per round (queue entries q and q + 64): 5 window dwords aligned to the
+//      key's first byte (v_alignbyte) -> v_perm with a per-(length, 1-byte gap) selector from an LDS
+//      table gives the big-endian packed key (k0, k1); further interior deletions are squeezed out
+//      by 128-bit shifts; tokens that run past the 2-segment window or the staged halo are deferred
+//      to the exact per-codepoint walker.
+// Non-ASCII tiles are listed by the main loop and walked afterwards by all 16 waves (UTF-8 decode +
+// two-level class table per lane).
+// Keys of <= 16 bytes go to the workgroup's LDS hash table (exact: the packed key IS the identity):
+// 4096 slots in 2-way sets, claimed only on a key's second sighting (a two-position Bloom
+// doorkeeper).  A miss is appended to one of 256 hash buckets in HBM, into the region this workgroup
+// owns in that bucket (one 64-bit LDS atomic on an absolute record cursor: no HBM atomics).  Keys > 16
+// bytes become long-token records (start, raw length, doc) resolved by the collision-safe
+// fingerprint sort (k_keys.hip).  At the end the LDS table is flushed, sorted by bucket, into the
+// workgroup's flush region.
 #include "mrg_device.h"
 #include "mrg_internal.h"
 
