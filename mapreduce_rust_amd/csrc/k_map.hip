@@ -204,8 +204,10 @@ struct alignas(16) KeyPair {
     uint64_t a, b;
 };
 
-// Workgroup LDS combine table: 2-way sets -- slots 2s and 2s + 1 of set s = low
-// hash bits.  A probe reads both keys at once (one LDS round trip: no tag step) and adds 1 to the
+// Workgroup LDS combine table: 2-way sets -- slots s and s + NS of set s = low
+// hash bits (way-major: way 0 of the 2048 sets, then way 1, so a wave's 16-byte reads of one way
+// spread over all 64 banks instead of half of them; A/B -0.5 % map).  A probe reads both keys at
+// once (one LDS round trip: no tag step) and adds 1 to the
 // matching slot's count.  A new key claims an empty way by a 64-bit CAS on k0 (EMPTY -> k0), then
 // writes k1 (and doc) and adds its first count; slots only ever go EMPTY -> (k0, EMPTY) -> (k0, k1),
 // so a slot read equal to the full key is that key's slot for good.  A reader that sees a half
@@ -271,7 +273,7 @@ struct LdsTable {
         if (!admitted(h)) return false;
         for (uint32_t w = 0; w < 2; ++w) {
             if (!(w ? e1 : e0)) continue;
-            const uint32_t s = s0 + w;
+            const uint32_t s = s0 + w * NS;  // way w of set s0: way-major layout
             const unsigned long long old = atomicCAS(&key[s].a, (unsigned long long)MRG_EMPTY_K0, (unsigned long long)a);
             if (old == MRG_EMPTY_K0) {
                 key[s].b = b;
@@ -288,12 +290,12 @@ struct LdsTable {
     // one probe per lane (slow path: one token per lane)
     __device__ __forceinline__ bool insert_wave(bool act, uint64_t a, uint64_t b, uint32_t d, uint32_t h,
                                                 uint32_t abl = 0) {
-        const uint32_t s0 = act ? 2u * (h & (NS - 1)) : 0u;
-        const KeyPair k0 = key[s0], k1 = key[s0 + 1];
+        const uint32_t s0 = act ? (h & (NS - 1)) : 0u;
+        const KeyPair k0 = key[s0], k1 = key[s0 + NS];
         const bool m0 = act & (((k0.a ^ a) | (k0.b ^ b)) == 0) & (!IDX || doc[s0] == d);
-        const bool m1 = act & !m0 & (((k1.a ^ a) | (k1.b ^ b)) == 0) & (!IDX || doc[s0 + 1] == d);
+        const bool m1 = act & !m0 & (((k1.a ^ a) | (k1.b ^ b)) == 0) & (!IDX || doc[s0 + NS] == d);
         bool hit = m0 | m1;
-        if (hit && !(abl & 16u)) atomicAdd(&cnt[m0 ? s0 : s0 + 1], 1u);
+        if (hit && !(abl & 16u)) atomicAdd(&cnt[m0 ? s0 : s0 + NS], 1u);
         const bool e0 = k0.a == MRG_EMPTY_K0, e1 = k1.a == MRG_EMPTY_K0;
         const bool need = act && !hit && (e0 || e1);
         if (__any(need)) {
@@ -355,20 +357,20 @@ __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint3
     const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
     const uint32_t hA = key_hash(a0, a1, dkey, hbits), hB = key_hash(b0, b1, dkey, hbits);
     const bool actA = ha && !(abl & 2u), actB = hb && !(abl & 2u);
-    const uint32_t sA = actA ? 2u * (hA & (NS - 1)) : 0u, sB = actB ? 2u * (hB & (NS - 1)) : 0u;
+    const uint32_t sA = actA ? (hA & (NS - 1)) : 0u, sB = actB ? (hB & (NS - 1)) : 0u;
     const uint32_t bA = bucket_of(hA), bB = bucket_of(hB);
     // both ways of both sets: four 16-byte reads in flight together, with the two region ends
-    const KeyPair kA0 = T.key[sA], kA1 = T.key[sA + 1], kB0 = T.key[sB], kB1 = T.key[sB + 1];
+    const KeyPair kA0 = T.key[sA], kA1 = T.key[sA + NS], kB0 = T.key[sB], kB1 = T.key[sB + NS];
     const uint64_t endA = R.end[bA], endB = R.end[bB];
     auto eq = [&](const KeyPair &k, uint64_t x, uint64_t y, uint32_t s) {
         return (((k.a ^ x) | (k.b ^ y)) == 0) & (!IDX || T.doc[s] == dkey);
     };
-    const bool mA0 = actA & eq(kA0, a0, a1, sA), mA1 = actA & !mA0 & eq(kA1, a0, a1, sA + 1);
-    const bool mB0 = actB & eq(kB0, b0, b1, sB), mB1 = actB & !mB0 & eq(kB1, b0, b1, sB + 1);
+    const bool mA0 = actA & eq(kA0, a0, a1, sA), mA1 = actA & !mA0 & eq(kA1, a0, a1, sA + NS);
+    const bool mB0 = actB & eq(kB0, b0, b1, sB), mB1 = actB & !mB0 & eq(kB1, b0, b1, sB + NS);
     bool hitA = mA0 | mA1, hitB = mB0 | mB1;
     if (!(abl & 16u)) {
-        if (hitA) atomicAdd(&T.cnt[mA0 ? sA : sA + 1], 1u);
-        if (hitB) atomicAdd(&T.cnt[mB0 ? sB : sB + 1], 1u);
+        if (hitA) atomicAdd(&T.cnt[mA0 ? sA : sA + NS], 1u);
+        if (hitB) atomicAdd(&T.cnt[mB0 ? sB : sB + NS], 1u);
     }
     // empty ways exist only until the table has filled (wave-uniform: a stale count only means
     // an unneeded test)
