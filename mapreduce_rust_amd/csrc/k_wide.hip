@@ -51,6 +51,61 @@ __device__ __forceinline__ bool key_lt(uint64_t a0, uint64_t a1, uint64_t b0, ui
     return a0 < b0 || (a0 == b0 && a1 < b1);
 }
 
+// The 64 key bits from bit h on (bit 0 = the most significant bit of k0), zero past bit 127.
+__device__ __forceinline__ uint64_t key_bits_from(uint64_t k0, uint64_t k1, uint32_t h) {
+    return h == 0 ? k0 : (h < 64 ? (k0 << h) | (k1 >> (64 - h)) : k1 << (h - 64));
+}
+// leading bits two keys share (128 if equal)
+__device__ __forceinline__ uint32_t common_bits(uint64_t a0, uint64_t a1, uint64_t b0, uint64_t b1) {
+    const uint64_t x0 = a0 ^ b0, x1 = a1 ^ b1;
+    return x0 ? (uint32_t)__builtin_clzll(x0) : (x1 ? 64u + (uint32_t)__builtin_clzll(x1) : 128u);
+}
+
+// Splitter index: m sorted splitters share their top cp bits; the next IB bits of a key select
+// ix[v] .. ix[v + 1], the splitters carrying those same bits, so a lookup compares the key with
+// that handful (usually 0-2) instead of walking log2(m) levels of 16-byte LDS reads.  A key whose
+// top cp bits differ from the splitters' lies below all of them or above all of them.
+template <uint32_t IB, class IX>
+struct SplitIndex {
+    const uint64_t *spl;  // m (k0, k1) pairs in LDS
+    const IX *ix;         // [2^IB + 1] in LDS
+    uint32_t m, cp;
+    __device__ __forceinline__ static uint32_t slot(uint64_t k0, uint64_t k1, uint32_t cp) {
+        return (uint32_t)(key_bits_from(k0, k1, cp) >> (64 - IB));
+    }
+    __device__ __forceinline__ static uint32_t prefix_bits(const uint64_t *spl, uint32_t m) {
+        return min(common_bits(spl[0], spl[1], spl[2 * (m - 1)], spl[2 * (m - 1) + 1]), 128u - IB);
+    }
+    // the index of m >= 1 splitters, by threads tid, tid + nt, ... (the caller synchronises)
+    __device__ __forceinline__ static void build(const uint64_t *spl, uint32_t m, IX *ix, uint32_t tid, uint32_t nt) {
+        const uint32_t cp = prefix_bits(spl, m);
+        for (uint32_t v = tid; v <= (1u << IB); v += nt) {  // first splitter whose slot is >= v
+            uint32_t lo = 0, hi = m;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (slot(spl[2 * mid], spl[2 * mid + 1], cp) < v) lo = mid + 1;
+                else hi = mid;
+            }
+            ix[v] = (IX)lo;
+        }
+    }
+    // number of splitters <= key (m >= 1)
+    __device__ __forceinline__ uint32_t upper(uint64_t k0, uint64_t k1) const {
+        const uint64_t p0 = spl[0], p1 = spl[1];
+        if (common_bits(k0, k1, p0, p1) < cp) return key_lt(k0, k1, p0, p1) ? 0u : m;
+        const uint32_t v = slot(k0, k1, cp);
+        uint32_t lo = ix[v], hi = ix[v + 1];
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (key_lt(k0, k1, spl[2 * mid], spl[2 * mid + 1])) hi = mid;
+            else lo = mid + 1;
+        }
+        return lo;
+    }
+};
+typedef SplitIndex<12, uint16_t> LeafIndex;   // L2: <= 1023 leaf splitters per L1 bucket
+typedef SplitIndex<8, uint8_t> L1Index;       // L1: <= 63 splitters per partition
+
 // ---------------------------------------------------------------- the map's records (count 1)
 // main segments: the tail regions (bucket-major, map workgroup minor), then the per-bucket
 // overflow lists -- the order of mrg_launch_wmain_counts
@@ -186,7 +241,17 @@ struct L1Args {
     uint32_t *cnt;           // [B1][ntiles] (scanned in place between the two kernels)
     uint64_t *out;           // L1 output, 2 words per record
     uint16_t *bid;           // [n] L1 bucket of each record: written by the counting pass, read by the scatter
+    const uint8_t *ix1;      // counting pass: per-partition splitter index [R][W_IX1] (null: binary search)
 };
+
+// L1 splitter index of partition r: 257 entries, then the prefix bit count (L1Index)
+constexpr uint32_t W_IX1 = 260;
+__global__ void k_wl1ix(const uint64_t *spl1, uint32_t m, uint8_t *ix1) {
+    const uint32_t r = blockIdx.x;
+    const uint64_t *sp = spl1 + 2ull * r * m;
+    L1Index::build(sp, m, ix1 + (uint64_t)r * W_IX1, threadIdx.x, blockDim.x);
+    if (threadIdx.x == 0) ix1[(uint64_t)r * W_IX1 + 257] = (uint8_t)L1Index::prefix_bits(sp, m);
+}
 
 // L1 tile t: records [t * T1, min(n, (t+1) * T1)); WITH_SCATTER: write them, else count them
 template <bool SCATTER>
@@ -197,11 +262,15 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl1(L1Args L) {
     uint32_t *s_h = reinterpret_cast<uint32_t *>(s_spl + 2ull * L.R * m);
     uint64_t *s_off = reinterpret_cast<uint64_t *>(s_h + ((L.B1 + 1u) & ~1u));
     uint64_t *s_ptr = s_off + W_SEGLDS;
+    uint8_t *s_ix = reinterpret_cast<uint8_t *>(s_ptr + W_SEGLDS);   // [R][W_IX1] if L.ix1
     __shared__ uint64_t s_lo, s_hi;
     const uint32_t tid = threadIdx.x, t = blockIdx.x;
     const uint64_t t0 = (uint64_t)t * MRG_WIDE_T1, t1 = min(L.n, t0 + MRG_WIDE_T1);
     for (uint32_t i = tid; i < 2u * L.R * m; i += W_WG) s_spl[i] = L.spl1[i];
     for (uint32_t b = tid; b < L.B1; b += W_WG) s_h[b] = SCATTER ? L.cnt[(uint64_t)b * L.ntiles + t] : 0u;
+    if (!SCATTER && L.ix1)
+        for (uint32_t i = tid; i < L.R * (W_IX1 / 4); i += W_WG)
+            reinterpret_cast<uint32_t *>(s_ix)[i] = reinterpret_cast<const uint32_t *>(L.ix1)[i];
     if (tid == 0) {
         const auto off = [&](uint64_t x) { return L.off[x]; };
         s_lo = seg_find(off, 0, L.nseg, t0);
@@ -249,12 +318,19 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl1(L1Args L) {
                 b = bk[u];
             } else {
                 const uint32_t r = part_of(k0[u], k1[u], L.R);
-                const uint32_t q = upper_idx(
-                    [&](uint32_t x, uint64_t &a, uint64_t &c) {
-                        a = s_spl[2ull * (r * m + x)];
-                        c = s_spl[2ull * (r * m + x) + 1];
-                    },
-                    m, k0[u], k1[u]);
+                uint32_t q;
+                if (L.ix1) {
+                    const uint8_t *ixr = s_ix + r * W_IX1;
+                    const L1Index li{s_spl + 2ull * r * m, ixr, m, ixr[257]};
+                    q = li.upper(k0[u], k1[u]);
+                } else {
+                    q = upper_idx(
+                        [&](uint32_t x, uint64_t &a, uint64_t &c) {
+                            a = s_spl[2ull * (r * m + x)];
+                            c = s_spl[2ull * (r * m + x) + 1];
+                        },
+                        m, k0[u], k1[u]);
+                }
                 b = r * L.B1r + q;
                 gw(L.bid)[base + (uint64_t)u * W_WG] = (uint16_t)b;
             }
@@ -365,16 +441,18 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
             s_spl[2 * q] = s_smp[2 * k];
             s_spl[2 * q + 1] = s_smp[2 * k + 1];
         }
+        lds_barrier();
+        // the sample is dead now: its LDS holds the splitter index
+        LeafIndex::build(s_spl, B2 - 1u, reinterpret_cast<uint16_t *>(s_smp), tid, W_WG);
     }
     for (uint32_t j = tid; j < MRG_WIDE_MAXB2; j += W_WG) {
         s_cnt[j] = 0;
         s_cur[j] = 0;
     }
     lds_barrier();
-    auto sub_of = [&](uint64_t k0, uint64_t k1) {
-        return upper_idx([&](uint32_t x, uint64_t &a, uint64_t &c) { a = s_spl[2 * x]; c = s_spl[2 * x + 1]; }, B2 - 1u,
-                         k0, k1);
-    };
+    const LeafIndex si{s_spl, reinterpret_cast<const uint16_t *>(s_smp), B2 - 1u,
+                       B2 > 1 ? LeafIndex::prefix_bits(s_spl, B2 - 1u) : 0u};
+    auto sub_of = [&](uint64_t k0, uint64_t k1) { return B2 > 1 ? si.upper(k0, k1) : 0u; };
     // ---- histogram (U records per thread in flight)
     constexpr int U = 4;
     typedef uint64_t v2 __attribute__((ext_vector_type(2)));
@@ -1358,26 +1436,78 @@ __global__ void k_wdrop(const uint32_t *nleaf, uint32_t B1r, uint32_t R, const u
 
 // ---------------------------------------------------------------- lines
 // One workgroup per L1 bucket streams the bucket's distinct keys (all its leaves, the dropped last
-// key of a partition excluded) in chunks of W_WCH: key i of the bucket -> its leaf by a search of
-// the leaves' running key counts (LDS), the lines laid out in LDS by a block scan of their lengths,
-// then stored to the output as aligned dwords (byte stores only at the two ends of a chunk).
-constexpr uint32_t W_WCH = 2048;              // keys per chunk (2 per thread)
-constexpr uint32_t W_STAGE = 40 * W_WCH;      // >= W_WCH lines of <= 16 + 1 + 20 + 1 bytes
+// key of a partition excluded) in chunks of W_WCH, one key per thread: key i of the bucket -> its
+// leaf by a search of the leaves' running key counts (LDS), the line built in registers as
+// little-endian words, OR-ed into a zeroed LDS stage at its offset from a block scan of the line
+// lengths (whole dwords: the first and last are shared with the neighbour lines), then the stage
+// is stored as aligned dwords (byte stores only at the two ends of a chunk) and zeroed on the way.
+// 512-thread workgroups, several per CU: while one formats, the others load and store.
+constexpr uint32_t W_WWG = 512;
+constexpr uint32_t W_WCH = W_WWG;             // keys per chunk
+constexpr uint32_t W_STAGE = 40 * W_WCH;      // >= W_WCH lines of <= 16 + 1 + 20 + 1 bytes (+ 3 of shift)
 
-__global__ __launch_bounds__(W_WG, 1) void k_wwrite(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *nleaf,
+__device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+// "key count\n" of a short key as little-endian bytes in w[0..4]; returns its length
+__device__ __forceinline__ uint32_t line_words(uint64_t k0, uint64_t k1, uint64_t n, uint64_t w[5]) {
+    const uint32_t L = mrg_short_len(k0, k1), nd = mrg_ndigits(n);
+    // suffix bytes: ' ', the nd digits, '\n' -- little-endian in t0..t2 (at most 22 bytes)
+    uint64_t t0 = ' ', t1 = 0, t2 = 0;
+    auto put = [&](uint32_t pos, uint64_t byte) {
+        const uint64_t v = byte << (8u * (pos & 7u));
+        if (pos < 8u) t0 |= v;
+        else if (pos < 16u) t1 |= v;
+        else t2 |= v;
+    };
+    if (n < 10u) {
+        t0 |= ((uint64_t)('0' + n) << 8) | ((uint64_t)'\n' << 16);
+    } else {
+        uint64_t v = n;
+        for (uint32_t i = nd; i >= 1u; --i) {
+            uint32_t dgt;
+            if (v <= 0xFFFFFFFFull) {
+                const uint32_t v32 = (uint32_t)v;
+                dgt = v32 % 10u;
+                v = v32 / 10u;
+            } else {
+                dgt = (uint32_t)(v % 10u);
+                v /= 10u;
+            }
+            put(i, '0' + dgt);
+        }
+        put(nd + 1u, '\n');
+    }
+    // key bytes first (big-endian packed -> byte-swapped words), the suffix shifted in at byte L
+    w[0] = bswap64(k0);
+    w[1] = bswap64(k1);
+    const uint32_t q = L >> 3, r = 8u * (L & 7u);
+    const uint64_t u0 = t0 << r;
+    const uint64_t u1 = (t1 << r) | (r ? t0 >> (64u - r) : 0ull);
+    const uint64_t u2 = (t2 << r) | (r ? t1 >> (64u - r) : 0ull);
+    const uint64_t u3 = r ? t2 >> (64u - r) : 0ull;
+    w[0] |= q == 0u ? u0 : 0ull;
+    w[1] |= q == 0u ? u1 : (q == 1u ? u0 : 0ull);
+    w[2] = q == 0u ? u2 : (q == 1u ? u1 : u0);
+    w[3] = q == 0u ? u3 : (q == 1u ? u2 : u1);
+    w[4] = q == 0u ? 0ull : (q == 1u ? u3 : u2);
+    return L + 2u + nd;
+}
+
+__global__ __launch_bounds__(W_WWG) void k_wwrite(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *nleaf,
                                                     const uint64_t *leaf_out, const uint32_t *leaf_nd,
                                                     const uint32_t *leaf_drop, const uint64_t *leaf_off,
                                                     uint8_t *out) {
     __shared__ uint32_t s_buf[W_STAGE / 4];
     __shared__ uint32_t s_kst[MRG_WIDE_MAXB2 + 1];   // keys before leaf l (this bucket)
     __shared__ uint64_t s_lout[MRG_WIDE_MAXB2];
-    __shared__ uint32_t s_ws[W_NW];
-    uint8_t *sb = reinterpret_cast<uint8_t *>(s_buf);
+    __shared__ uint32_t s_ws[W_WWG / 64];
+    const uint8_t *sb = reinterpret_cast<const uint8_t *>(s_buf);
     const uint32_t tid = threadIdx.x, b = blockIdx.x;
     const uint32_t nl = nleaf[b];
     const uint64_t l0 = (uint64_t)b * MRG_WIDE_MAXB2;
-    {  // running key counts of the leaves (MAXB2 / W_WG per thread)
-        constexpr uint32_t PT = MRG_WIDE_MAXB2 / W_WG;
+    for (uint32_t i = tid; i < W_STAGE / 4; i += W_WWG) s_buf[i] = 0;
+    {  // running key counts of the leaves (MAXB2 / W_WWG per thread)
+        constexpr uint32_t PT = MRG_WIDE_MAXB2 / W_WWG;
         uint32_t v[PT], sum = 0;
         for (uint32_t x = 0; x < PT; ++x) {
             const uint32_t l = tid * PT + x;
@@ -1386,7 +1516,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wwrite(const uint64_t *keys, const 
             sum += v[x];
         }
         uint32_t tot;
-        uint32_t run = block_scan_excl(sum, s_ws, &tot);
+        uint32_t run = block_scan_excl<W_WWG / 64>(sum, s_ws, &tot);
         for (uint32_t x = 0; x < PT; ++x) {
             s_kst[tid * PT + x] = run;
             run += v[x];
@@ -1396,69 +1526,62 @@ __global__ __launch_bounds__(W_WG, 1) void k_wwrite(const uint64_t *keys, const 
     lds_barrier();
     const uint32_t K = s_kst[MRG_WIDE_MAXB2];
     uint64_t dst = leaf_off[l0];
-    // this thread's keys of chunk c0 (keys 2t, 2t + 1): leaf by a search of the running counts, then
-    // the key and count loads.  The next chunk's are fetched before this chunk is laid out and
-    // stored, so their leaf search and load latency overlap the current chunk's work.
-    struct Two {
-        uint64_t a[2], c[2], n[2];
+    // this thread's key of chunk c0: leaf by a search of the running counts, then the key and count
+    // loads.  The next chunk's are fetched before this chunk is laid out and stored, so their leaf
+    // search and load latency overlap the current chunk's work.
+    struct One {
+        uint64_t a, c, n;
     };
-    auto fetch = [&](uint32_t c0, Two &F) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const uint32_t i = c0 + 2 * tid + (uint32_t)u;
-            F.a[u] = F.c[u] = F.n[u] = 0;
-            if (i < K) {
-                uint32_t lo = 0, hi = nl;   // leaf l: s_kst[l] <= i < s_kst[l + 1] (last such l)
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (s_kst[mid] <= i) lo = mid;
-                    else hi = mid;
-                }
-                const uint64_t slot = s_lout[lo] + (i - s_kst[lo]);
-                F.a[u] = keys[2 * slot];
-                F.c[u] = keys[2 * slot + 1];
-                F.n[u] = ocnt[slot];
+    auto fetch = [&](uint32_t c0, One &F) {
+        const uint32_t i = c0 + tid;
+        F.a = F.c = F.n = 0;
+        if (i < K) {
+            uint32_t lo = 0, hi = nl;   // leaf l: s_kst[l] <= i < s_kst[l + 1] (last such l)
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_kst[mid] <= i) lo = mid;
+                else hi = mid;
             }
+            const uint64_t slot = s_lout[lo] + (i - s_kst[lo]);
+            F.a = keys[2 * slot];
+            F.c = keys[2 * slot + 1];
+            F.n = ocnt[slot];
         }
     };
-    Two cur, nxt;
+    One cur, nxt;
     if (K) fetch(0, cur);
     for (uint32_t c0 = 0; c0 < K; c0 += W_WCH) {
         if (c0 + W_WCH < K) fetch(c0 + W_WCH, nxt);
-        const uint64_t *a = cur.a, *c = cur.c, *n = cur.n;
-        uint32_t len[2] = {0, 0}, nd[2] = {0, 0}, ll[2] = {0, 0};
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-            if (c0 + 2 * tid + (uint32_t)u < K) {
-                len[u] = mrg_short_len(a[u], c[u]);
-                nd[u] = mrg_ndigits(n[u]);
-                ll[u] = len[u] + 2u + nd[u];
-            }
+        uint64_t w[5];
+        const uint32_t ll = c0 + tid < K ? line_words(cur.a, cur.c, cur.n, w) : 0u;
         uint32_t tot;
-        const uint32_t at = block_scan_excl(ll[0] + ll[1], s_ws, &tot);
+        const uint32_t at = block_scan_excl<W_WWG / 64>(ll, s_ws, &tot);
         const uint32_t sh = (uint32_t)(dst & 3u);   // stage at (dst & 3): output dwords align in LDS
-        uint32_t o = sh + at;
+        if (ll) {
+            const uint32_t o = sh + at, base = o >> 2, bs = 8u * (o & 3u);
+            const uint32_t ndw = ((o & 3u) + ll + 3u) >> 2;
+            uint32_t prev = 0;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (!ll[u]) continue;
-            uint8_t *q = sb + o;
-            for (uint32_t x = 0; x < len[u]; ++x) q[x] = (uint8_t)mrg_key_byte(a[u], c[u], x);
-            q[len[u]] = ' ';
-            uint64_t v = n[u];
-            for (uint32_t x = nd[u]; x > 0; --x) {
-                q[len[u] + x] = (uint8_t)('0' + v % 10u);
-                v /= 10u;
+            for (uint32_t j = 0; j < 10; ++j) {
+                const uint32_t d = (uint32_t)(w[j >> 1] >> (32u * (j & 1u)));
+                const uint32_t e = (d << bs) | (bs ? prev >> (32u - bs) : 0u);
+                prev = d;
+                if (j < ndw) atomicOr(&s_buf[base + j], e);
             }
-            q[len[u] + 1 + nd[u]] = '\n';
-            o += ll[u];
+            if (10u < ndw) atomicOr(&s_buf[base + 10u], prev >> (32u - bs));
         }
         lds_barrier();
         const uint64_t end = dst + tot;
         const uint64_t a4 = (dst + 3u) & ~3ull, e4 = end & ~3ull;
-        for (uint64_t x = dst + tid; x < min(a4, end); x += W_WG) out[x] = sb[sh + (x - dst)];
-        for (uint64_t w = a4 / 4 + tid; w < e4 / 4; w += W_WG)
-            reinterpret_cast<uint32_t *>(out)[w] = s_buf[(sh + (w * 4 - dst)) / 4];
-        for (uint64_t x = max(e4, a4) + tid; x < end; x += W_WG) out[x] = sb[sh + (x - dst)];
+        for (uint64_t x = dst + tid; x < min(a4, end); x += W_WWG) out[x] = sb[sh + (x - dst)];
+        for (uint64_t x = max(e4, a4) + tid; x < end; x += W_WWG) out[x] = sb[sh + (x - dst)];
+        for (uint64_t w4 = a4 / 4 + tid; w4 < e4 / 4; w4 += W_WWG) {
+            const uint32_t i = (sh + (uint32_t)(w4 * 4 - dst)) / 4;
+            reinterpret_cast<uint32_t *>(out)[w4] = s_buf[i];
+        }
+        lds_barrier();
+        // zero what this chunk used (its byte-stored ends included) for the next chunk's ORs
+        for (uint32_t i = tid; i < (sh + tot + 3u) / 4u; i += W_WWG) s_buf[i] = 0;
         dst = end;
         lds_barrier();
         cur = nxt;
@@ -1632,9 +1755,15 @@ size_t mrg_wide_l1_lds(uint32_t R, uint32_t B1r, uint32_t B1) {
 }
 void mrg_wide_launch_l1(const BucketArgs &a, const uint64_t *off, const uint64_t *segptr, uint64_t nseg, uint64_t n,
                         const uint64_t *spl1, uint32_t R, uint32_t B1r, uint32_t *cnt, uint32_t ntiles, uint64_t *out,
-                        uint16_t *bid, bool scatter, hipStream_t s) {
-    L1Args L{a, off, segptr, nseg, n, spl1, R, B1r, R * B1r, ntiles, cnt, out, bid};
-    const size_t lds = mrg_wide_l1_lds(R, B1r, R * B1r);
+                        uint16_t *bid, uint8_t *ix1, bool scatter, hipStream_t s) {
+    L1Args L{a, off, segptr, nseg, n, spl1, R, B1r, R * B1r, ntiles, cnt, out, bid, nullptr};
+    size_t lds = mrg_wide_l1_lds(R, B1r, R * B1r);
+    // the counting pass searches the splitters through an index when it fits beside them in LDS
+    if (!scatter && ix1 && B1r >= 5 && lds + (size_t)W_IX1 * R <= 160u * 1024u) {
+        hipLaunchKernelGGL(k_wl1ix, dim3(R), dim3(320), 0, s, spl1, B1r - 1u, ix1);
+        L.ix1 = ix1;
+        lds += (size_t)W_IX1 * R;
+    }
     if (scatter) hipLaunchKernelGGL(k_wl1<true>, dim3(ntiles), dim3(W_WG), lds, s, L);
     else hipLaunchKernelGGL(k_wl1<false>, dim3(ntiles), dim3(W_WG), lds, s, L);
 }
@@ -1716,7 +1845,7 @@ void mrg_wide_launch_drop(const uint32_t *nleaf, uint32_t B1r, uint32_t R, const
 void mrg_wide_launch_write(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *nleaf, const uint64_t *leaf_out,
                            const uint32_t *leaf_nd, const uint32_t *leaf_drop, const uint64_t *leaf_off, uint32_t B1,
                            uint8_t *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_wwrite, dim3(B1), dim3(W_WG), 0, s, keys, ocnt, nleaf, leaf_out, leaf_nd, leaf_drop, leaf_off,
+    hipLaunchKernelGGL(k_wwrite, dim3(B1), dim3(W_WWG), 0, s, keys, ocnt, nleaf, leaf_out, leaf_nd, leaf_drop, leaf_off,
                        out);
 }
 void mrg_wide_launch_part_off(const uint64_t *leaf_off, uint32_t B1r, uint32_t R, uint64_t total, uint64_t *part_off,

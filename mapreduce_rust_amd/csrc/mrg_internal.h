@@ -326,7 +326,7 @@ void mrg_wide_launch_split1(const SortRec *smp, uint32_t S, uint32_t R, uint32_t
 size_t mrg_wide_l1_lds(uint32_t R, uint32_t B1r, uint32_t B1);
 void mrg_wide_launch_l1(const BucketArgs &a, const uint64_t *off, const uint64_t *segptr, uint64_t nseg, uint64_t n,
                         const uint64_t *spl1, uint32_t R, uint32_t B1r, uint32_t *cnt, uint32_t ntiles, uint64_t *out,
-                        uint16_t *bid, bool scatter, hipStream_t s);
+                        uint16_t *bid, uint8_t *ix1, bool scatter, hipStream_t s);
 void mrg_wide_launch_bstart(const uint32_t *cnt, uint32_t B1, uint32_t ntiles, uint64_t n, uint64_t *bstart,
                             hipStream_t s);
 void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstart, const uint64_t *spl1, uint32_t B1,

@@ -715,15 +715,17 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     uint64_t *K1 = pget<uint64_t>(p, 2 * (n + nw) + 2);
     uint64_t *bstart = pget<uint64_t>(p, B1 + 1);
     uint16_t *bid = pget<uint16_t>(p, std::max<uint64_t>(n, 1));   // L1 bucket, then L2 leaf, of each record
+    uint8_t *ix1 = getenv("MRG_TEST_NO_L1IX") ? nullptr : pget<uint8_t>(p, 260ull * R);
     if (n) {
-        mrg_wide_launch_l1(B, om, segptr, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, bid, false, s);
+        mrg_wide_launch_l1(B, om, segptr, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, bid, ix1, false, s);
         mrg_scan_u32(cnt1, cnt1, (uint64_t)B1 * ntiles, st2, s);
-        mrg_wide_launch_l1(B, om, segptr, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, bid, true, s);
+        mrg_wide_launch_l1(B, om, segptr, nsm, n, spl1, R, B1r, cnt1, ntiles, K1, bid, nullptr, true, s);
     } else {
         HIPCHK(hipMemsetAsync(cnt1, 0, 4ull * B1 * ntiles, s));
     }
     mrg_wide_launch_bstart(cnt1, B1, ntiles, n, bstart, s);
     p.put(cnt1); p.put(st2); p.put(cm); p.put(om); p.put(cf); p.put(of); p.put(st1); p.put(segptr);
+    if (ix1) p.put(ix1);
     mark();  // 3: L1
     // ---- L2: leaves inside every L1 bucket
     const uint64_t NL = (uint64_t)B1 * MRG_WIDE_MAXB2;
