@@ -34,6 +34,7 @@ __device__ __forceinline__ GASW T *gw(T *p) {
 constexpr int W_WG = 1024;
 constexpr int W_NW = W_WG / 64;
 constexpr uint32_t W_S2 = 8192;       // L2 samples per L1 bucket (sorted in LDS)
+constexpr uint32_t W_SC = 8192;       // L2 scatter chunk (staged in the samples' LDS)
 constexpr int W_LWG = 256;            // leaf workgroup (four per CU: while one waits on memory, others work)
 constexpr int W_LNW = W_LWG / 64;
 constexpr uint32_t W_SLOTS = 1024;    // leaf LDS table slots
@@ -396,9 +397,12 @@ struct L2Args {
 
 __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     __shared__ uint64_t s_smp[2 * W_S2];            // samples (k0, k1), bitonic-sorted
-    __shared__ uint64_t s_spl[2 * (MRG_WIDE_MAXB2 - 1)];
+    __shared__ uint64_t s_spl[2 * MRG_WIDE_MAXB2];  // (one spare pair: the scatter's leaf ids fill it all)
     __shared__ uint32_t s_cnt[MRG_WIDE_MAXB2];
     __shared__ uint32_t s_cur[MRG_WIDE_MAXB2];
+    __shared__ uint32_t s_bst[MRG_WIDE_MAXB2];      // scatter: a chunk's leaf starts
+    static_assert(W_SC * sizeof(uint64_t) * 2 <= sizeof(s_smp) && W_SC * sizeof(uint16_t) <= sizeof(s_spl),
+                  "the scatter's stage fits the sample and splitter arrays");
     __shared__ uint32_t s_ws[W_NW];
     const uint32_t tid = threadIdx.x, b = blockIdx.x;
     const uint64_t base = L.bstart[b], nb = L.bstart[b + 1] - base;
@@ -496,20 +500,55 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         if (tid == 0) L.nleaf[b] = B2;
     }
     lds_barrier();
-    // ---- scatter
+    // ---- scatter, staged through LDS: a chunk of W_SC records is counting-sorted by leaf in LDS,
+    // then stored so that consecutive threads write consecutive records of one leaf (a run of ~8
+    // records per leaf per chunk instead of one 16-byte store per record at a random place: the
+    // unstaged scatter wrote 2x its bytes to HBM and ran at a fifth of the read passes' rate)
+    constexpr uint32_t SU = W_SC / W_WG;
+    v2 *stg = reinterpret_cast<v2 *>(s_smp);              // the chunk in leaf order (the sample's LDS)
+    uint16_t *stl = reinterpret_cast<uint16_t *>(s_spl);  // its leaves (the splitters' LDS)
     GASW v2 *outv = reinterpret_cast<GASW v2 *>(gw(L.out) + 2 * base);
-    for (uint64_t i0 = tid; i0 < nb; i0 += (uint64_t)U * W_WG) {
-        v2 x[U];
-        uint32_t j[U];
+    for (uint64_t c0 = 0; c0 < nb; c0 += W_SC) {
+        const uint32_t nc = (uint32_t)min<uint64_t>(W_SC, nb - c0);
+        v2 x[SU];
+        uint32_t j[SU], r[SU];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t i = min(i0 + (uint64_t)u * W_WG, (uint64_t)(nb - 1u));
+        for (uint32_t u = 0; u < SU; ++u) {
+            const uint32_t p = tid + u * W_WG;
+            const uint64_t i = c0 + min(p, nc - 1u);
             x[u] = inv[i];
             j[u] = gw(L.sub)[base + i];   // the histogram pass's leaf: no second splitter search
         }
+        if (tid < B2) s_cnt[tid] = 0;
+        lds_barrier();
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (i0 + (uint64_t)u * W_WG < nb) outv[atomicAdd(&s_cur[j[u]], 1u)] = x[u];
+        for (uint32_t u = 0; u < SU; ++u)
+            if (tid + u * W_WG < nc) r[u] = atomicAdd(&s_cnt[j[u]], 1u);
+        lds_barrier();
+        {
+            uint32_t tot;
+            const uint32_t ex = block_scan_excl(tid < B2 ? s_cnt[tid] : 0u, s_ws, &tot);
+            if (tid < B2) s_bst[tid] = ex;
+        }
+        lds_barrier();
+#pragma unroll
+        for (uint32_t u = 0; u < SU; ++u)
+            if (tid + u * W_WG < nc) {
+                const uint32_t p = s_bst[j[u]] + r[u];
+                stg[p] = x[u];
+                stl[p] = (uint16_t)j[u];
+            }
+        lds_barrier();
+#pragma unroll
+        for (uint32_t u = 0; u < SU; ++u) {
+            const uint32_t p = tid + u * W_WG;
+            if (p < nc) {
+                const uint32_t q = stl[p];
+                outv[s_cur[q] + (p - s_bst[q])] = stg[p];
+            }
+        }
+        lds_barrier();
+        if (tid < B2) s_cur[tid] += s_cnt[tid];   // the thread that zeroes s_cnt[tid] next chunk
     }
 }
 

@@ -12,6 +12,6 @@ for v in ${VARIANTS:-lib}; do
   if [ -n "$DEBUG" ]; then
     MRG_DEBUG=1 MRG_LIB=$PWD/mapreduce_rust_amd/$v/libmrgpu.so timeout -k 10 300 python -u bench.py --workload unique \
       --files-per-gpu ${FILES:-50} --steps 2 --warmup 1 --no-cpu-baseline --no-e2e > gpurun_out/ab/c5d.log 2>&1 || exit $?
-    echo "$v debug: $(grep -E 'wide phases|wide:' gpurun_out/ab/c5d.log | tail -2 | tr '\n' ' ')"
+    echo "$v debug: $(grep -E 'wide phases' gpurun_out/ab/c5d.log | tail -1 | tr '\n' ' ')"
   fi
 done
