@@ -821,7 +821,11 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const uint32_t total = (abl & 68u) ? 0u : lane_u32(incl, 63);
             MRG_PT(2);
             uint32_t nslow = 0;
-            const bool may_claim = __builtin_amdgcn_readfirstlane(*(volatile unsigned int *)&s_fill) < (uint32_t)CAP;
+            // an atomic LDS load (ds_read_b32): a volatile read of the same word compiled to a FLAT
+            // load + s_waitcnt vmcnt(0), which made every tile wait for the previous tile's tail stores
+            const bool may_claim =
+                __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+                (uint32_t)CAP;
             my_tokens += (abl & 4u) ? cnt : 0u;
             wave_sync_lds();
 
