@@ -95,6 +95,9 @@ __device__ __forceinline__ const CAS T *cp(const T *p) {
 }
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+// byte-aligned LDS views (the key window read of the token rounds)
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t u32u __attribute__((aligned(1)));
 template <class T>
 __device__ __forceinline__ T g_add(T *p, T v) {
     return __hip_atomic_fetch_add(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -555,9 +558,11 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ uint16_t s_q[NW][QCAP];
     // LUT and length masks first in LDS (highest alignment): their base then fits the 16-bit
     // offset field of ds_read, so a lookup needs no separate address add
-    // ASCII class W | S << 4, one byte per character: the 128 entries are 32 dwords, one per LDS
-    // bank, so a wave's lookups never conflict (lanes reading the same dword share it)
-    __shared__ __attribute__((aligned(1024))) uint8_t s_lut[128];
+    // ASCII class per byte position p of a dword: s_lut[p][c] = (W | S << 4) << p, one byte per
+    // character, so the four lookups of a dword OR straight into its nibble pair (no per-byte shift).
+    // Each table is 128 bytes = 32 dwords, one per LDS bank, and one instruction reads one table: a
+    // wave's lookups never conflict (lanes reading the same dword share it)
+    __shared__ __attribute__((aligned(1024))) uint8_t s_lut[4][128];
     // v_perm selectors per (key length, 1-byte gap position; 16 = none) over the r-aligned window
     __shared__ __attribute__((aligned(16))) uint32_t s_sel[17 * 17][4];
     // workgroup: combine table + tail-region cursors
@@ -597,9 +602,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         s_tot[1] = 0;
         s_fill = 0;
     }
-    if (tid < 128) {
-        const uint32_t c = mrg_uclass((uint32_t)tid);
-        s_lut[tid] = (uint8_t)((c == MRG_CLS_W ? 1u : 0u) | (c == MRG_CLS_S ? 0x10u : 0u));
+    if (tid < 512) {
+        const uint32_t c = mrg_uclass((uint32_t)tid & 127u);
+        s_lut[tid >> 7][tid & 127] = (uint8_t)(((c == MRG_CLS_W ? 1u : 0u) | (c == MRG_CLS_S ? 0x10u : 0u)) << (tid >> 7));
     }
     auto zmask = [](uint32_t L, uint32_t j) {  // word j, byte p (p = 0 least significant) holds key byte 4j + 3 - p
         uint32_t m = 0;
@@ -628,7 +633,6 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     const uint32_t hbits = A.hash_bits;
     GAS uint64_t *const pool = gp(A.pool);
     uint8_t *win = s_win[wv];
-    const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
     uint64_t *mp = s_mp[wv];
     uint16_t *queue = s_q[wv];
     __syncthreads();
@@ -710,19 +714,22 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const uint32_t lo_rel = doc_lo > Ab ? (uint32_t)(doc_lo - Ab) : 0u;
         const uint32_t hi_rel = (uint32_t)umin64(doc_hi - Ab, (uint64_t)(BLK + HALO));
         auto classify = [&](const uint4 &x, uint32_t B) -> uint32_t {
-            // all 16 lookups in flight before the first use (one LDS wait per segment)
+            // all 16 lookups in flight before the first use (one LDS wait per segment); byte b of a
+            // dword reads table b, whose entries are already shifted to bit b (W) and 4 + b (S)
             uint32_t e[16];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint32_t w = k == 0 ? x.x : (k == 1 ? x.y : (k == 2 ? x.z : x.w));
 #pragma unroll
                 for (int b = 0; b < 4; ++b)
-                    e[4 * k + b] = s_lut[b == 0 ? (w & 0x7Fu) : __builtin_amdgcn_ubfe(w, 8 * b, 7)];
+                    e[4 * k + b] = s_lut[b][b == 0 ? (w & 0x7Fu) : __builtin_amdgcn_ubfe(w, 8 * b, 7)];
             }
-            // nibbles: W of bytes 0-3, S of bytes 0-3, W of bytes 4-7, ... (byte i: bit i % 4)
-            uint32_t y = e[0];
+            // nibbles: W of bytes 0-3, S of bytes 0-3, W of bytes 4-7, ... (byte i: bit i % 4):
+            // dword k's byte of y is the OR of its four lookups
+            uint32_t yk[4];
 #pragma unroll
-            for (int i = 1; i < 16; ++i) y |= e[i] << (i + 4 * (i / 4));
+            for (int k = 0; k < 4; ++k) yk[k] = e[4 * k] | e[4 * k + 1] | e[4 * k + 2] | e[4 * k + 3];
+            const uint32_t y = (yk[0] | (yk[1] << 8)) | ((yk[2] | (yk[3] << 8)) << 16);
             const uint32_t t = y & 0x0F0F0F0Fu, u = (y >> 4) & 0x0F0F0F0Fu;
             // bytes 0 and 2 of t | t >> 4: W of bytes 0-7 and 8-15 (u: S)
             const uint32_t m = __builtin_amdgcn_perm(u | (u >> 4), t | (t >> 4), 0x06040200u);  // W16 | S16 << 16
@@ -741,7 +748,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                            e3 = lane_u32(X.e.w, 1);
             const uint32_t k = (uint32_t)lane & 15u;
             const uint32_t dwv = k < 8u ? (k < 4u ? e0 : e1) : (k < 12u ? e2 : e3);
-            const uint32_t cl = s_lut[__builtin_amdgcn_ubfe(dwv, 8u * (k & 3u), 7)];
+            const uint32_t cl = s_lut[0][__builtin_amdgcn_ubfe(dwv, 8u * (k & 3u), 7)];
             const bool in = (uint32_t)BLK + k < hi_rel;  // bytes past the document are White_Space
             const uint32_t wm = (uint32_t)__ballot(lane < 16 && in && (cl & 1u));
             const uint32_t sm = (uint32_t)__ballot(lane < 16 && (!in || (cl & 0x10u)));
@@ -750,7 +757,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const bool n0 = na(X.v0), n1 = na(X.v1), ne = na(X.e);
         // class of the byte before the block (lane 0's e, byte 15)
         const uint32_t prev_blk =
-            Ab > doc_lo ? (uint32_t)(s_lut[(lane_u32(X.e.w, 0) >> 24) & 0x7Fu] >> 4) : 1u;
+            Ab > doc_lo ? (uint32_t)(s_lut[0][(lane_u32(X.e.w, 0) >> 24) & 0x7Fu] >> 4) : 1u;
         MRG_PT(1);
         // the next block's registers are waited for HERE, before this block's tail stores are
         // issued: vmcnt also counts stores, so a wait placed after them would wait for their
@@ -859,11 +866,14 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 uint32_t tlen = one_gap ? span - 1u : span;
                 // key bytes of the window from s + first, big-endian packed, zero padded: output byte p
                 // of word j is key byte 4j + 3 - p (selector r + 3 - p [+ 1 past the gap], 0x0C = zero)
+                // the 17 window bytes from the key's first byte as five dwords: one unaligned 16-byte
+                // LDS read and one 4-byte read (gfx950 runs in unaligned access mode: no dword
+                // alignment, no v_alignbyte), then one selector word per output word
                 const uint32_t off = (uint32_t)BEHIND + s + first;
+                const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
                 const uint32_t dw = off >> 2, r = off & 3u;
                 const uint32_t d0 = win32[dw], d1 = win32[dw + 1], d2 = win32[dw + 2], d3 = win32[dw + 3],
                                d4 = win32[dw + 4];
-                // the window aligned to the key's first byte, then one selector word per output word
                 const u32x4 sl = *reinterpret_cast<const u32x4 *>(s_sel[(fast ? tlen : 0u) * 17u + ga]);
                 const uint32_t a0 = __builtin_amdgcn_alignbyte(d1, d0, r), a1 = __builtin_amdgcn_alignbyte(d2, d1, r),
                                a2 = __builtin_amdgcn_alignbyte(d3, d2, r), a3 = __builtin_amdgcn_alignbyte(d4, d3, r),
