@@ -286,21 +286,30 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl1(L1Args L) {
             if (x < shi) s_ptr[x - slo] = L.segptr[x];
         }
     lds_barrier();
-    // U records per thread per round: their loads are all in flight before the first is used
+    // U records per thread per round: their loads are all in flight before the first is used.
+    // A thread visits its records in increasing order, so it keeps its segment (first record, end,
+    // base address) in registers and only steps to the next segment when a record crosses its end:
+    // no per-record search (three dependent LDS reads before every load).
     constexpr int U = 4;
+    auto seg_off = [&](uint64_t x) -> uint64_t { return cached ? s_off[x - slo] : L.off[x]; };
+    auto seg_ptr = [&](uint64_t x) -> const GASW uint64_t * {
+        return reinterpret_cast<const GASW uint64_t *>(cached ? s_ptr[x - slo] : L.segptr[x]);
+    };
+    uint64_t sg = seg_find(seg_off, slo, shi, min(t0 + tid, t1 - 1u));
+    uint64_t seg_lo = seg_off(sg), seg_hi = seg_off(sg + 1);
+    const GASW uint64_t *seg_p = seg_ptr(sg);
     for (uint64_t base = t0 + tid; base < t1; base += (uint64_t)U * W_WG) {
         uint64_t k0[U], k1[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t i = min(base + (uint64_t)u * W_WG, t1 - 1u);  // past the tile: a repeat, unused
-            const GASW uint64_t *rp;
-            if (cached) {
-                const uint64_t sg = seg_find([&](uint64_t x) { return s_off[x - slo]; }, slo, shi, i);
-                rp = reinterpret_cast<const GASW uint64_t *>(s_ptr[sg - slo]) + 2 * (i - s_off[sg - slo]);
-            } else {
-                const uint64_t sg = seg_find([&](uint64_t x) { return L.off[x]; }, slo, shi, i);
-                rp = reinterpret_cast<const GASW uint64_t *>(L.segptr[sg]) + 2 * (i - L.off[sg]);
+            while (i >= seg_hi) {  // rare: the next non-empty segment
+                ++sg;
+                seg_lo = seg_hi;
+                seg_hi = seg_off(sg + 1);
+                seg_p = seg_ptr(sg);
             }
+            const GASW uint64_t *rp = seg_p + 2 * (i - seg_lo);
             typedef uint64_t v2 __attribute__((ext_vector_type(2)));
             const v2 x = *reinterpret_cast<const GASW v2 *>(rp);
             k0[u] = x.x;
