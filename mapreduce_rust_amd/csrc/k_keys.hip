@@ -84,13 +84,20 @@ struct alignas(16) BaKey {
 // Add c to key (a, b[, d]).  Slots fill monotonically (k0, then k1, then doc, each by CAS from its
 // empty value), so a slot whose fields all equal the key is the key's slot for good: the common case
 // is one 16-byte read and one add.  A partly claimed slot is resolved by the CAS protocol.
+// first probe slot of hash h: 16 hash bits below the bucket bits scaled to [0, CAP)
+template <bool IDX, bool C32>
+__device__ __forceinline__ uint32_t ba_slot(uint32_t h) {
+    return (((h >> (32 - MRG_NBUCKET_LOG2 - 16)) & 0xFFFFu) * ba_cap<IDX, C32>()) >> 16;
+}
+
+// first: the key of the first probe slot, read by the caller (possibly before other adds: a stale
+// EMPTY is resolved by the CAS protocol below, and a filled slot never changes)
 template <bool IDX, bool C32, class CT>
-__device__ __forceinline__ bool ba_add(BaKey *key, CT *cnt, unsigned int *doc, uint64_t a,
-                                       uint64_t b, uint32_t d, uint64_t c, uint32_t h) {
+__device__ __forceinline__ bool ba_add_from(BaKey *key, CT *cnt, unsigned int *doc, uint64_t a,
+                                            uint64_t b, uint32_t d, uint64_t c, uint32_t h, BaKey first) {
     constexpr uint32_t CAP = ba_cap<IDX, C32>();
-    // 16 hash bits below the bucket bits scaled to [0, CAP)
-    uint32_t slot = (((h >> (32 - MRG_NBUCKET_LOG2 - 16)) & 0xFFFFu) * CAP) >> 16;
-    BaKey kn = key[slot];
+    uint32_t slot = ba_slot<IDX, C32>(h);
+    BaKey kn = first;
     for (int p = 0; p < BA_PROBE; ++p) {
         const BaKey k = kn;
         // the next probe slot's key is read now, beside this one's processing (a stale EMPTY there is
@@ -123,6 +130,12 @@ __device__ __forceinline__ bool ba_add(BaKey *key, CT *cnt, unsigned int *doc, u
         slot = nxt;
     }
     return false;
+}
+
+template <bool IDX, bool C32, class CT>
+__device__ __forceinline__ bool ba_add(BaKey *key, CT *cnt, unsigned int *doc, uint64_t a,
+                                       uint64_t b, uint32_t d, uint64_t c, uint32_t h) {
+    return ba_add_from<IDX, C32>(key, cnt, doc, a, b, d, c, h, key[ba_slot<IDX, C32>(h)]);
 }
 
 template <bool IDX, bool C32>
@@ -214,20 +227,34 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
             for (int k = 0; k < BA_U; ++k) asm volatile("" : "+v"(X.d[k]));
     };
     uint64_t abl_acc = 0;  // MRG_AGG_ABLATE (timing only): what the skipped work would have consumed
+    // records of a chunk: every hash first, then record k + 1's first probe slot is read while
+    // record k is added, so the probe chains of neighbouring records overlap by one LDS round trip
     auto sum_chunk = [&](uint32_t r, uint32_t off, const Chunk &X) {
         const uint32_t n = s_rn[r];
+        if (A.ablate) {
+#pragma unroll
+            for (int k = 0; k < BA_U; ++k) {
+                const bool ok = off + 64u * k + (uint32_t)lane < n;
+                const uint64_t a = X.k[k].x, c = X.k[k].y;
+                const uint32_t d = IDX ? X.d[k] : MRG_EMPTY_DOC;
+                abl_acc += ok ? ((A.ablate & 2u) ? (a ^ c) : (uint64_t)ba_hash(a, c, d, A.hash_bits)) : 0u;
+            }
+            return;
+        }
+        uint32_t hk[BA_U];
+#pragma unroll
+        for (int k = 0; k < BA_U; ++k) hk[k] = ba_hash(X.k[k].x, X.k[k].y, IDX ? X.d[k] : MRG_EMPTY_DOC, A.hash_bits);
+        BaKey pre = s_key[ba_slot<IDX, C32>(hk[0])];
 #pragma unroll
         for (int k = 0; k < BA_U; ++k) {
             const bool ok = off + 64u * k + (uint32_t)lane < n;
             const uint64_t a = X.k[k].x, c = X.k[k].y;
             const uint32_t d = IDX ? X.d[k] : MRG_EMPTY_DOC;
-            if (A.ablate) {
-                abl_acc += ok ? ((A.ablate & 2u) ? (a ^ c) : (uint64_t)ba_hash(a, c, d, A.hash_bits)) : 0u;
-                continue;
-            }
+            const BaKey first = pre;
+            if (k + 1 < BA_U) pre = s_key[ba_slot<IDX, C32>(hk[k + 1 < BA_U ? k + 1 : k])];
             bool ovf = false;
-            const uint32_t h = ba_hash(a, c, d, A.hash_bits);
-            if (ok && mine(h)) ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, a, c, d, 1ull, h);
+            const uint32_t h = hk[k];
+            if (ok && mine(h)) ovf = !ba_add_from<IDX, C32>(s_key, s_cnt, s_doc, a, c, d, 1ull, h, first);
             if (__any(ovf)) overflow(ovf, a, c, d, 1);
         }
     };
