@@ -587,6 +587,8 @@ struct LeafArgs {
     unsigned long long *prof;  // MRG_WIDE_PROF builds: phase clocks
     uint32_t *big_list;      // leaves the one-wave kernel passes to the workgroup kernel
     unsigned long long *big_n;
+    uint32_t *leaf_pk;       // 1: the leaf's counts sit in the low word of its key slots (no ocnt entry)
+    uint32_t pack;           // packing allowed (every count fits 32 bits)
 };
 
 // first weighted key >= (p, a, b)
@@ -1258,6 +1260,16 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
             ++npass;
             continue;
         }
+        // Packed leaf: when every key of the leaf is at most 12 bytes (the low word of k1 is zero
+        // padding) and counts fit 32 bits, a count is stored in that low word of its key slot and
+        // no count array entry is written (the line writer reads 16 bytes per line instead of 24)
+        bool pk = false;
+        {
+            uint32_t lw = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < W_VIPL; ++k) lw |= (uint32_t)key[k].y;   // padding items are zero
+            pk = L.pack && !__any(lw != 0u);
+        }
         const v2 f = v2{__shfl(key[0].x, 0), __shfl(key[0].y, 0)};   // item 0 (a member if NT > 0)
         uint64_t o0 = 0, o1 = 0;
 #pragma unroll
@@ -1280,8 +1292,12 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
                 D = 1;
                 my_ll = line_len(f.x, f.y, n);
                 if (lane == 0) {
-                    ko[0] = f;
-                    co[0] = n;
+                    if (pk) {
+                        ko[0] = v2{f.x, f.y | n};
+                    } else {
+                        ko[0] = f;
+                        co[0] = n;
+                    }
                     my_last = 0;
                     bytes = my_ll;
                 }
@@ -1433,8 +1449,12 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
                             n += s_cb[s2];
                         }
                     }
-                    ko[dpos] = x;
-                    co[dpos] = n;
+                    if (pk) {
+                        ko[dpos] = v2{x.x, x.y | n};
+                    } else {
+                        ko[dpos] = x;
+                        co[dpos] = n;
+                    }
                     my_ll = line_len(x.x, x.y, n);
                     bytes += my_ll;
                     my_last = dpos;
@@ -1448,6 +1468,7 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
             L.leaf_out[lid] = out0;
             L.leaf_nd[lid] = D;
             L.leaf_bytes[lid] = bytes;
+            L.leaf_pk[lid] = pk ? 1u : 0u;
             if (D == 0) L.leaf_last[lid] = 0;
         }
         keys += D;
@@ -1541,13 +1562,13 @@ __device__ __forceinline__ uint32_t line_words(uint64_t k0, uint64_t k1, uint64_
     return L + 2u + nd;
 }
 
-__global__ __launch_bounds__(W_WWG) void k_wwrite(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *nleaf,
-                                                    const uint64_t *leaf_out, const uint32_t *leaf_nd,
-                                                    const uint32_t *leaf_drop, const uint64_t *leaf_off,
-                                                    uint8_t *out) {
+__global__ __launch_bounds__(W_WWG) void k_wwrite(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *leaf_pk,
+                                                    const uint32_t *nleaf, const uint64_t *leaf_out,
+                                                    const uint32_t *leaf_nd, const uint32_t *leaf_drop,
+                                                    const uint64_t *leaf_off, uint8_t *out) {
     __shared__ uint32_t s_buf[W_STAGE / 4];
     __shared__ uint32_t s_kst[MRG_WIDE_MAXB2 + 1];   // keys before leaf l (this bucket)
-    __shared__ uint64_t s_lout[MRG_WIDE_MAXB2];
+    __shared__ uint64_t s_lout[MRG_WIDE_MAXB2];      // first key slot of leaf l; bit 63: counts packed
     __shared__ uint32_t s_ws[W_WWG / 64];
     const uint8_t *sb = reinterpret_cast<const uint8_t *>(s_buf);
     const uint32_t tid = threadIdx.x, b = blockIdx.x;
@@ -1560,7 +1581,7 @@ __global__ __launch_bounds__(W_WWG) void k_wwrite(const uint64_t *keys, const ui
         for (uint32_t x = 0; x < PT; ++x) {
             const uint32_t l = tid * PT + x;
             v[x] = l < nl ? leaf_nd[l0 + l] - (leaf_drop[l0 + l] ? 1u : 0u) : 0u;
-            if (l < nl) s_lout[l] = leaf_out[l0 + l];
+            if (l < nl) s_lout[l] = leaf_out[l0 + l] | ((uint64_t)(leaf_pk[l0 + l] != 0u) << 63);
             sum += v[x];
         }
         uint32_t tot;
@@ -1590,10 +1611,16 @@ __global__ __launch_bounds__(W_WWG) void k_wwrite(const uint64_t *keys, const ui
                 if (s_kst[mid] <= i) lo = mid;
                 else hi = mid;
             }
-            const uint64_t slot = s_lout[lo] + (i - s_kst[lo]);
+            const uint64_t lo_out = s_lout[lo];
+            const uint64_t slot = (lo_out & ~(1ull << 63)) + (i - s_kst[lo]);
             F.a = keys[2 * slot];
             F.c = keys[2 * slot + 1];
-            F.n = ocnt[slot];
+            if (lo_out >> 63) {   // packed leaf: the count is the low word of k1
+                F.n = F.c & 0xFFFFFFFFull;
+                F.c &= ~0xFFFFFFFFull;
+            } else {
+                F.n = ocnt[slot];
+            }
         }
     };
     One cur, nxt;
@@ -1644,18 +1671,20 @@ __global__ void k_wpart_off(const uint64_t *leaf_off, uint32_t B1r, uint32_t R, 
 }
 
 // dense KeySet (for consumers other than the line writer): leaf l's keys go to dense_off[l] ..
-__global__ __launch_bounds__(256) void k_wdense(const uint64_t *keys, const uint64_t *ocnt, const uint64_t *leaf_out,
-                                                const uint32_t *leaf_nd, const uint32_t *dense_off, uint32_t B1r,
-                                                KeySet ks) {
+__global__ __launch_bounds__(256) void k_wdense(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *leaf_pk,
+                                                const uint64_t *leaf_out, const uint32_t *leaf_nd,
+                                                const uint32_t *dense_off, uint32_t B1r, KeySet ks) {
     const uint64_t lid = blockIdx.x;
     const uint32_t D = leaf_nd[lid];
     const uint64_t o0 = leaf_out[lid], d0 = dense_off[lid];
+    const bool pk = leaf_pk[lid] != 0u;
     const uint32_t part = (uint32_t)(lid / MRG_WIDE_MAXB2) / B1r;
     for (uint32_t p = threadIdx.x; p < D; p += blockDim.x) {
-        const uint64_t a = keys[2 * (o0 + p)], c = keys[2 * (o0 + p) + 1];
+        const uint64_t a = keys[2 * (o0 + p)], cw = keys[2 * (o0 + p) + 1];
+        const uint64_t c = pk ? cw & ~0xFFFFFFFFull : cw;
         ks.k0[d0 + p] = a;
         ks.k1[d0 + p] = c;
-        ks.cnt[d0 + p] = ocnt[o0 + p];
+        ks.cnt[d0 + p] = pk ? (cw & 0xFFFFFFFFull) : ocnt[o0 + p];
         ks.len[d0 + p] = mrg_short_len(a, c);
         ks.part[d0 + p] = part;
         ks.doc[d0 + p] = MRG_EMPTY_DOC;
@@ -1832,7 +1861,7 @@ void mrg_wide_launch_weights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *
 void mrg_wide_launch_leaf(const WideLeafArgs &w, uint32_t B1, hipStream_t s) {
     LeafArgs L{w.kin, w.kout, w.bstart, w.nleaf, w.leaf_lo, w.leaf_lb, w.B1r, w.R, w.wk0, w.wk1, w.wcnt, w.wpart, w.nw,
                w.maxd ? min(w.maxd, W_MAXD) : W_MAXD, w.ocnt, w.leaf_out, w.leaf_nd, w.leaf_bytes, w.leaf_last, w.ovf_list,
-               w.ovf_n, w.nkeys, w.wr, w.prof, w.big_list, w.big_n};
+               w.ovf_n, w.nkeys, w.wr, w.prof, w.big_list, w.big_n, w.leaf_pk, w.pack};
     hipLaunchKernelGGL(k_wranges, gridw((uint64_t)B1 * MRG_WIDE_MAXB2), dim3(256), 0, s, L, B1);
     hipLaunchKernelGGL(k_wleafw, dim3(B1 * W_VQ), dim3(64), 0, s, L);
     // the passed-on leaves: a fixed grid loops over the list (its length is read on the device)
@@ -1842,7 +1871,7 @@ void mrg_wide_launch_fallback(const WideLeafArgs &w, const uint32_t *list, uint3
                               hipStream_t s) {
     LeafArgs L{w.kin, w.kout, w.bstart, w.nleaf, w.leaf_lo, w.leaf_lb, w.B1r, w.R, w.wk0, w.wk1, w.wcnt, w.wpart, w.nw,
                w.maxd ? min(w.maxd, W_MAXD) : W_MAXD, w.ocnt, w.leaf_out, w.leaf_nd, w.leaf_bytes, w.leaf_last, w.ovf_list,
-               w.ovf_n, w.nkeys, w.wr, w.prof, w.big_list, w.big_n};
+               w.ovf_n, w.nkeys, w.wr, w.prof, w.big_list, w.big_n, w.leaf_pk, w.pack};
     uint64_t *wrange = (uint64_t *)pool.get(16ull * nlist);
     uint64_t *cnt = (uint64_t *)pool.get(8ull * (nlist + 1)), *off = (uint64_t *)pool.get(8ull * (nlist + 1));
     uint64_t *scantmp = (uint64_t *)pool.get(8ull * mrg_scan_tmp_elems(nlist + 1));
@@ -1890,18 +1919,19 @@ void mrg_wide_launch_drop(const uint32_t *nleaf, uint32_t B1r, uint32_t R, const
                           const uint32_t *leaf_last, uint32_t *leaf_drop, hipStream_t s) {
     hipLaunchKernelGGL(k_wdrop, gridw(R), dim3(256), 0, s, nleaf, B1r, R, leaf_nd, leaf_bytes, leaf_last, leaf_drop);
 }
-void mrg_wide_launch_write(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *nleaf, const uint64_t *leaf_out,
-                           const uint32_t *leaf_nd, const uint32_t *leaf_drop, const uint64_t *leaf_off, uint32_t B1,
-                           uint8_t *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_wwrite, dim3(B1), dim3(W_WWG), 0, s, keys, ocnt, nleaf, leaf_out, leaf_nd, leaf_drop, leaf_off,
-                       out);
+void mrg_wide_launch_write(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *leaf_pk, const uint32_t *nleaf,
+                           const uint64_t *leaf_out, const uint32_t *leaf_nd, const uint32_t *leaf_drop,
+                           const uint64_t *leaf_off, uint32_t B1, uint8_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_wwrite, dim3(B1), dim3(W_WWG), 0, s, keys, ocnt, leaf_pk, nleaf, leaf_out, leaf_nd, leaf_drop,
+                       leaf_off, out);
 }
 void mrg_wide_launch_part_off(const uint64_t *leaf_off, uint32_t B1r, uint32_t R, uint64_t total, uint64_t *part_off,
                               hipStream_t s) {
     hipLaunchKernelGGL(k_wpart_off, gridw(R + 1), dim3(256), 0, s, leaf_off, B1r, R, total, part_off);
 }
-void mrg_wide_launch_dense(const uint64_t *keys, const uint64_t *ocnt, const uint64_t *leaf_out, const uint32_t *leaf_nd,
-                           const uint32_t *dense_off, uint32_t B1, uint32_t B1r, KeySet ks, hipStream_t s) {
-    hipLaunchKernelGGL(k_wdense, dim3(B1 * MRG_WIDE_MAXB2), dim3(256), 0, s, keys, ocnt, leaf_out, leaf_nd, dense_off,
-                       B1r, ks);
+void mrg_wide_launch_dense(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *leaf_pk, const uint64_t *leaf_out,
+                           const uint32_t *leaf_nd, const uint32_t *dense_off, uint32_t B1, uint32_t B1r, KeySet ks,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(k_wdense, dim3(B1 * MRG_WIDE_MAXB2), dim3(256), 0, s, keys, ocnt, leaf_pk, leaf_out, leaf_nd,
+                       dense_off, B1r, ks);
 }

@@ -315,6 +315,8 @@ struct WideLeafArgs {
     unsigned long long *prof;    // diagnostics (builds with -DMRG_WIDE_PROF): leaf phase clocks [8]
     uint32_t *big_list;          // [B1 * MRG_WIDE_MAXB2] leaves passed from the one-wave to the workgroup kernel
     unsigned long long *big_n;   // their count (zeroed by the caller)
+    uint32_t *leaf_pk;           // [B1 * MRG_WIDE_MAXB2] 1: the leaf's counts are packed into its key slots (zeroed by the caller)
+    uint32_t pack;               // packing allowed: every count fits 32 bits (fewer than 2^32 tokens)
 };
 void mrg_wide_launch_counts(const BucketArgs &a, uint64_t *cnt_main, uint64_t *segptr, uint64_t *cnt_flush,
                             hipStream_t s);
@@ -339,13 +341,14 @@ void mrg_wide_launch_fallback(const WideLeafArgs &w, const uint32_t *list, uint3
                               hipStream_t s);
 void mrg_wide_launch_drop(const uint32_t *nleaf, uint32_t B1r, uint32_t R, const uint32_t *leaf_nd, uint64_t *leaf_bytes,
                           const uint32_t *leaf_last, uint32_t *leaf_drop, hipStream_t s);
-void mrg_wide_launch_write(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *nleaf, const uint64_t *leaf_out,
-                           const uint32_t *leaf_nd, const uint32_t *leaf_drop, const uint64_t *leaf_off, uint32_t B1,
-                           uint8_t *out, hipStream_t s);
+void mrg_wide_launch_write(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *leaf_pk, const uint32_t *nleaf,
+                           const uint64_t *leaf_out, const uint32_t *leaf_nd, const uint32_t *leaf_drop,
+                           const uint64_t *leaf_off, uint32_t B1, uint8_t *out, hipStream_t s);
 void mrg_wide_launch_part_off(const uint64_t *leaf_off, uint32_t B1r, uint32_t R, uint64_t total, uint64_t *part_off,
                               hipStream_t s);
-void mrg_wide_launch_dense(const uint64_t *keys, const uint64_t *ocnt, const uint64_t *leaf_out, const uint32_t *leaf_nd,
-                           const uint32_t *dense_off, uint32_t B1, uint32_t B1r, KeySet ks, hipStream_t s);
+void mrg_wide_launch_dense(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *leaf_pk, const uint64_t *leaf_out,
+                           const uint32_t *leaf_nd, const uint32_t *dense_off, uint32_t B1, uint32_t B1r, KeySet ks,
+                           hipStream_t s);
 
 // ---- k_gen.hip
 int mrg_gen_zipf_impl(uint8_t *dst, uint64_t n, uint64_t seed, uint64_t file_index, uint32_t vocab, double s,

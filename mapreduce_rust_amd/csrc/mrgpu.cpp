@@ -172,11 +172,12 @@ struct WideRes {
     bool ready = false;
     uint32_t B1 = 0, B1r = 0;
     uint64_t *kout = nullptr, *ocnt = nullptr;
-    uint32_t *nleaf = nullptr, *leaf_nd = nullptr, *leaf_last = nullptr;
+    uint32_t *nleaf = nullptr, *leaf_nd = nullptr, *leaf_last = nullptr, *leaf_pk = nullptr;
     uint64_t *leaf_out = nullptr, *leaf_bytes = nullptr;
     uint64_t distinct = 0;
     void release(Pool &p) {
         p.put(kout); p.put(ocnt); p.put(nleaf); p.put(leaf_nd); p.put(leaf_last); p.put(leaf_out); p.put(leaf_bytes);
+        p.put(leaf_pk);
         *this = WideRes{};
     }
 };
@@ -597,7 +598,7 @@ void wide_densify(mrg_ctx *c, uint64_t extra) {
     uint32_t *tmp = pget<uint32_t>(p, mrg_scan_tmp_elems(nl + 1));
     mrg_scan_u32(w.leaf_nd, doff, nl, tmp, s);
     keys_reserve(c, w.distinct + extra + 1);
-    mrg_wide_launch_dense(w.kout, w.ocnt, w.leaf_out, w.leaf_nd, doff, w.B1, w.B1r, c->keys.ks, s);
+    mrg_wide_launch_dense(w.kout, w.ocnt, w.leaf_pk, w.leaf_out, w.leaf_nd, doff, w.B1, w.B1r, c->keys.ks, s);
     HIPCHK(hipMemcpyAsync(&c->d_cnt[CNT_KEYS], &w.distinct, 8, hipMemcpyHostToDevice, s));
     sync(c);
     p.put(doff);
@@ -748,6 +749,8 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     w.leaf_nd = pget<uint32_t>(p, NL + 1);
     w.leaf_bytes = pget<uint64_t>(p, NL + 1);
     w.leaf_last = pget<uint32_t>(p, NL);
+    w.leaf_pk = pget<uint32_t>(p, NL);
+    HIPCHK(hipMemsetAsync(w.leaf_pk, 0, 4 * NL, s));
     HIPCHK(hipMemsetAsync(w.leaf_nd, 0, 4 * (NL + 1), s));
     HIPCHK(hipMemsetAsync(w.leaf_bytes, 0, 8 * (NL + 1), s));
     uint32_t *ovf_list = pget<uint32_t>(p, NL);
@@ -764,6 +767,10 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     HIPCHK(hipMemsetAsync(L.prof, 0, 64, s));
     L.big_list = pget<uint32_t>(p, NL);
     L.big_n = pget<unsigned long long>(p, 1);
+    L.leaf_pk = w.leaf_pk;
+    // counts packed into the key slots of leaves whose keys are <= 12 bytes: every count fits 32 bits
+    // when the job has fewer than 2^32 tokens (MRG_TEST_NO_PACK: the unpacked layout everywhere)
+    L.pack = (c->h_cnt[CNT_TOKENS] < 0xFFFFFFFFull && !getenv("MRG_TEST_NO_PACK")) ? 1u : 0u;
     HIPCHK(hipMemsetAsync(L.big_n, 0, 8, s));
     mrg_wide_launch_leaf(L, B1, s);
     mark();  // 5: leaves
@@ -1176,7 +1183,7 @@ void wide_reduce(mrg_ctx *c) {
         c->out_cap = total + 16;
         c->d_out = pget<uint8_t>(p, c->out_cap);
     }
-    mrg_wide_launch_write(w.kout, w.ocnt, w.nleaf, w.leaf_out, w.leaf_nd, drop, off, w.B1, c->d_out, s);
+    mrg_wide_launch_write(w.kout, w.ocnt, w.leaf_pk, w.nleaf, w.leaf_out, w.leaf_nd, drop, off, w.B1, c->d_out, s);
     uint64_t *poff = pget<uint64_t>(p, c->R + 1);
     mrg_wide_launch_part_off(off, w.B1r, c->R, total, poff, s);
     c->part_off.assign(c->R + 1, 0);
