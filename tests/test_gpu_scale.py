@@ -109,7 +109,8 @@ def test_c5_slice_vs_oracle(ctx):
 @pytest.fixture
 def knobs():
     keys = ["MRG_TEST_TAIL_CAP", "MRG_TEST_OVF_CAP", "MRG_TEST_AGG_OCAP", "MRG_WIDE", "MRG_TEST_LEAF_CAP",
-            "MRG_TEST_LEAF_TARGET", "MRG_TEST_SORT_LCAP", "MRG_TEST_AGG_WIDE_OVF", "MRG_TEST_AGG_NSUB"]
+            "MRG_TEST_LEAF_TARGET", "MRG_TEST_SORT_LCAP", "MRG_TEST_AGG_WIDE_OVF", "MRG_TEST_AGG_NSUB",
+            "MRG_TEST_NO_PACK"]
     saved = {k: os.environ.get(k) for k in keys}
 
     def set_(**kw):
@@ -364,6 +365,33 @@ def test_wide_sample_sort_knobs_vs_oracle(ctx, corpus, knobs, cap, target):
         assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST), (len(docs), R)
     if cap == "8":
         assert ctx.stats()["overflow_keys"] > 0   # leaves finished by the fallback
+
+
+@pytest.mark.parametrize("nopack", ["0", "1"])
+def test_wide_packed_counts_vs_oracle(ctx, knobs, nopack):
+    """One-wave leaves whose keys are all <= 12 bytes store their counts in the key slots' low word
+    (k_wide.hip, packed leaves); leaves holding a 13..16-byte key, workgroup and fallback leaves keep
+    the count array.  Near-unique 12-byte keys with 13..16-byte words and repeated keys mixed in,
+    packed and (MRG_TEST_NO_PACK) unpacked, through the line writer and through the dense key set
+    (final.txt), against the oracle."""
+    import torch
+    import oracle_lib as O
+    from gpu_util import run_wc
+    n = 4 * MIB
+    t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
+    ctx.gen_unique(t.data_ptr(), n, 0xC5, 13)
+    uniq = t[:n].cpu().numpy().tobytes()
+    longw = b" ".join(b"w%013d" % i + b"q" * (i % 3) for i in range(20000))  # 14..16-byte keys
+    reps = b" ".join([b"repeated"] * 5000 + [b"twelvecharsx"] * 3000)
+    knobs(MRG_WIDE=1, MRG_TEST_NO_PACK=nopack)
+    for docs, R in (([uniq], 16), ([uniq[: 2 * MIB], longw, reps], 7), ([reps, uniq[:MIB]], 1)):
+        assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST), (len(docs), R)
+    # the dense key set made from the leaves (final.txt, built on the device from the job's keys):
+    # LC_ALL=C sort of every mr-{r}.txt line (src/run.sh:16-20)
+    docs = [uniq[:MIB], longw, reps]
+    outs = run_wc(ctx, docs, 5)
+    assert outs == O.wc(docs, 5, O.FAST)
+    assert ctx.final() == b"".join(l + b"\n" for l in sorted(l for o in outs for l in o.split(b"\n") if l))
 
 
 def test_wide_many_partitions_vs_oracle(ctx, knobs):
