@@ -81,15 +81,15 @@ struct alignas(16) BaKey {
     unsigned long long a, b;
 };
 
-// Add c to key (a, b[, d]).  Slots fill monotonically (k0, then k1, then doc, each by CAS from its
-// empty value), so a slot whose fields all equal the key is the key's slot for good: the common case
-// is one 16-byte read and one add.  A partly claimed slot is resolved by the CAS protocol.
 // first probe slot of hash h: 16 hash bits below the bucket bits scaled to [0, CAP)
 template <bool IDX, bool C32>
 __device__ __forceinline__ uint32_t ba_slot(uint32_t h) {
     return (((h >> (32 - MRG_NBUCKET_LOG2 - 16)) & 0xFFFFu) * ba_cap<IDX, C32>()) >> 16;
 }
 
+// Add c to key (a, b[, d]).  Slots fill monotonically (k0, then k1, then doc, each by CAS from its
+// empty value), so a slot whose fields all equal the key is the key's slot for good: the common case
+// is one 16-byte read and one add.  A partly claimed slot is resolved by the CAS protocol.
 // first: the key of the first probe slot, read by the caller (possibly before other adds: a stale
 // EMPTY is resolved by the CAS protocol below, and a filled slot never changes)
 template <bool IDX, bool C32, class CT>
