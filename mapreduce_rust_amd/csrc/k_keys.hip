@@ -52,16 +52,21 @@ __device__ __forceinline__ uint64_t wg_append(unsigned long long *counter, bool 
 // current one is summed, and a record that finds its key costs one 16-byte LDS read + one LDS add.
 constexpr int BA_WG = 1024;
 constexpr int BA_NW = BA_WG / 64;
-// LDS table slots per bucket: wc with 32-bit counts (the job has fewer than 2^32 tokens) 7424
-// (16-byte key + 4-byte count: 145 KiB), wc with 64-bit counts 6112 (143 KiB), the indexer 4096
-// (+ 4-byte doc); the rest of the LDS holds the per-region record counts and chunk offsets.  About
-// half the slots stay free at 2^20 distinct keys over 256 buckets.
+// LDS table slots per bucket: wc with 32-bit counts (the job has fewer than 2^32 tokens) 6912
+// (16-byte key + 4-byte count: 135 KiB, beside 16 KiB of miss queues), wc with 64-bit counts 6112
+// (143 KiB), the indexer 4096 (+ 4-byte doc); the rest of the LDS holds the per-region record counts
+// and chunk offsets.  More than half the slots stay free at 2^20 distinct keys over 256 buckets.
 template <bool IDX, bool C32>
-constexpr uint32_t ba_cap() { return IDX ? 4096u : (C32 ? 7424u : 6112u); }
+constexpr uint32_t ba_cap() { return IDX ? 4096u : (C32 ? 6912u : 6112u); }
 constexpr int BA_PROBE = 64;
 constexpr int BA_U = 8;            // records per lane per chunk
 template <bool C32>
-constexpr int ba_maxreg() { return C32 ? 1024 : 2048; }  // map workgroups (regions) the size table holds
+constexpr int ba_maxreg() { return C32 ? 512 : 2048; }  // map workgroups (regions) the size table holds
+// wc with 32-bit counts: records whose first probe misses wait in a per-wave LDS queue of BA_QN and are
+// probed a (nearly) full wave at a time
+constexpr uint32_t BA_QN = 64;
+template <bool IDX, bool C32>
+constexpr bool ba_queue() { return !IDX && C32; }
 
 #define GASK __attribute__((address_space(1)))
 template <class T>
@@ -147,6 +152,7 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
     __shared__ unsigned int s_doc[IDX ? BA_CAP : 1];
     __shared__ uint32_t s_rn[ba_maxreg<C32>()];      // tail records of region r in this bucket
     __shared__ uint32_t s_cs[ba_maxreg<C32>() + 1];  // first chunk of region r (chunks numbered region by region)
+    __shared__ BaKey s_mq[ba_queue<IDX, C32>() ? BA_NW : 1][ba_queue<IDX, C32>() ? BA_QN : 1];  // miss queues
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int i = tid; i < (int)BA_CAP; i += BA_WG) {
@@ -227,6 +233,19 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
             for (int k = 0; k < BA_U; ++k) asm volatile("" : "+v"(X.d[k]));
     };
     uint64_t abl_acc = 0;  // MRG_AGG_ABLATE (timing only): what the skipped work would have consumed
+    uint32_t qn = 0;       // records in this wave's miss queue (wave-uniform)
+    auto drain = [&]() {   // the queued records, one per lane, through the full probe
+        if (!ba_queue<IDX, C32>() || qn == 0) return;
+        const bool act = (uint32_t)lane < qn;
+        const BaKey r = s_mq[ba_queue<IDX, C32>() ? wv : 0][act ? lane : 0];
+        bool ovf = false;
+        if (act) {
+            const uint32_t h = ba_hash(r.a, r.b, MRG_EMPTY_DOC, A.hash_bits);
+            ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, r.a, r.b, MRG_EMPTY_DOC, 1ull, h);
+        }
+        if (__any(ovf)) overflow(ovf, r.a, r.b, MRG_EMPTY_DOC, 1);
+        qn = 0;
+    };
     // records of a chunk: every hash first, then record k + 1's first probe slot is read while
     // record k is added, so the probe chains of neighbouring records overlap by one LDS round trip
     auto sum_chunk = [&](uint32_t r, uint32_t off, const Chunk &X) {
@@ -245,6 +264,30 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
 #pragma unroll
         for (int k = 0; k < BA_U; ++k) hk[k] = ba_hash(X.k[k].x, X.k[k].y, IDX ? X.d[k] : MRG_EMPTY_DOC, A.hash_bits);
         BaKey pre = s_key[ba_slot<IDX, C32>(hk[0])];
+        if constexpr (ba_queue<IDX, C32>()) {
+            // first probe here (the key sits in its first slot: add); every other record joins the
+            // wave's miss queue, which is probed when the next batch would overflow it
+#pragma unroll
+            for (int k = 0; k < BA_U; ++k) {
+                const bool ok = off + 64u * k + (uint32_t)lane < n;
+                const uint64_t a = X.k[k].x, c = X.k[k].y;
+                const BaKey first = pre;
+                if (k + 1 < BA_U) pre = s_key[ba_slot<IDX, C32>(hk[k + 1 < BA_U ? k + 1 : k])];
+                const uint32_t h = hk[k];
+                const bool me = ok && mine(h);
+                const bool hit = me && first.a == a && first.b == c;
+                if (hit) atomicAdd(&s_cnt[ba_slot<IDX, C32>(h)], (CT)1);
+                const bool miss = me && !hit;
+                const uint64_t mm = __ballot(miss);
+                if (mm) {
+                    const uint32_t m = (uint32_t)__builtin_popcountll(mm);
+                    if (qn + m > BA_QN) drain();
+                    if (miss) s_mq[wv][qn + (uint32_t)__builtin_popcountll(mm & mrg_lanemask_lt())] = BaKey{a, c};
+                    qn += m;
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < BA_U; ++k) {
             const bool ok = off + 64u * k + (uint32_t)lane < n;
@@ -282,6 +325,7 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
             sum_chunk(rB, oB, XB);
         }
     }
+    drain();  // the rest of the miss queue
 
     if (A.ablate && abl_acc == 0x9E3779B97F4A7C15ull) atomicAdd(&A.counters[CNT_OVF2], 1ull);
     // ---- 2. this bucket's slice of every map workgroup's flushed table (a few entries each): the

@@ -464,7 +464,7 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
             HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
         }
         // 32-bit LDS counts (larger table) when no key can reach 2^32: fewer tokens than that
-        const bool c32 = c->h_cnt[CNT_TOKENS] < 0xFFFFFFFFull && nreg <= 1024;
+        const bool c32 = c->h_cnt[CNT_TOKENS] < 0xFFFFFFFFull && nreg <= 512;
         mrg_launch_bucket_agg(B, idx, c32, s);
         read_counters(c);
         if (c->h_cnt[CNT_KEYS] > c->keys.cap)
