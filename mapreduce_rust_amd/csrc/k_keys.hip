@@ -301,7 +301,7 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
             if (__any(ovf)) overflow(ovf, a, c, d, 1);
         }
     };
-    {
+    if (!(A.ablate & 4u)) {
         Chunk XA, XB;
         uint32_t kA = (uint32_t)wv, rA = 0, oA = 0;
         if (kA < NC) {

@@ -162,7 +162,7 @@ struct BucketArgs {
     KeySet out;
     unsigned long long *counters;
     uint32_t hash_bits;
-    uint32_t ablate;             // timing only (MRG_AGG_ABLATE): 1 = no table adds, 2 = no hash either
+    uint32_t ablate;             // timing only (MRG_AGG_ABLATE): 1 = no table adds, 2 = no hash either, 4 = no tail stream at all
     uint32_t nsub;               // workgroups per bucket, each summing one hash sub-range (1 = whole bucket)
     uint64_t kcap;               // capacity of `out` (keys beyond it are counted, not written)
     uint32_t n_reduce;           // partition of every key written (SipHash-1-3 % n_reduce; 0 = leave to k_partition)
