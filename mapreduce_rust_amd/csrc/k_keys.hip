@@ -403,15 +403,42 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
         }
     }
     __syncthreads();
-    // the keys out: one device atomic per workgroup and pass (a wave atomic each, 32 K of them on one
-    // counter, all at the end of the launch)
-    __shared__ uint32_t s_w[BA_NW];
+    // the keys out: per-wave counts of every pass of 1024 slots in one sweep, one wave scan, ONE
+    // device atomic per workgroup (was one per pass: 1792 on one counter at the end of the launch)
+    constexpr int NP = (int)((BA_CAP + BA_WG - 1) / BA_WG);
+    constexpr int NPW = NP * BA_NW;
+    static_assert(NPW <= 128, "one wave scans two entries per lane");
+    __shared__ uint32_t s_po[NPW];
     __shared__ unsigned long long s_base;
-    for (int i0 = 0; i0 < (int)BA_CAP; i0 += BA_WG) {  // BA_CAP need not be a multiple of BA_WG
-        const int i = min(i0 + tid, (int)BA_CAP - 1);
+#pragma unroll
+    for (int pp = 0; pp < NP; ++pp) {
+        const int i = pp * BA_WG + tid;
+        const uint64_t m = __ballot(i < (int)BA_CAP && s_key[min(i, (int)BA_CAP - 1)].a != MRG_EMPTY_K0);
+        if (lane == 0) s_po[pp * BA_NW + wv] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (wv == 0) {
+        const int e0 = 2 * lane, e1 = e0 + 1;
+        const uint32_t c0 = e0 < NPW ? s_po[e0] : 0u, c1 = e1 < NPW ? s_po[e1] : 0u;
+        uint32_t incl = c0 + c1;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        const uint32_t ex = incl - c0 - c1;
+        if (e0 < NPW) s_po[e0] = ex;
+        if (e1 < NPW) s_po[e1] = ex + c0;
+        const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+        if (lane == 0) s_base = tot ? atomicAdd(&A.counters[CNT_KEYS], (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    const uint64_t kbase = s_base;
+    for (int pp = 0; pp < NP; ++pp) {
+        const int i = min(pp * BA_WG + tid, (int)BA_CAP - 1);
         const BaKey k = s_key[i];
-        const bool full = i0 + tid < (int)BA_CAP && k.a != MRG_EMPTY_K0;
-        const uint64_t j = wg_append<BA_WG>(&A.counters[CNT_KEYS], full, s_w, &s_base);
+        const bool full = pp * BA_WG + tid < (int)BA_CAP && k.a != MRG_EMPTY_K0;
+        const uint64_t m = __ballot(full);
+        const uint64_t j = kbase + s_po[pp * BA_NW + wv] + (uint64_t)__popcll(m & mrg_lanemask_lt());
         if (full && j < A.kcap) {
             gk(A.out.k0)[j] = k.a;
             gk(A.out.k1)[j] = k.b;
