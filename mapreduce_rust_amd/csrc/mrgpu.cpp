@@ -202,6 +202,7 @@ struct mrg_ctx {
     uint32_t agg_nsub = 1;  // bucket-aggregation workgroups per bucket (grown when the tables overflow)
     std::vector<double> bcap_rate;  // tail records per (bucket, map workgroup) per input byte of the workgroup
     uint64_t ocap_hint = 0;         // records per bucket overflow list
+    bool spec_agg = false, spec_c32 = false;  // last wc job took the bucket path (with 32-bit counts)
     // job
     bool job = false;
     int app = 0;
@@ -425,48 +426,91 @@ struct MapBufs {
     }
 };
 
+struct AggLaunch {
+    BucketArgs B{};
+    bool c32 = false, live = false;
+};
+
+uint64_t agg_ocap(mrg_ctx *c) {
+    uint64_t ocap = std::max<uint64_t>(c->ovf_hint, 1u << 20);
+    if (const uint64_t t = env_u64("MRG_TEST_AGG_OCAP", 0)) ocap = t;  // test knob: force the regrow path
+    return ocap;
+}
+
+// one launch of the per-bucket aggregation over the map's output (its overflow list is returned to
+// the pool by agg_put); zero: clear the two counters it adds to (the map launch zeroed them)
+AggLaunch agg_launch(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap, uint64_t ocap, uint32_t nsub,
+                     uint64_t nlong, bool c32, bool zero) {
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const bool idx = is_idx(c);
+    // every workgroup (bucket, sub-range) may emit a full table of keys
+    keys_reserve(c, (uint64_t)MRG_NBUCKET * std::max<uint32_t>(nsub, 1u) * MRG_BA_CAP + ocap + nlong + 1);
+    AggLaunch L;
+    BucketArgs &B = L.B;
+    B.pool = A.pool; B.rbase = A.rbase; B.bcap = A.bcap; B.bcount = A.bcount;
+    B.movf = A.ovf; B.monext = A.onext; B.mocap = A.ocap;
+    B.fk0 = A.fk0; B.fk1 = A.fk1; B.fcnt = A.fcnt; B.fdoc = A.fdoc; B.foff = A.foff;
+    B.nreg = nreg; B.regcap = regcap;
+    B.ok0 = pget<uint64_t>(p, ocap); B.ok1 = pget<uint64_t>(p, ocap);
+    B.ocnt = pget<uint32_t>(p, ocap); B.odoc = idx ? pget<uint32_t>(p, ocap) : nullptr;
+    B.ocap = ocap;
+    B.out = c->keys.ks;
+    B.counters = c->d_cnt;
+    B.hash_bits = hash_bits(c);
+    B.ablate = getenv("MRG_AGG_ABLATE") ? (uint32_t)atoi(getenv("MRG_AGG_ABLATE")) : 0u;
+    B.nsub = nsub;
+    B.kcap = c->keys.cap;
+    B.n_reduce = c->R;
+    if (zero) {
+        HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
+        HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
+    }
+    mrg_launch_bucket_agg(B, idx, c32, s);
+    L.c32 = c32;
+    L.live = true;
+    return L;
+}
+
+void agg_put(mrg_ctx *c, AggLaunch &L) {
+    if (!L.live) return;
+    Pool &p = c->pool;
+    p.put(L.B.ok0); p.put(L.B.ok1); p.put(L.B.ocnt); p.put(L.B.odoc);
+    L.live = false;
+}
+
 // Map-side records: per-bucket LDS aggregation of tail chunks + flushed map tables, exact overflow
 // through the HBM table, then the long keys.
 // Returns false (nothing aggregated) when far more keys miss the per-bucket tables than the overflow
 // path handles well (millions of distinct keys without the tail share that selects the wide path up
 // front): the caller then runs the wide aggregation on the same map output.
-bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap, LongItems li) {
+// pre: a launch the caller made right behind the map (before its counters reached the host), used
+// when its parameters still hold -- the counters read after the map are then already its own.
+bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap, LongItems li,
+                      AggLaunch *pre = nullptr) {
     if (nreg > 2048) raise(MRG_EINVAL, "internal: %u map workgroups exceed the aggregation's region table", nreg);
-    Pool &p = c->pool;
-    hipStream_t s = c->stream;
     const bool idx = is_idx(c);
-    uint64_t ocap = std::max<uint64_t>(c->ovf_hint, 1u << 20);
-    if (const uint64_t t = env_u64("MRG_TEST_AGG_OCAP", 0)) ocap = t;  // test knob: force the regrow path
+    uint64_t ocap = agg_ocap(c);
     uint32_t agg_launches = 0;
     uint32_t nsub = c->agg_nsub;
     if (const uint64_t t = env_u64("MRG_TEST_AGG_NSUB", 0)) nsub = (uint32_t)t;
+    const bool dirty = pre && pre->live;  // a launch since the map: its counters need clearing before another
     for (;;) {
         ++agg_launches;
-        // every workgroup (bucket, sub-range) may emit a full table of keys
-        keys_reserve(c, (uint64_t)MRG_NBUCKET * std::max<uint32_t>(nsub, 1u) * MRG_BA_CAP + ocap + li.n + 1);
-        BucketArgs B{};
-        B.pool = A.pool; B.rbase = A.rbase; B.bcap = A.bcap; B.bcount = A.bcount;
-        B.movf = A.ovf; B.monext = A.onext; B.mocap = A.ocap;
-        B.fk0 = A.fk0; B.fk1 = A.fk1; B.fcnt = A.fcnt; B.fdoc = A.fdoc; B.foff = A.foff;
-        B.nreg = nreg; B.regcap = regcap;
-        B.ok0 = pget<uint64_t>(p, ocap); B.ok1 = pget<uint64_t>(p, ocap);
-        B.ocnt = pget<uint32_t>(p, ocap); B.odoc = idx ? pget<uint32_t>(p, ocap) : nullptr;
-        B.ocap = ocap;
-        B.out = c->keys.ks;
-        B.counters = c->d_cnt;
-        B.hash_bits = hash_bits(c);
-        B.ablate = getenv("MRG_AGG_ABLATE") ? (uint32_t)atoi(getenv("MRG_AGG_ABLATE")) : 0u;
-        B.nsub = nsub;
-        B.kcap = c->keys.cap;
-        B.n_reduce = c->R;
-        if (agg_launches > 1) {  // the map launch zeroed every counter; the map leaves these two alone
-            HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
-            HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
-        }
         // 32-bit LDS counts (larger table) when no key can reach 2^32: fewer tokens than that
         const bool c32 = c->h_cnt[CNT_TOKENS] < 0xFFFFFFFFull && nreg <= 512;
-        mrg_launch_bucket_agg(B, idx, c32, s);
-        read_counters(c);
+        AggLaunch L;
+        if (pre && pre->live && agg_launches == 1 && pre->B.nsub == nsub && pre->B.ocap == ocap &&
+            pre->B.kcap >= (uint64_t)MRG_NBUCKET * std::max<uint32_t>(nsub, 1u) * MRG_BA_CAP + ocap + li.n + 1 &&
+            (!pre->c32 || c32)) {
+            L = *pre;  // its counters came with the map's
+            pre->live = false;
+        } else {
+            if (pre) agg_put(c, *pre);
+            L = agg_launch(c, A, nreg, regcap, ocap, nsub, li.n, c32, agg_launches > 1 || dirty);
+            read_counters(c);
+        }
+        BucketArgs &B = L.B;
         if (c->h_cnt[CNT_KEYS] > c->keys.cap)
             raise(MRG_EINVAL, "internal: bucket aggregation emitted %llu keys for %llu slots",
                   (unsigned long long)c->h_cnt[CNT_KEYS], (unsigned long long)c->keys.cap);
@@ -479,21 +523,21 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         // to 16; the count is remembered by the context.  Beyond that, the wide aggregation.
         const uint64_t heavy = env_u64("MRG_TEST_AGG_WIDE_OVF", 4ull << 20);
         if (novf > heavy && nsub < 16 && !env_u64("MRG_TEST_AGG_NSUB", 0)) {
-            p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
+            agg_put(c, L);
             nsub = c->agg_nsub = std::min<uint32_t>(16, 2 * nsub);  // overflow counts records, not keys: double
             if (getenv("MRG_DEBUG")) fprintf(stderr, "[mrgpu] bucket agg: %llu overflow records -> %u workgroups per bucket\n", (unsigned long long)novf, nsub);
             continue;
         }
         const char *wenv = getenv("MRG_WIDE");  // MRG_WIDE=0 pins the bucket path (tests of its overflow)
         if (!idx && novf > heavy && !(wenv && atoi(wenv) == 0)) {
-            p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
+            agg_put(c, L);
             c->agg_nsub = 1;  // the next job starts from one workgroup per bucket (a low-cardinality job
                               // would otherwise stream every bucket 16 times)
             if (getenv("MRG_DEBUG")) fprintf(stderr, "[mrgpu] bucket agg: %llu overflow records -> wide\n", (unsigned long long)novf);
             return false;
         }
         if (novf > ocap) {  // overflow list too small: grow (remembered) and run again
-            p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
+            agg_put(c, L);
             ocap = c->ovf_hint = novf + novf / 8 + 1024;
             continue;
         }
@@ -502,9 +546,11 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
             src.k0 = B.ok0; src.k1 = B.ok1; src.cnt = B.ocnt; src.doc = B.odoc; src.n = novf;
             table_aggregate(c, src);
         }
-        p.put(B.ok0); p.put(B.ok1); p.put(B.ocnt); p.put(B.odoc);
+        agg_put(c, L);
         c->st.overflow_keys = novf;
         c->st.agg_launches = agg_launches;
+        c->spec_agg = !idx;
+        c->spec_c32 = L.c32;
         {  // the next job's workgroups per bucket: enough sub-ranges for this job's key count
             const uint64_t per = (uint64_t)MRG_NBUCKET * 4096u;
             c->agg_nsub = (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, (c->h_cnt[CNT_KEYS] + per - 1) / per));
@@ -913,6 +959,7 @@ void job_map(mrg_ctx *c) {
     if (const uint64_t t = env_u64("MRG_TEST_OVF_CAP", 0)) ocap = t;
     MapArgs A{};
     MapBufs M;
+    AggLaunch spec;  // the aggregation launched right behind the map (wc, the last job took the bucket path)
     uint32_t launches = 0;
     for (;;) {
         std::vector<uint64_t> rbase(MRG_NBUCKET, 0);
@@ -976,6 +1023,15 @@ void job_map(mrg_ctx *c) {
         ev_rec(c, 1);
         HIPCHK(hipGetLastError());
         ++launches;
+        // the aggregation queued behind the map before the host sees the map's counters (one host
+        // round trip less per job); checked against them below and by bucket_aggregate, and dropped
+        // when the map reruns, goes wide or the 32-bit-count guess was wrong
+        if (launches == 1 && !idx && c->spec_agg && !M.prof && !getenv("MRG_WIDE") && !getenv("MRG_NO_SPEC_AGG") &&
+            !env_u64("MRG_TEST_AGG_NSUB", 0) && grid <= 2048) {
+            ev_rec(c, 2);
+            spec = agg_launch(c, A, (uint32_t)grid, cap, agg_ocap(c), c->agg_nsub, lcap, c->spec_c32 && grid <= 512,
+                              false);
+        }
         // overflow-list fill into pinned scratch, then the counters: one host wait for both
         uint32_t *onext = (uint32_t *)&c->h_cnt[CNT_N + 8];
         HIPCHK(hipMemcpyAsync(onext, M.onext, 4ull * MRG_NBUCKET, hipMemcpyDeviceToHost, s));
@@ -1015,6 +1071,7 @@ void job_map(mrg_ctx *c) {
         }
         const uint64_t nl = c->h_cnt[CNT_LONG];
         if (c->h_cnt[CNT_OVF] == 0 && nl <= lcap) break;
+        agg_put(c, spec);
         // capacity exceeded: grow each bucket's regions to its demand (remembered), run again
         if (c->h_cnt[CNT_OVF]) {
             std::vector<uint32_t> cnt((uint64_t)grid * MRG_NBUCKET);
@@ -1047,6 +1104,7 @@ void job_map(mrg_ctx *c) {
     c->st.map_records = c->h_cnt[CNT_REC];
     const uint64_t errpos = c->h_cnt[CNT_ERRPOS];
     auto release_map = [&]() {
+        agg_put(c, spec);
         M.release(p);
         p.put(d_doc_off); p.put(d_cb); p.put(d_ids);
     };
@@ -1057,14 +1115,23 @@ void job_map(mrg_ctx *c) {
         raise(MRG_EUTF8, "stream did not contain valid UTF-8: document %u (id %u), byte offset %llu", d, ids[d],
               (unsigned long long)(errpos - c->doc_off[d]));
     }
-    ev_rec(c, 2);
+    if (!spec.live) ev_rec(c, 2);
     LongItems li{};
     li.base = c->d_in; li.start = M.lstart; li.rawlen = M.llen; li.doc = M.ldoc; li.cnt = nullptr;
     li.n = c->h_cnt[CNT_LONG];
     // high cardinality (most tokens missed the map-side combine): sort-based aggregation
     bool wide = !idx && c->h_cnt[CNT_REC] > (32ull << 20) && 2 * c->h_cnt[CNT_REC] > c->h_cnt[CNT_TOKENS];
     if (const char *v = getenv("MRG_WIDE")) wide = !idx && atoi(v) != 0;  // test / tuning override
-    if (wide || !bucket_aggregate(c, A, (uint32_t)grid, cap, li)) wide_aggregate(c, A, (uint32_t)grid, cap, li);
+    if (wide && spec.live) {  // the queued aggregation was not needed: its counters back to the map's zeros
+        agg_put(c, spec);
+        HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
+        HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
+    }
+    if (wide) c->spec_agg = false;
+    if (wide || !bucket_aggregate(c, A, (uint32_t)grid, cap, li, &spec)) {
+        c->spec_agg = false;
+        wide_aggregate(c, A, (uint32_t)grid, cap, li);
+    }
     ev_rec(c, 3);
     release_map();
     c->st.ms_aggregate = ev_ms(c, 2, 3);
