@@ -458,7 +458,9 @@ static int faithful_reduce_task(int n_files, uint32_t r, const char *dir, bytes_
     uint32_t prevl = 0;
     uint64_t nvals = 0;
     for (size_t t = 0; t < nkv && rc == ORACLE_OK; ++t) {                    /* :169-184 */
-        if (!prev) { prev = kv[t].k; prevl = kv[t].kl; }
+        if (prevl == 0) { prev = kv[t].k; prevl = kv[t].kl; }            /* :170-172 `prev.is_empty()`: an
+                                                                            empty key never stays prev, so empty-key
+                                                                            lines fold into the next group */
         if (kv[t].kl != prevl || memcmp(kv[t].k, prev, prevl)) {
             size_t before = out->n;
             by_put(out, prev, prevl);
@@ -496,6 +498,18 @@ static int wc_faithful(const uint8_t *const *files, const size_t *lens, int n_fi
 }
 
 /* ------------------------------------------------------------------ public entry points */
+
+/* Worker::reduce (worker.rs:157-193) on intermediates already in `dir` (mr-{m}-{r}.txt, m < n_files):
+ * the bytes of mr-{r}.txt are returned (and written to dir/mr-{r}.txt). */
+int oracle_reduce_files(const char *dir, int n_files, uint32_t r, uint8_t **out, size_t *out_len) {
+    if (!dir || n_files < 0) return ORACLE_EARG;
+    bytes_t o = {0};
+    int rc = faithful_reduce_task(n_files, r, dir, &o);
+    if (rc != ORACLE_OK) { free(o.p); return rc; }
+    *out = o.p ? o.p : (uint8_t *)malloc(1);
+    *out_len = o.n;
+    return ORACLE_OK;
+}
 
 /* Word count over n_files inputs, nReduce = R.  Output: all mr-{r}.txt concatenated in r order
  * (*out, *out_len), with part_off[0..R] byte offsets.  mode ORACLE_FAITHFUL needs `dir`. */

@@ -46,6 +46,8 @@ def lib():
         L.oracle_wc_mt.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
                                    ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(u8p),
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
+        L.oracle_reduce_files.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(u8p),
+                                          ctypes.POINTER(ctypes.c_size_t)]
         L.oracle_free.argtypes = [ctypes.c_void_p]
         _lib = L
     return _lib
@@ -159,3 +161,19 @@ def wc_mt(buffers, n_reduce, threads=8):
     if rc:
         raise OracleError(rc)
     return _split(_take(out, olen.value), list(offs), n_reduce)
+
+
+def reduce_files(contents, r=0):
+    """The FAITHFUL reduce task (worker.rs:157-193) over intermediate file contents: contents[m] is
+    written to mr-{m}-{r}.txt in a scratch directory, then the oracle reads them back and reduces."""
+    L = lib()
+    with tempfile.TemporaryDirectory(prefix="oracle_rd_") as d:
+        for m, c in enumerate(contents):
+            with open(os.path.join(d, f"mr-{m}-{r}.txt"), "wb") as f:
+                f.write(c)
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t()
+        rc = L.oracle_reduce_files(d.encode(), len(contents), r, ctypes.byref(out), ctypes.byref(n))
+    if rc:
+        raise OracleError(rc)
+    return _take(out, n.value)

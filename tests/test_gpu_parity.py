@@ -450,29 +450,7 @@ def test_wide_path_synthetic_and_unicode(ctx, wide):
 
 # ---- the reference's text intermediates mr-{m}-{r}.txt
 
-def _ref_reduce(files, drop_last=True):
-    """worker.rs:79-109 + 157-193 restated over intermediate file contents (wc::reduce = len)."""
-    kvs = []
-    for c in files:
-        for line in c.decode("utf-8").split("\n"):
-            if not line:
-                continue
-            f = line.split(" ")
-            assert len(f) == 2
-            kvs.append((f[0], f[1]))
-    kvs.sort(key=lambda kv: kv[0].encode())
-    out, prev, vals = [], "", []
-    for k, v in kvs:
-        if prev == "":
-            prev = k
-        if k != prev:
-            out.append(f"{prev} {len(vals)}\n")
-            vals = []
-            prev = k
-        vals.append(v)
-    if not drop_last and vals:
-        out.append(f"{prev} {len(vals)}\n")
-    return "".join(out).encode()
+from reduce_twin import REDUCE_EDGE_CASES, ref_reduce as _ref_reduce  # noqa: E402
 
 
 @pytest.mark.parametrize("R", ["10", "1", "3", "64"])
@@ -501,15 +479,7 @@ def test_map_text_unicode_and_long_tokens(ctx):
 
 def test_reduce_text_edge_cases(ctx):
     import mapreduce_rust_amd as M
-    cases = [
-        [b"b 1\na 1\n", b"a 1\nc 7\n\n\nb x\n"],          # values other than "1" still count 1 each
-        [b" 1\n 1\nzz 1\nab 1\n"],                        # empty keys join the first group (prev == "")
-        [b" 1\n"],                                        # only empty keys
-        [b"a-b 1\nx\xc3\xa9y 1\na-b 1\nq 1"],             # non-\w key bytes kept verbatim, no final \n
-        [("k" * 40 + " 1\n").encode() * 3 + ("k" * 39 + "j 1\n").encode() + b"z 1\n"],  # long keys
-        [b"", b"\n\n", b"w 1\n"],                         # empty files and empty lines
-        [],
-    ]
+    cases = REDUCE_EDGE_CASES
     for files in cases:
         for flags, drop in ((0, True), (M.FLAG_NO_COMPAT_DROP_LAST, False)):
             assert ctx.reduce_text(files, flags) == _ref_reduce(files, drop), (files, flags)
