@@ -92,11 +92,17 @@ typedef struct {
     uint64_t exchange_recv;    /* bytes this rank received from peers */
     uint64_t map_spill;        /* map records that overflowed their tail region into a bucket's shared
                                   overflow list (last map launch) */
+    uint64_t nonascii_tiles;   /* 1 KiB tiles that took the non-ASCII tokenizer (last map launch) */
+    uint64_t tail_records_16;  /* map records stored as 16-byte tail records (keys of 13..16 bytes; the
+                                  others are 12-byte records) */
+    uint32_t spec_agg;         /* the aggregation queued behind the map: 0 none, 1 used, 2 dropped */
+    uint32_t agg_path;         /* aggregation taken: 0 none, 1 bucket tables, 2 wide (sort-based) */
 } mrg_stats;
 
 /* ABI history: 1 = round-1 layout; 2 = mrg_run_job's last argument is n_gpus (was a device index);
- * 3 = 24-byte exchange records (were 40), mrg_run_get_stats.  mrg_version() names the ABI it implements. */
-#define MRG_ABI_VERSION 3
+ * 3 = 24-byte exchange records (were 40), mrg_run_get_stats; 4 = mrg_stats gains nonascii_tiles,
+ * tail_records_16, spec_agg, agg_path.  mrg_version() names the ABI it implements. */
+#define MRG_ABI_VERSION 4
 
 const char *mrg_last_error(void);
 const char *mrg_version(void);

@@ -1087,6 +1087,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     if (tid == 0) {
         g_add(&A.counters[CNT_TOKENS], (unsigned long long)s_tot[0]);
         g_add(&A.counters[CNT_REC], (unsigned long long)s_tot[1]);
+        if (s_ngen) g_add(&A.counters[CNT_NONASCII], (unsigned long long)s_ngen);
     }
     MRG_PT(6);
 #ifdef MRG_MAP_PROF

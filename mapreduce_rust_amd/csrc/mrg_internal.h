@@ -30,6 +30,7 @@ enum {
     CNT_KEYS = 4,     // distinct keys appended to the KeySet
     CNT_OVF = 5,      // tail records that found neither region nor overflow-list room (rerun)
     CNT_OVF2 = 6,     // keys that did not fit their bucket's LDS table (exact overflow path)
+    CNT_NONASCII = 7, // 1 KiB tiles that took the non-ASCII tokenizer
     CNT_N = 8
 };
 

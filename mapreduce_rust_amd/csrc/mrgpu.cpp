@@ -75,6 +75,11 @@ uint64_t env_u64(const char *name, uint64_t dflt) {
     const char *v = getenv(name);
     return v && *v ? strtoull(v, nullptr, 10) : dflt;
 }
+// MRG_WIDE=<non-zero>: force the wide (sort-based) aggregation; MRG_WIDE=0 pins the bucket path
+bool wide_forced() {
+    const char *v = getenv("MRG_WIDE");
+    return v && *v && atoi(v) != 0;
+}
 
 template <class F>
 int guard(F &&f) {
@@ -236,6 +241,10 @@ struct mrg_comm {
     uint64_t *d_counts = nullptr;
     int *d_flag = nullptr;
     std::atomic<bool> aborted{false};  // ncclCommAbort was called (by this rank or by mrg_run_job's watchdog)
+    // held around every RCCL enqueue of a rank thread and around the abort, so mrg_run_job's watchdog
+    // does not free the communicator (ncclCommAbort) between a rank thread's aborted-check and its
+    // RCCL call; never held across a wait on the stream
+    std::timed_mutex mu;
 };
 
 struct mrg_parts {
@@ -428,6 +437,7 @@ struct MapBufs {
 
 struct AggLaunch {
     BucketArgs B{};
+    uint64_t nlong = 0;  // long keys the launch reserved key slots for
     bool c32 = false, live = false;
 };
 
@@ -467,6 +477,7 @@ AggLaunch agg_launch(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regca
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
     }
     mrg_launch_bucket_agg(B, idx, c32, s);
+    L.nlong = nlong;
     L.c32 = c32;
     L.live = true;
     return L;
@@ -500,12 +511,19 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         // 32-bit LDS counts (larger table) when no key can reach 2^32: fewer tokens than that
         const bool c32 = c->h_cnt[CNT_TOKENS] < 0xFFFFFFFFull && nreg <= 512;
         AggLaunch L;
+        // the queued launch is reused only when it ran with this job's parameters: sub-ranges, overflow
+        // capacity, count width, and key slots for at least the long keys the map produced (the map
+        // reruns whenever its long keys exceed lcap, which drops the queued launch, so li.n <= nlong
+        // holds here; it is checked rather than assumed)
         if (pre && pre->live && agg_launches == 1 && pre->B.nsub == nsub && pre->B.ocap == ocap &&
+            li.n <= pre->nlong &&
             pre->B.kcap >= (uint64_t)MRG_NBUCKET * std::max<uint32_t>(nsub, 1u) * MRG_BA_CAP + ocap + li.n + 1 &&
-            (!pre->c32 || c32)) {
+            pre->c32 == c32) {
             L = *pre;  // its counters came with the map's
             pre->live = false;
+            c->st.spec_agg = 1;
         } else {
+            if (pre && pre->live) c->st.spec_agg = 2;
             if (pre) agg_put(c, *pre);
             L = agg_launch(c, A, nreg, regcap, ocap, nsub, li.n, c32, agg_launches > 1 || dirty);
             read_counters(c);
@@ -550,7 +568,8 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         c->st.overflow_keys = novf;
         c->st.agg_launches = agg_launches;
         c->spec_agg = !idx;
-        c->spec_c32 = L.c32;
+        c->spec_c32 = c32;  // the width this job allowed (not the one a reused launch happened to use)
+        c->st.agg_path = 1;
         {  // the next job's workgroups per bucket: enough sub-ranges for this job's key count
             const uint64_t per = (uint64_t)MRG_NBUCKET * 4096u;
             c->agg_nsub = (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, (c->h_cnt[CNT_KEYS] + per - 1) / per));
@@ -918,6 +937,7 @@ void job_map(mrg_ctx *c) {
     if (c->doc_off.empty()) raise(MRG_EINVAL, "no input: call mrg_job_set_input first");
     c->wide.release(c->pool);  // a second map of the same job replaces the first one's keys
     c->mapped = c->reduced = false;
+    c->st.spec_agg = c->st.agg_path = 0;
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     const uint32_t nd = (uint32_t)c->doc_off.size() - 1;
@@ -1026,11 +1046,14 @@ void job_map(mrg_ctx *c) {
         // the aggregation queued behind the map before the host sees the map's counters (one host
         // round trip less per job); checked against them below and by bucket_aggregate, and dropped
         // when the map reruns, goes wide or the 32-bit-count guess was wrong
-        if (launches == 1 && !idx && c->spec_agg && !M.prof && !getenv("MRG_WIDE") && !getenv("MRG_NO_SPEC_AGG") &&
-            !env_u64("MRG_TEST_AGG_NSUB", 0) && grid <= 2048) {
+        // (MRG_WIDE=1 forces the wide path, so nothing is queued; MRG_WIDE=0 and MRG_TEST_AGG_NSUB still
+        // queue it: their tests run through this path)
+        if (launches == 1 && !idx && c->spec_agg && !M.prof && !wide_forced() && !getenv("MRG_NO_SPEC_AGG") &&
+            grid <= 2048) {
             ev_rec(c, 2);
-            spec = agg_launch(c, A, (uint32_t)grid, cap, agg_ocap(c), c->agg_nsub, lcap, c->spec_c32 && grid <= 512,
-                              false);
+            uint32_t nsub = c->agg_nsub;
+            if (const uint64_t t = env_u64("MRG_TEST_AGG_NSUB", 0)) nsub = (uint32_t)t;
+            spec = agg_launch(c, A, (uint32_t)grid, cap, agg_ocap(c), nsub, lcap, c->spec_c32 && grid <= 512, false);
         }
         // overflow-list fill into pinned scratch, then the counters: one host wait for both
         uint32_t *onext = (uint32_t *)&c->h_cnt[CNT_N + 8];
@@ -1071,6 +1094,7 @@ void job_map(mrg_ctx *c) {
         }
         const uint64_t nl = c->h_cnt[CNT_LONG];
         if (c->h_cnt[CNT_OVF] == 0 && nl <= lcap) break;
+        if (spec.live) c->st.spec_agg = 2;  // the rerun invalidates the queued aggregation
         agg_put(c, spec);
         // capacity exceeded: grow each bucket's regions to its demand (remembered), run again
         if (c->h_cnt[CNT_OVF]) {
@@ -1102,6 +1126,7 @@ void job_map(mrg_ctx *c) {
     c->st.tokens = c->h_cnt[CNT_TOKENS];
     c->st.long_tokens = c->h_cnt[CNT_LONG];
     c->st.map_records = c->h_cnt[CNT_REC];
+    c->st.nonascii_tiles = c->h_cnt[CNT_NONASCII];
     const uint64_t errpos = c->h_cnt[CNT_ERRPOS];
     auto release_map = [&]() {
         agg_put(c, spec);
@@ -1123,6 +1148,7 @@ void job_map(mrg_ctx *c) {
     bool wide = !idx && c->h_cnt[CNT_REC] > (32ull << 20) && 2 * c->h_cnt[CNT_REC] > c->h_cnt[CNT_TOKENS];
     if (const char *v = getenv("MRG_WIDE")) wide = !idx && atoi(v) != 0;  // test / tuning override
     if (wide && spec.live) {  // the queued aggregation was not needed: its counters back to the map's zeros
+        c->st.spec_agg = 2;
         agg_put(c, spec);
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
@@ -1130,6 +1156,7 @@ void job_map(mrg_ctx *c) {
     if (wide) c->spec_agg = false;
     if (wide || !bucket_aggregate(c, A, (uint32_t)grid, cap, li, &spec)) {
         c->spec_agg = false;
+        c->st.agg_path = 2;
         wide_aggregate(c, A, (uint32_t)grid, cap, li);
     }
     ev_rec(c, 3);
@@ -1490,6 +1517,7 @@ void test_fail(const char *stage, int rank) {
 
 // An RCCL call of the exchange: on failure the communicator is aborted (its peers' pending operations
 // then fail instead of waiting forever) and the call raises MRG_ECOMM.
+// Caller holds m->mu (a CommLock).
 void nccl_or_abort(mrg_comm *m, ncclResult_t r, const char *what) {
     if (r == ncclSuccess) return;
     if (!m->aborted.exchange(true)) (void)ncclCommAbort(m->comm);
@@ -1500,12 +1528,31 @@ void check_not_aborted(mrg_comm *m) {
     if (m->aborted.load()) raise(MRG_ECOMM, "the communicator was aborted (another rank of the job failed)");
 }
 
+// The communicator's lock for a run of RCCL enqueues, taken only if it has not been aborted (the
+// abort frees it): a watchdog abort waits for the enqueues, and enqueues after it raise MRG_ECOMM.
+struct CommLock {
+    std::unique_lock<std::timed_mutex> lk;
+    explicit CommLock(mrg_comm *m) : lk(m->mu) { check_not_aborted(m); }
+};
+
+// Abort from any thread (mrg_run_job's watchdog), serialised with the rank threads' enqueues.  An
+// enqueue can itself block inside RCCL (a first send/recv to a peer sets up the connection and waits
+// for that peer): a lock still held after 2 s belongs to such a blocked call, which is exactly what
+// ncclCommAbort exists to release, so the abort then goes ahead without the lock.
+void comm_abort(mrg_comm *m) {
+    std::unique_lock<std::timed_mutex> lk(m->mu, std::chrono::milliseconds(2000));
+    if (m->comm && !m->aborted.exchange(true)) (void)ncclCommAbort(m->comm);
+}
+
 // Max of `flag` over the ranks (one RCCL all-reduce into the preallocated status word): every rank
 // learns whether any rank failed, so all of them leave the exchange together.
 int agree(mrg_ctx *c, mrg_comm *m, int flag) {
     check_not_aborted(m);
     HIPCHK(hipMemcpyAsync(m->d_flag, &flag, sizeof flag, hipMemcpyHostToDevice, c->stream));
-    nccl_or_abort(m, ncclAllReduce(m->d_flag, m->d_flag, 1, ncclInt, ncclMax, m->comm, c->stream), "ncclAllReduce");
+    {
+        CommLock lk(m);
+        nccl_or_abort(m, ncclAllReduce(m->d_flag, m->d_flag, 1, ncclInt, ncclMax, m->comm, c->stream), "ncclAllReduce");
+    }
     int any = 0;
     HIPCHK(hipMemcpyAsync(&any, m->d_flag, sizeof any, hipMemcpyDeviceToHost, c->stream));
     sync(c);
@@ -1560,7 +1607,10 @@ void job_shuffle(mrg_ctx *c, mrg_comm *m) {
     for (uint32_t o = 0; o < G; ++o) sc[3 * o + 2] = mine.code ? 1u : 0u;
     // ---- collective 1: the counts all-to-all (with every rank's status)
     HIPCHK(hipMemcpyAsync(m->d_counts, sc.data(), 24ull * G, hipMemcpyHostToDevice, s));
-    nccl_or_abort(m, ncclAllToAll(m->d_counts, m->d_counts + 3 * G, 3, ncclUint64, m->comm, s), "ncclAllToAll");
+    {
+        CommLock lk(m);
+        nccl_or_abort(m, ncclAllToAll(m->d_counts, m->d_counts + 3 * G, 3, ncclUint64, m->comm, s), "ncclAllToAll");
+    }
     HIPCHK(hipMemcpyAsync(rc.data(), m->d_counts + 3 * G, 24ull * G, hipMemcpyDeviceToHost, s));
     sync(c);
     check_not_aborted(m);
@@ -1602,17 +1652,20 @@ void job_shuffle(mrg_ctx *c, mrg_comm *m) {
     if (sc[3 * me]) HIPCHK(hipMemcpyAsync(rrec + rro[me] * X, srec + sro[me] * X, sc[3 * me] * X, hipMemcpyDeviceToDevice, s));
     if (sc[3 * me + 1]) HIPCHK(hipMemcpyAsync(rheap + rho[me], sheap + sho[me], sc[3 * me + 1], hipMemcpyDeviceToDevice, s));
     uint64_t sent = 0, recv = 0;
-    nccl_or_abort(m, ncclGroupStart(), "ncclGroupStart");
-    for (uint32_t o = 0; o < G; ++o) {
-        if (o == me) continue;
-        if (sc[3 * o]) nccl_or_abort(m, ncclSend(srec + sro[o] * X, sc[3 * o] * X, ncclUint8, (int)o, m->comm, s), "ncclSend");
-        if (sc[3 * o + 1]) nccl_or_abort(m, ncclSend(sheap + sho[o], sc[3 * o + 1], ncclUint8, (int)o, m->comm, s), "ncclSend");
-        if (rc[3 * o]) nccl_or_abort(m, ncclRecv(rrec + rro[o] * X, rc[3 * o] * X, ncclUint8, (int)o, m->comm, s), "ncclRecv");
-        if (rc[3 * o + 1]) nccl_or_abort(m, ncclRecv(rheap + rho[o], rc[3 * o + 1], ncclUint8, (int)o, m->comm, s), "ncclRecv");
-        sent += sc[3 * o] * X + sc[3 * o + 1];
-        recv += rc[3 * o] * X + rc[3 * o + 1];
+    {
+        CommLock lk(m);
+        nccl_or_abort(m, ncclGroupStart(), "ncclGroupStart");
+        for (uint32_t o = 0; o < G; ++o) {
+            if (o == me) continue;
+            if (sc[3 * o]) nccl_or_abort(m, ncclSend(srec + sro[o] * X, sc[3 * o] * X, ncclUint8, (int)o, m->comm, s), "ncclSend");
+            if (sc[3 * o + 1]) nccl_or_abort(m, ncclSend(sheap + sho[o], sc[3 * o + 1], ncclUint8, (int)o, m->comm, s), "ncclSend");
+            if (rc[3 * o]) nccl_or_abort(m, ncclRecv(rrec + rro[o] * X, rc[3 * o] * X, ncclUint8, (int)o, m->comm, s), "ncclRecv");
+            if (rc[3 * o + 1]) nccl_or_abort(m, ncclRecv(rheap + rho[o], rc[3 * o + 1], ncclUint8, (int)o, m->comm, s), "ncclRecv");
+            sent += sc[3 * o] * X + sc[3 * o + 1];
+            recv += rc[3 * o] * X + rc[3 * o + 1];
+        }
+        nccl_or_abort(m, ncclGroupEnd(), "ncclGroupEnd");
     }
-    nccl_or_abort(m, ncclGroupEnd(), "ncclGroupEnd");
     HIPCHK(hipEventRecord(e1, s));
     HIPCHK(hipEventSynchronize(e1));
     check_not_aborted(m);  // a watchdog abort ends a transfer early: its buffers are not to be used
@@ -1794,7 +1847,7 @@ void text_reduce(mrg_ctx *c, const uint8_t *const *files, const uint64_t *sizes,
 extern "C" {
 
 const char *mrg_last_error(void) { return g_err.c_str(); }
-const char *mrg_version(void) { return "mrgpu 0.3 (gfx950, abi 3)"; }
+const char *mrg_version(void) { return "mrgpu 0.4 (gfx950, abi 4)"; }
 
 int mrg_open(int device, mrg_ctx **out) {
     return guard([&] {
@@ -2329,7 +2382,7 @@ void run_ranks(std::vector<RankState> &rs, bool watch, F &&fn, std::vector<int> 
             if (ms_since(first_fail) < (double)grace_ms) continue;
             aborted = true;
             for (auto &r : rs)
-                if (r.m && r.m->comm && !r.m->aborted.exchange(true)) (void)ncclCommAbort(r.m->comm);
+                if (r.m) comm_abort(r.m);
         }
     }
     for (auto &t : th) t.join();

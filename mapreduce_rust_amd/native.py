@@ -55,7 +55,9 @@ class Stats(C.Structure):
                 ("ms_map", C.c_double), ("ms_aggregate", C.c_double), ("ms_sort", C.c_double),
                 ("ms_format", C.c_double), ("map_launches", C.c_uint32), ("agg_launches", C.c_uint32),
                 ("overflow_keys", C.c_uint64), ("ms_exchange", C.c_double), ("exchange_sent", C.c_uint64),
-                ("exchange_recv", C.c_uint64), ("map_spill", C.c_uint64)]
+                ("exchange_recv", C.c_uint64), ("map_spill", C.c_uint64),
+                ("nonascii_tiles", C.c_uint64), ("tail_records_16", C.c_uint64), ("spec_agg", C.c_uint32),
+                ("agg_path", C.c_uint32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

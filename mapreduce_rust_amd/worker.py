@@ -7,8 +7,9 @@ Same task structure and file conventions as the reference:
 intermediates="text" (default, wc): mr-{m}-{r}.txt byte-identical to the reference's ("key 1" per
 token in input order, mrg_map_text / mrg_reduce_text), so GPU and reference CPU workers can take
 each other's tasks.  intermediates="records": the engine's combined form, mr-{m}-{r}.rec (per-key
-counts as 24-byte exchange records + long-key heap, include/mrgpu.h; little-endian u64 n_records,
-u64 heap_bytes, records, heap) -- far smaller, and the only form for the indexer.  mr-{r}.txt is
+counts as 24-byte exchange records + long-key heap, include/mrgpu.h; a 32-byte little-endian header
+{u64 magic "MRGREC\\0\\0", u32 format, u32 record bytes, u64 n_records, u64 heap_bytes}, then the records
+and the heap) -- far smaller, and the only form for the indexer.  mr-{r}.txt is
 byte-identical to the reference's either way.  A map task and a reduce task may run in different
 processes, as in the reference (the files in the working directory are the hand-off).
 """
@@ -18,6 +19,42 @@ import struct
 from . import native
 
 APPS = {"wc": native.APP_WC, "indexer": native.APP_INDEXER}
+
+
+REC_MAGIC = b"MRGREC\0\0"
+REC_FORMAT = 2            # the exchange-record format of include/mrgpu.h (24-byte records, ABI >= 3)
+_REC_HDR = struct.Struct("<8sIIQQ")
+
+
+class RecFileError(ValueError):
+    pass
+
+
+def read_rec(path):
+    """(records, heap) of an mr-{m}-{r}.rec file; raises RecFileError on a foreign, stale-format or
+    truncated file (the import would otherwise read past what the file holds)."""
+    with open(path, "rb") as f:
+        hdr = f.read(_REC_HDR.size)
+        if len(hdr) != _REC_HDR.size:
+            raise RecFileError(f"{path}: truncated header")
+        magic, fmt, xb, n, hb = _REC_HDR.unpack(hdr)
+        if magic != REC_MAGIC:
+            raise RecFileError(f"{path}: not an mrgpu record file")
+        if fmt != REC_FORMAT or xb != native.XREC_BYTES:
+            raise RecFileError(f"{path}: record format {fmt} ({xb}-byte records), expected {REC_FORMAT} "
+                               f"({native.XREC_BYTES}-byte records)")
+        rec = f.read(n * xb)
+        heap = f.read(hb)
+        if len(rec) != n * xb or len(heap) != hb or f.read(1):
+            raise RecFileError(f"{path}: size does not match its header ({n} records, {hb} heap bytes)")
+    return rec, heap
+
+
+def write_rec(path, rec, heap):
+    with open(path, "wb") as f:
+        f.write(_REC_HDR.pack(REC_MAGIC, REC_FORMAT, native.XREC_BYTES, len(rec) // native.XREC_BYTES, len(heap)))
+        f.write(rec)
+        f.write(heap)
 
 
 def _rec_path(m, r, cwd):
@@ -59,10 +96,7 @@ class Worker:
         try:
             for r in range(self.reduce_n):                                 # worker.rs:120-125
                 rec, heap = parts.get(r)
-                with open(_rec_path(m, r, self.cwd), "wb") as f:
-                    f.write(struct.pack("<QQ", len(rec) // native.XREC_BYTES, len(heap)))
-                    f.write(rec)
-                    f.write(heap)
+                write_rec(_rec_path(m, r, self.cwd), rec, heap)
         finally:
             parts.free()
         return True
@@ -80,12 +114,11 @@ class Worker:
             return True
         recs, heaps, seg_r, seg_h = [], [], [], []
         for m in range(self.map_n):                                        # worker.rs:84-107
-            with open(_rec_path(m, r, self.cwd), "rb") as f:
-                n, hb = struct.unpack("<QQ", f.read(16))
-                recs.append(f.read(n * native.XREC_BYTES))
-                heaps.append(f.read(hb))
-                seg_r.append(n)
-                seg_h.append(hb)
+            rec, heap = read_rec(_rec_path(m, r, self.cwd))
+            recs.append(rec)
+            heaps.append(heap)
+            seg_r.append(len(rec) // native.XREC_BYTES)
+            seg_h.append(len(heap))
         out = self._reduce_records(r, b"".join(recs), b"".join(heaps), seg_r, seg_h)
         with open(os.path.join(self.cwd, f"mr-{r}.txt"), "wb") as f:       # worker.rs:167-168
             f.write(out)

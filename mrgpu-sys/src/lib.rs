@@ -24,7 +24,7 @@ pub const fn mrg_flag_debug_hash_bits(n: u32) -> u32 {
     (n & 0xFF) << 8
 }
 pub const MRG_XREC_BYTES: usize = 24;
-pub const MRG_ABI_VERSION: u32 = 3;
+pub const MRG_ABI_VERSION: u32 = 4;
 pub const MRG_COMM_ID_BYTES: usize = 128;
 
 #[repr(C)]
@@ -60,6 +60,10 @@ pub struct mrg_stats {
     pub exchange_sent: u64,
     pub exchange_recv: u64,
     pub map_spill: u64,
+    pub nonascii_tiles: u64,
+    pub tail_records_16: u64,
+    pub spec_agg: u32,
+    pub agg_path: u32,
 }
 
 #[repr(C)]

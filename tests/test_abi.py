@@ -48,12 +48,12 @@ def test_no_gpu_is_a_clean_error():
 
 def test_record_layout_constant():
     src = open(os.path.join(ROOT, "include", "mrgpu.h")).read()
-    assert "#define MRG_XREC_BYTES 24" in src and "#define MRG_ABI_VERSION 3" in src
+    assert "#define MRG_XREC_BYTES 24" in src and "#define MRG_ABI_VERSION 4" in src
     from mapreduce_rust_amd import native, shuffle
     assert native.XREC_BYTES == shuffle.XREC == 24 and native.ABI_VERSION == 3
-    assert b"abi 3" in native.load().mrg_version()
+    assert b"abi 4" in native.load().mrg_version()
     rs = open(os.path.join(ROOT, "mrgpu-sys", "src", "lib.rs")).read()
-    assert "pub const MRG_XREC_BYTES: usize = 24;" in rs and "pub const MRG_ABI_VERSION: u32 = 3;" in rs
+    assert "pub const MRG_XREC_BYTES: usize = 24;" in rs and "pub const MRG_ABI_VERSION: u32 = 4;" in rs
 
 
 def test_merge_sorted_lines_host():
@@ -102,3 +102,34 @@ def test_rust_ffi_crate_declares_the_header():
     stats_c = re.findall(r"^\s+(?:uint64_t|uint32_t|double)\s+(\w+);", hdr.split("} mrg_stats;")[0], re.M)
     stats_rs = re.findall(r"pub (\w+): (?:u64|u32|f64),", rs.split("pub struct mrg_stats")[1].split("}")[0])
     assert stats_c == stats_rs
+
+
+def test_rec_file_header_checks(tmp_path):
+    """mr-{m}-{r}.rec (worker.py, intermediates="records"): magic + format + record size in the header;
+    a stale 16-byte-header file, a wrong format and a truncated body are refused before any import."""
+    import struct
+    from mapreduce_rust_amd import native, worker as W
+    X = native.XREC_BYTES
+    p = str(tmp_path / "mr-0-0.rec")
+    rec, heap = bytes(range(X)) * 3, b"abcdefghijklmnopq"
+    W.write_rec(p, rec, heap)
+    assert W.read_rec(p) == (rec, heap)
+    with open(p, "wb") as f:                                   # the round-3 layout: <u64 n, u64 heap>
+        f.write(struct.pack("<QQ", 3, len(heap)) + rec + heap)
+    with pytest.raises(W.RecFileError, match="not an mrgpu record file"):
+        W.read_rec(p)
+    with open(p, "wb") as f:
+        f.write(struct.pack("<8sIIQQ", W.REC_MAGIC, 1, 40, 3, 0) + bytes(120))
+    with pytest.raises(W.RecFileError, match="record format 1"):
+        W.read_rec(p)
+    W.write_rec(p, rec, heap)
+    data = open(p, "rb").read()
+    for cut in (10, len(data) - 1):
+        with open(p, "wb") as f:
+            f.write(data[:cut])
+        with pytest.raises(W.RecFileError):
+            W.read_rec(p)
+    with open(p, "wb") as f:
+        f.write(data + b"x")
+    with pytest.raises(W.RecFileError, match="does not match"):
+        W.read_rec(p)

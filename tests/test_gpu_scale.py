@@ -149,6 +149,51 @@ def test_map_spill_and_rerun_vs_oracle(ctx, corpus, knobs, wide):
     assert st["map_launches"] >= 2, st
 
 
+def test_speculative_aggregation_paths_vs_oracle(ctx, corpus, knobs):
+    """The bucket aggregation queued behind the map before the host has read the map's counters
+    (mrgpu.cpp job_map): on a context whose previous job took the bucket path it is launched, then
+    reused (spec_agg 1) or dropped (spec_agg 2) -- with MRG_WIDE unset, on the map-rerun path
+    (tail regions of 1 record, 16-record overflow lists), the aggregation-regrow path (overflow list of
+    1000 records, 4-bit hashes) and with sub-ranges; every output against the oracle."""
+    import torch
+    import mapreduce_rust_amd as M
+    import oracle_lib as O
+    from gpu_util import run_wc
+    n = 16 * MIB
+    t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
+    ctx.gen_zipf(t.data_ptr(), n, 0x5EED2026, 9, 1 << 16, 1.1)
+    docs = corpus[:3] + [t[:n].cpu().numpy().tobytes()]
+    exp = O.wc(docs, 10, O.FAST)
+
+    def primed(**kw):  # a plain job first: it takes the bucket path, so the next job queues the launch
+        knobs()
+        assert run_wc(ctx, docs, 10) == exp
+        assert ctx.stats()["agg_path"] == 1
+        knobs(**kw)
+        got = run_wc(ctx, docs, 10)
+        return got, ctx.stats()
+
+    got, st = primed()
+    assert got == exp and st["spec_agg"] == 1 and st["agg_path"] == 1, st
+    got, st = primed(MRG_TEST_TAIL_CAP=1, MRG_TEST_OVF_CAP=16)   # map rerun: the queued launch is dropped
+    assert got == exp and st["map_launches"] >= 2 and st["spec_agg"] == 2, st
+    got, st = primed(MRG_TEST_AGG_NSUB=3)                        # launched with the forced sub-ranges
+    assert got == exp and st["spec_agg"] == 1, st
+    got, st = primed(MRG_WIDE=0)
+    assert got == exp and st["spec_agg"] == 1, st
+    knobs()
+    run_wc(ctx, corpus, 10, flags=M.debug_hash_bits(4))
+    knobs(MRG_TEST_AGG_OCAP=1000)                                # reused, then its overflow list regrown
+    got = run_wc(ctx, corpus, 10, flags=M.debug_hash_bits(4))
+    st = ctx.stats()
+    assert got == O.wc(corpus, 10, O.FAST)
+    assert st["spec_agg"] == 1 and st["agg_launches"] >= 2 and st["overflow_keys"] > 1000, st
+    knobs(MRG_WIDE=1)                                            # forced wide: nothing queued
+    assert run_wc(ctx, docs, 10) == exp
+    st = ctx.stats()
+    assert st["spec_agg"] == 0 and st["agg_path"] == 2, st
+
+
 def test_aggregation_overflow_regrow_vs_oracle(ctx, corpus, knobs):
     """Every key in one bucket (4-bit internal hashes), the HBM overflow list of the bucket
     aggregation started at 1000 records: it overflows, is regrown and the aggregation reruns."""
