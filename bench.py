@@ -6,7 +6,13 @@ Workload (N = 1): configs[2] = C3, wc on 10 GiB of synthetic Zipf(1.1) ASCII tex
 vocabulary 2^20, nReduce = 64), generated in HBM.  N > 1: C4's shape, 50 files (12.5 GiB) per GPU
 (400 files = 100 GiB at N = 8), nReduce = 64, owner(r) = r % N, the shuffle = libmrgpu.so's own RCCL
 exchange over xGMI (mrg_job_shuffle; torch.distributed only hands out the communicator id).
-Weak scaling: per-GPU work is fixed.  --workload unique: configs[4] (C5), near-unique 12-char keys.
+Weak scaling: per-GPU work is fixed.  --workload unique: configs[4] (C5), near-unique 12-char keys;
+--workload zipf_u: the C3 text with Gutenberg-like Unicode (the reference corpus's kind of text).
+
+The default N = 1 run adds, beside the C3 line: the end-to-end leg (files on disk -> mrg_run_job), a
+zipf_u sub-object (k_map GB/s on Unicode text against the ASCII rate), a c5 sub-object (configs[4] at
+50 x 256 MiB, 3 timed steps), a c2 sub-object (the indexer's latency on the bundled corpus,
+configs[1]) and the CPU baseline; --quick leaves all of them out.
 
 A step = one whole job over the resident input: map (tokenize + combine) -> aggregate + SipHash
 partition -> [shuffle] -> sort -> format; the output bytes of every mr-{r}.txt are in HBM at the end
@@ -46,7 +52,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["zipf", "unique"], default="zipf")
+    ap.add_argument("--workload", choices=["zipf", "zipf_u", "unique"], default="zipf",
+                    help="zipf: C3 ASCII; zipf_u: the same Zipf text with Gutenberg-like Unicode; unique: C5")
     ap.add_argument("--files-per-gpu", type=int, default=0, help="0: 40 at N=1 (C3), 50 at N>1 (C4)")
     ap.add_argument("--file-mib", type=int, default=256)
     ap.add_argument("--reduce", type=int, default=64)
@@ -57,6 +64,11 @@ def parse():
     ap.add_argument("--cpu-w1-mib", type=int, default=128, help="C3 slice for the W = 1 CPU run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end leg (files on disk -> mrg_run_job)")
+    ap.add_argument("--no-zipf-u", action="store_true", help="skip the Gutenberg-like Unicode leg (N = 1)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 leg (N = 1)")
+    ap.add_argument("--no-c2", action="store_true", help="skip the C2 indexer latency leg (N = 1)")
+    ap.add_argument("--quick", action="store_true", help="the headline C3 line only (no extra legs)")
+    ap.add_argument("--c5-files", type=int, default=50, help="C5 leg: 256 MiB files (50 = configs[4]'s 1e9 keys)")
     ap.add_argument("--lds-cap", type=int, default=0)
     ap.add_argument("--shuffle-1", action="store_true",
                     help="N = 1 only: run the library's RCCL shuffle in a one-rank communicator every step (the "
@@ -175,6 +187,189 @@ def end_to_end(buf, files, fbytes, n_reduce):
         shutil.rmtree(d, ignore_errors=True)
 
 
+WL_LABEL = {"zipf": "C3: wc, Zipf(%.2f) ASCII text, vocab %d",
+            "zipf_u": "C3 text with Gutenberg-like Unicode (U+2019/201C/201D/2014, U+00E9): wc, Zipf(%.2f), vocab %d",
+            "unique": "C5: near-unique 12-char keys (1% repeats)"}
+
+
+def generate(ctx, buf, workload, files, fbytes, rank, a, dev, quiet=False):
+    for i in range(files):
+        fi = rank * files + i
+        p = buf.data_ptr() + i * fbytes
+        if workload == "zipf":
+            ctx.gen_zipf(p, fbytes, a.seed, fi, a.vocab, a.zipf_s)
+        elif workload == "zipf_u":
+            ctx.gen_text(p, fbytes, a.seed, fi, a.vocab, a.zipf_s, 1)
+        else:
+            ctx.gen_unique(p, fbytes, a.seed, fi)
+        if rank == 0 and not quiet and (i % 8 == 7 or i == files - 1):
+            torch.cuda.synchronize(dev)
+            log(f"generated {i + 1}/{files} {workload} files of {fbytes // MIB} MiB")
+    torch.cuda.synchronize(dev)
+
+
+def time_steps(ctx, step, steps, warmup, dev, world, rank, label):
+    """W untimed warmup steps, then K steps bracketed by a barrier + synchronize on both sides; per-step
+    wall times (max over ranks) and the library's per-stage stats of every timed step."""
+    for w in range(warmup):
+        t_w = time.perf_counter()
+        step()
+        if rank == 0:
+            log(f"{label} warmup {w + 1}/{warmup}: {time.perf_counter() - t_w:.3f} s  {ctx.stats()}")
+    # kernel time of every stage: HIP events on the library's stream (= torch's current stream)
+    ctx.set_timing(True)
+    stats, step_s = [], []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ts = time.perf_counter()
+        step()
+        step_s.append(time.perf_counter() - ts)
+        s = ctx.stats()
+        stats.append(s)
+        if rank == 0:
+            log(f"{label} step: map {s['ms_map']:.2f} ms ({s['map_launches']} launch), agg {s['ms_aggregate']:.2f}, "
+                f"sort {s['ms_sort']:.2f}, format {s['ms_format']:.2f}"
+                + (f", exchange {s['ms_exchange']:.2f}" if world > 1 else "")
+                + f"; wall {step_s[-1] * 1e3:.2f}")
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ctx.set_timing(False)
+    t = torch.tensor([dt] + step_s, dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t[0].item(), t[1:].tolist(), stats
+
+
+def med(stats, k):
+    return statistics.median(s[k] for s in stats)
+
+
+def stage_roofline(stats, shard, out_bytes):
+    """Per-stage roofline: median HIP-event ms of each stage, its
+    algorithmic bytes per job, achieved GB/s and fraction of HBM peak; PMC bytes per job from
+    profiles/stage_traffic.json when it was measured on these kernel sources and this input size."""
+    st = stats[-1]
+    keys, tail, t16 = st["distinct_keys"], st["map_records"], st["tail_records_16"]
+    rec_bytes = 12 * (tail - t16) + 16 * t16
+    algo = {
+        "map": (shard, "input bytes, read once"),
+        "aggregate": (rec_bytes + 36 * keys, "tail records read (12 or 16 B each) + 36 B per distinct key written"),
+        "sort": (5 * 32 * keys, "a 32-B sort record per key: written, read + written by the scatter, by the leaf sort"),
+        "format": (out_bytes + 2 * 32 * keys, "output bytes written + the sort records read twice (lengths, write)"),
+    }
+    ms_key = {"map": "ms_map", "aggregate": "ms_aggregate", "sort": "ms_sort", "format": "ms_format"}
+    pmc, note = None, "no PMC measurement for these kernel sources"
+    tpath = os.path.join(ROOT, "profiles", "stage_traffic.json")
+    if os.path.exists(tpath):
+        tj = json.load(open(tpath))
+        if tj.get("kernel_src_sha") != M.native.kernel_source_sha():
+            note = "profiles/stage_traffic.json was measured on other kernel sources: not reported"
+        elif tj.get("input_bytes") != shard:
+            note = "profiles/stage_traffic.json was measured on another input size: not reported"
+        else:
+            pmc = tj
+            note = ("rocprofv3 PMC of these kernel sources (kernel_src_sha %s): per job, 2 x FETCH_SIZE + WRITE_SIZE "
+                    "over the stage's kernels, profiles/stage_traffic.json" % tj["kernel_src_sha"])
+    stages = {}
+    for k, (b, what) in algo.items():
+        ms = med(stats, ms_key[k])
+        ach = b / (ms / 1e3) / 1e9 if ms > 0 else None
+        stages[k] = {"ms_median": round(ms, 3), "algorithmic_bytes": int(b), "algorithmic": what,
+                     "achieved_gbs": round(ach, 1) if ach else None,
+                     "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
+                     "pmc_bytes": pmc["stage_hbm_bytes"].get(k) if pmc else None,
+                     "pmc_gbs": round(pmc["stage_hbm_bytes"][k] / (ms / 1e3) / 1e9, 1) if pmc and ms > 0 else None}
+    ratio = round(pmc["job_hbm_bytes"] / shard, 3) if pmc else None
+    return stages, ratio, note
+
+
+def leg(ctx, dev, a, workload, files, steps, warmup):
+    """An extra single-GPU workload (zipf_u, C5) on its own buffer, timed like the headline line."""
+    fbytes = a.file_mib * MIB
+    shard = files * fbytes
+    buf = torch.empty(shard + 64, dtype=torch.uint8, device=dev)
+    generate(ctx, buf, workload, files, fbytes, 0, a, dev, quiet=True)
+    doc_off = [i * fbytes for i in range(files + 1)]
+
+    def step():
+        ctx.job_begin(M.APP_WC, a.reduce)
+        ctx.set_input(buf.data_ptr(), doc_off)
+        ctx.map()
+        return ctx.reduce()
+
+    dt, step_max, stats = time_steps(ctx, step, steps, warmup, dev, 1, 0, workload)
+    del buf
+    torch.cuda.empty_cache()
+    m = statistics.median(step_max)
+    map_ms = med(stats, "ms_map")
+    st = stats[-1]
+    tiles = -(-shard // 1024)
+    return {"workload": WL_LABEL[workload] if workload == "unique" else WL_LABEL[workload] % (a.zipf_s, a.vocab),
+            "input_bytes": shard, "files": files, "n_reduce": a.reduce, "steps": steps, "warmup": warmup,
+            "value": round(shard / m / 1e9, 3), "unit": "GB/s", "ms_per_step": round(m * 1e3, 3),
+            "k_map_ms_median": round(map_ms, 3), "k_map_gbs": round(shard / (map_ms / 1e3) / 1e9, 1),
+            "stages_ms": {k: round(med(stats, k), 3) for k in ("ms_map", "ms_aggregate", "ms_sort", "ms_format")},
+            "tokens": st["tokens"], "long_tokens": st["long_tokens"], "map_records": st["map_records"],
+            "distinct_keys": st["distinct_keys"], "nonascii_tiles": st["nonascii_tiles"],
+            "nonascii_tile_frac": round(st["nonascii_tiles"] / tiles, 4), "agg_path": st["agg_path"]}
+
+
+def c2_latency(ctx, dev):
+    """configs[1]: the indexer (word -> sorted unique documents) on the bundled corpus, nReduce 10:
+    latency of the whole job with the corpus resident in HBM (median of 5, after one warmup) and
+    through mrg_run_job from files on disk (read + H2D + job + D2H + mr-{r}.txt writes)."""
+    c1 = [gzip.open(os.path.join(ROOT, "tests", "golden", "corpus", f"gut-{m}.txt.gz")).read() for m in range(6)]
+    names = [f"data/gut-{m}.txt" for m in range(6)]
+    off = [0]
+    for b in c1:
+        off.append(off[-1] + len(b))
+    buf = torch.frombuffer(bytearray(b"".join(c1) + bytes(64)), dtype=torch.uint8).to(dev)
+    lat = []
+    for i in range(6):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ctx.job_begin(M.APP_INDEXER, 10)
+        ctx.set_doc_names(names)
+        ctx.set_input(buf.data_ptr(), off)
+        ctx.map()
+        n_out = ctx.reduce()
+        if i:
+            lat.append((time.perf_counter() - t0) * 1e3)
+    st = ctx.stats()
+    d = tempfile.mkdtemp(prefix="mrg_c2_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        os.makedirs(os.path.join(d, "data"))
+        paths = []
+        for m, b in enumerate(c1):
+            pth = os.path.join(d, "data", f"gut-{m}.txt")
+            with open(pth, "wb") as f:
+                f.write(b)
+            paths.append(pth)
+        e2e = []
+        for i in range(6):
+            t0 = time.perf_counter()
+            M.native.run_job(paths, 10, M.APP_INDEXER, d)
+            if i:
+                e2e.append((time.perf_counter() - t0) * 1e3)
+    finally:
+        import shutil
+        shutil.rmtree(d, ignore_errors=True)
+    res = {"workload": "C2: indexer on the bundled corpus (6 files, 4.1 MB), nReduce 10",
+           "latency_ms_resident": round(statistics.median(lat), 3),
+           "latency_ms_end_to_end": round(statistics.median(e2e), 3),
+           "stages_ms": {k: round(st[k], 3) for k in ("ms_map", "ms_aggregate", "ms_sort", "ms_format")},
+           "distinct_keys": st["distinct_keys"], "output_bytes": n_out,
+           "note": "resident: job_begin .. reduce (output in HBM), median of 5 after a warmup; end_to_end: "
+                   "mrg_run_job over the 6 files on disk incl. the mr-{r}.txt writes, median of 5"}
+    log(f"C2 indexer: {res['latency_ms_resident']} ms resident, {res['latency_ms_end_to_end']} ms end to end")
+    return res
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -182,6 +377,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
+    if a.quick:
+        a.no_e2e = a.no_cpu_baseline = a.no_zipf_u = a.no_c5 = a.no_c2 = True
     gpu = local % max(1, torch.cuda.device_count())  # = local on a node with one GPU per rank
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -203,17 +400,7 @@ def main():
     if world == 1 and a.shuffle_1:
         comm = M.Comm(ctx, M.comm_id(), 1, 0)
     buf = torch.empty(shard + 64, dtype=torch.uint8, device=dev)
-    for i in range(files):
-        fi = rank * files + i
-        p = buf.data_ptr() + i * fbytes
-        if a.workload == "zipf":
-            ctx.gen_zipf(p, fbytes, a.seed, fi, a.vocab, a.zipf_s)
-        else:
-            ctx.gen_unique(p, fbytes, a.seed, fi)
-        if rank == 0 and (i % 8 == 7 or i == files - 1):
-            torch.cuda.synchronize(dev)
-            log(f"generated {i + 1}/{files} files of {a.file_mib} MiB")
-    torch.cuda.synchronize(dev)
+    generate(ctx, buf, a.workload, files, fbytes, rank, a, dev)
     doc_off = [i * fbytes for i in range(files + 1)]
     doc_ids = [rank * files + i for i in range(files)]
 
@@ -227,42 +414,9 @@ def main():
             S.shuffle(ctx, world, dev)    # host-staged rehearsal (gloo)
         return ctx.reduce()               # ends with a host read of the output size
 
-    for w in range(a.warmup):
-        t_w = time.perf_counter()
-        step()
-        if rank == 0:
-            log(f"warmup {w + 1}/{a.warmup}: {time.perf_counter() - t_w:.3f} s  {ctx.stats()}")
-    # kernel time of the dominant kernel: HIP events on the library's stream (= torch's current
-    # stream, set above) around every k_map launch
-    ctx.set_timing(True)
-    stats = []
-    step_s = []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    out_bytes = 0
-    for _ in range(a.steps):
-        ts = time.perf_counter()
-        out_bytes = step()
-        step_s.append(time.perf_counter() - ts)
-        s = ctx.stats()
-        stats.append(s)
-        if rank == 0:
-            log(f"step: map {s['ms_map']:.2f} ms ({s['map_launches']} launch), agg {s['ms_aggregate']:.2f}, "
-                f"sort {s['ms_sort']:.2f}, format {s['ms_format']:.2f}"
-                + (f", exchange {s['ms_exchange']:.2f}" if comm is not None or world > 1 else "")
-                + f"; wall {step_s[-1] * 1e3:.2f}")
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    ctx.set_timing(False)
-    t = torch.tensor([dt] + step_s, dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt, step_max = t[0].item(), t[1:].tolist()
-    med = statistics.median(step_max)
+    dt, step_max, stats = time_steps(ctx, step, a.steps, a.warmup, dev, world, rank, "")
+    out_bytes = ctx.stats()["output_bytes"]
+    m = statistics.median(step_max)
     st = ctx.stats()
 
     # D2H of the mr-{r}.txt bytes into a pinned host buffer (what a worker writing the files pays
@@ -277,9 +431,8 @@ def main():
     d2h_ms = (time.perf_counter() - td) * 1e3
     del host_out
 
-    value = shard * world / med / 1e9
-    map_ms = [s["ms_map"] for s in stats]
-    med_map_ms = statistics.median(map_ms)
+    value = shard * world / m / 1e9
+    med_map_ms = med(stats, "ms_map")
     achieved = shard / (med_map_ms / 1e3) / 1e9  # algorithmic bytes per k_map launch = input bytes read once
     traffic, traffic_note = None, "no PMC measurement for this kernel source"
     tpath = os.path.join(ROOT, "profiles", "map_traffic.json")
@@ -293,15 +446,15 @@ def main():
             traffic = tj.get("hbm_bytes_per_launch")
             traffic_note = ("rocprofv3 PMC of this kernel source (kernel_src_sha %s): 2 x FETCH_SIZE + WRITE_SIZE "
                             "per k_map launch, profiles/map_traffic.json" % tj["kernel_src_sha"])
+    stages, job_ratio, stages_note = stage_roofline(stats, shard, out_bytes)
 
     # xGMI roofline of the exchange (N > 1 over RCCL): peer bytes per rank (max of sent and received)
     # / the HIP-event time of the send/recv group, against (N - 1) links x 153 GB/s one way (each GPU
     # of the node has a direct link to each peer).  Max over ranks of time and bytes.
     xgmi = None
     if comm is not None and world > 1:
-        ex_ms = statistics.median(s["ms_exchange"] for s in stats)
-        ex_b = max(statistics.median(s["exchange_sent"] for s in stats),
-                   statistics.median(s["exchange_recv"] for s in stats))
+        ex_ms = med(stats, "ms_exchange")
+        ex_b = max(med(stats, "exchange_sent"), med(stats, "exchange_recv"))
         tx = torch.tensor([ex_ms, ex_b], dtype=torch.float64, device=dev)
         dist.all_reduce(tx, op=dist.ReduceOp.MAX)
         ex_ms, ex_b = tx.tolist()
@@ -311,10 +464,14 @@ def main():
                 "peak": peak, "unit": "GB/s", "frac": round(ach / peak, 4),
                 "note": "libmrgpu RCCL send/recv group: max-over-ranks peer bytes / HIP-event time (median step)"}
 
-    wl = {"zipf": ("C3: wc, Zipf(%.2f) ASCII text, vocab %d" % (a.zipf_s, a.vocab)) if world == 1 else
-          ("C4: wc, Zipf(%.2f) text sharded over %d GPUs, %s shuffle"
-           % (a.zipf_s, world, "RCCL" if a.backend == "nccl" else "gloo (host-staged rehearsal)")),
-          "unique": "C5: near-unique 12-char keys (1% repeats)" + ("" if world == 1 else ", %d GPUs" % world)}
+    if a.workload == "unique":
+        wl = WL_LABEL["unique"] + ("" if world == 1 else ", %d GPUs" % world)
+    elif world == 1:
+        wl = WL_LABEL[a.workload] % (a.zipf_s, a.vocab)
+    else:
+        wl = ("C4: wc, Zipf(%.2f) %s text sharded over %d GPUs, %s shuffle"
+              % (a.zipf_s, "ASCII" if a.workload == "zipf" else "Gutenberg-like Unicode", world,
+                 "RCCL" if a.backend == "nccl" else "gloo (host-staged rehearsal)"))
     line = {
         "metric": "word-count input GB/s (whole node) at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 3),
@@ -322,32 +479,37 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": round(med * 1e3, 3),
+        "ms_per_step": round(m * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": wl[a.workload] + (" + one-rank RCCL shuffle rehearsal" if a.shuffle_1 and world == 1 else ""), "input_bytes_per_gpu": shard, "files_per_gpu": files,
+        "config": {"workload": wl + (" + one-rank RCCL shuffle rehearsal" if a.shuffle_1 and world == 1 else ""),
+                   "input_bytes_per_gpu": shard, "files_per_gpu": files,
                    "file_bytes": fbytes, "n_reduce": a.reduce, "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "kernel": "k_map (tokenize + LDS combine)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_note": traffic_note,
                      "algorithmic_bytes_per_launch": shard, "kernel_ms_median": round(med_map_ms, 3),
-                     "whole_job_frac": round(value / world / HBM_PEAK_GBS, 4)},
+                     "whole_job_frac": round(value / world / HBM_PEAK_GBS, 4),
+                     "stages": stages, "whole_job_traffic_ratio": job_ratio, "stages_note": stages_note},
         "xgmi": xgmi,
         "timing": {"value_basis": "median step (max over ranks)", "ms_per_step_mean": round(dt / a.steps * 1e3, 3),
                    "value_mean": round(shard * world * a.steps / dt / 1e9, 3),
                    "output_d2h_ms": round(d2h_ms, 3),
-                   "value_with_output_d2h": round(shard * world / (med + d2h_ms / 1e3) / 1e9, 3)},
-        "stages_ms": {k: round(statistics.median(s[k] for s in stats), 3)
-                      for k in ("ms_map", "ms_aggregate", "ms_sort", "ms_format")},
+                   "value_with_output_d2h": round(shard * world / (m + d2h_ms / 1e3) / 1e9, 3)},
+        "stages_ms": {k: round(med(stats, k), 3) for k in ("ms_map", "ms_aggregate", "ms_sort", "ms_format")},
         "job": {"tokens": st["tokens"], "map_records": st["map_records"], "distinct_keys": st["distinct_keys"],
-                "output_bytes": out_bytes, "map_launches": [s["map_launches"] for s in stats]},
+                "output_bytes": out_bytes, "map_launches": [s["map_launches"] for s in stats],
+                "nonascii_tiles": st["nonascii_tiles"], "spec_agg": [s["spec_agg"] for s in stats],
+                "agg_path": st["agg_path"]},
     }
-    if world == 1 and not a.no_e2e and a.workload == "zipf":
+    single = world == 1 and a.workload == "zipf" and not a.shuffle_1
+    if single and not a.no_e2e:
         line["end_to_end"] = end_to_end(buf, files, fbytes, a.reduce)
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "zipf":
+    cpu = None
+    if rank == 0 and single and not a.no_cpu_baseline:
         n = min(a.cpu_slice_mib * MIB, shard)
         host = buf[:n].cpu().numpy().tobytes()
         W = cpu_cores()
@@ -359,7 +521,25 @@ def main():
             cuts.append(j if j > 0 else cuts[-1])
         cuts.append(n)
         slice_files = [host[cuts[i]:cuts[i + 1]] for i in range(W)]
-        line["cpu_baseline"] = cpu_baseline(slice_files, min(a.cpu_w1_mib * MIB, n), a.reduce)
+        del host
+        cpu = (slice_files, min(a.cpu_w1_mib * MIB, n))
+    if single:
+        del buf
+        torch.cuda.empty_cache()
+        if not a.no_zipf_u:
+            u = leg(ctx, dev, a, "zipf_u", files, 5, 2)
+            u["k_map_vs_ascii"] = round(u["k_map_gbs"] / achieved, 4)
+            line["zipf_u"] = u
+            log(f"zipf_u: {u['value']} GB/s, k_map {u['k_map_gbs']} GB/s = {u['k_map_vs_ascii']} of ASCII, "
+                f"{u['nonascii_tile_frac']} of tiles non-ASCII")
+        if not a.no_c5:
+            c5 = leg(ctx, dev, a, "unique", a.c5_files, 3, 1)
+            line["c5"] = c5
+            log(f"C5: {c5['value']} GB/s ({c5['ms_per_step']} ms per step, {c5['distinct_keys']} keys)")
+        if not a.no_c2:
+            line["c2"] = c2_latency(ctx, dev)
+    if cpu is not None:
+        line["cpu_baseline"] = cpu_baseline(cpu[0], cpu[1], a.reduce)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if comm is not None:

@@ -241,6 +241,13 @@ void mrg_free(void *p);
  * written to d_dst[0 .. n_bytes).  Deterministic in (seed, file_index); see DESIGN.md. */
 int mrg_gen_zipf(mrg_ctx *ctx, uint8_t *d_dst, uint64_t n_bytes, uint64_t seed, uint64_t file_index,
                  uint32_t vocab, double s);
+/* The same Zipf text in a given style: MRG_TEXT_ASCII (= mrg_gen_zipf) or MRG_TEXT_GUTENBERG (the
+ * reference corpus's kind of Unicode: U+2019 apostrophes, U+201C/U+201D quotes, U+2014 dashes joining
+ * words, Latin-1 letters; about one non-ASCII codepoint per 150 bytes). */
+#define MRG_TEXT_ASCII 0
+#define MRG_TEXT_GUTENBERG 1
+int mrg_gen_text(mrg_ctx *ctx, uint8_t *d_dst, uint64_t n_bytes, uint64_t seed, uint64_t file_index,
+                 uint32_t vocab, double s, uint32_t style);
 /* Near-unique 12-character keys (BASELINE config C5): token i of file f, 1% repeats. */
 int mrg_gen_unique(mrg_ctx *ctx, uint8_t *d_dst, uint64_t n_bytes, uint64_t seed, uint64_t file_index);
 

@@ -7,6 +7,12 @@
 // (exercises wc.rs's delete-and-join); ' ' between tokens, '\n' after every 12th.  Tokens are laid
 // out by an exclusive scan of their lengths; the file is filled up to n_bytes with whole tokens and
 // padded with '\n'.
+// Style 1 ("zipf_u", Gutenberg-like Unicode; the reference corpus src/data/gut-*.txt has one non-ASCII
+// codepoint per ~190 bytes in its larger files, mostly U+2019/201C/201D/2014 and Latin-1 letters): the
+// same tokens, with the inner apostrophe written as U+2019, 1.5 % of tokens opened by U+201C and 1.5 %
+// closed by U+201D (deleted: not \w), 0.3 % followed by U+2014 instead of the separator (deleted, so
+// the two words join into one key) and 0.3 % with one letter replaced by U+00E9 (\w, a 2-byte key byte
+// pair).  About one non-ASCII codepoint per 150 bytes: nearly every 1 KiB tile holds one.
 // C5: near-unique keys: token i = 12 chars of [a-z0-9] from splitmix64(seed + i), 1% copies of an
 // earlier token.
 #include <string.h>
@@ -36,10 +42,12 @@ struct ZipfDev {
     const uint32_t *alias;
     uint32_t V;
     uint64_t seed, file;
+    uint32_t style;  // 0 ASCII, 1 Gutenberg-like Unicode
 };
 
 struct Tok {
     uint32_t w, len, punct, apos;  // punct: 0 or char; apos: 0 or position
+    uint32_t oq, cq, dash, acc;    // style 1: U+201C before, U+201D after, U+2014 as separator, U+00E9 at acc - 1
 };
 
 __device__ inline Tok zipf_token(const ZipfDev &z, uint64_t j) {
@@ -55,6 +63,17 @@ __device__ inline Tok zipf_token(const ZipfDev &z, uint64_t j) {
     const uint32_t ar = (uint32_t)((y >> 40) % 10000u);
     t.apos = (ar < 200u && wl >= 2u) ? 1u + (uint32_t)((y >> 8) % (wl - 1u)) : 0u;
     t.len = wl + (t.punct ? 1u : 0u) + (t.apos ? 1u : 0u) + 1u;  // + separator
+    t.oq = t.cq = t.dash = t.acc = 0;
+    if (z.style == 1) {
+        const uint64_t u2 = splitmix64(y);
+        t.oq = (uint32_t)(u2 % 10000u) < 150u;
+        t.cq = (uint32_t)((u2 >> 14) % 10000u) < 150u;
+        t.dash = (uint32_t)((u2 >> 28) % 10000u) < 30u;
+        t.acc = (uint32_t)((u2 >> 42) % 10000u) < 30u ? 1u + (uint32_t)((u2 >> 56) % wl) : 0u;
+        // U+2019 is 3 bytes (the ASCII apostrophe was 1), the quotes 3 each, U+2014 replaces the 1-byte
+        // separator, U+00E9 replaces one letter
+        t.len += (t.apos ? 2u : 0u) + 3u * (t.oq + t.cq) + (t.dash ? 2u : 0u) + (t.acc ? 1u : 0u);
+    }
     return t;
 }
 
@@ -71,12 +90,20 @@ __global__ void k_zipf_write(ZipfDev z, uint64_t J, const uint64_t *off, uint8_t
     if (o + t.len > n) return;
     uint8_t *p = dst + o;
     const uint32_t a = z.voff[t.w], wl = z.voff[t.w + 1] - a;
+    auto put3 = [&](uint32_t b2) { p[0] = 0xE2; p[1] = 0x80; p[2] = (uint8_t)b2; p += 3; };
+    if (t.oq) put3(0x9C);  // U+201C
     for (uint32_t k = 0; k < wl; ++k) {
-        if (t.apos && k == t.apos) *p++ = '\'';
-        *p++ = z.vocab[a + k];
+        if (t.apos && k == t.apos) {
+            if (z.style == 1) put3(0x99);  // U+2019
+            else *p++ = '\'';
+        }
+        if (t.acc && k == t.acc - 1) { p[0] = 0xC3; p[1] = 0xA9; p += 2; }  // U+00E9
+        else *p++ = z.vocab[a + k];
     }
     if (t.punct) *p++ = (uint8_t)t.punct;
-    *p = (j % 12u == 11u) ? '\n' : ' ';
+    if (t.cq) put3(0x9D);  // U+201D
+    if (t.dash) put3(0x94);  // U+2014 instead of the separator
+    else *p = (j % 12u == 11u) ? '\n' : ' ';
 }
 
 __global__ void k_unique_write(uint8_t *dst, uint64_t n, uint64_t seed, uint64_t first, uint64_t J) {
@@ -162,10 +189,10 @@ int build_zipf(uint64_t seed, uint32_t V, double s) {
 }  // namespace
 
 int mrg_gen_zipf_impl(uint8_t *dst, uint64_t n, uint64_t seed, uint64_t file_index, uint32_t vocab, double s,
-                      hipStream_t st) {
-    if (vocab < 1 || s <= 0) return -1;
+                      uint32_t style, hipStream_t st) {
+    if (vocab < 1 || s <= 0 || style > 1) return -1;
     if (build_zipf(seed, vocab, s)) return -1;
-    ZipfDev z{g_zipf.d_vocab, g_zipf.d_voff, g_zipf.d_prob, g_zipf.d_alias, vocab, seed, file_index};
+    ZipfDev z{g_zipf.d_vocab, g_zipf.d_voff, g_zipf.d_prob, g_zipf.d_alias, vocab, seed, file_index, style};
     const uint64_t J = n / 3 + 2;  // every token is >= 3 bytes: J tokens always overfill n bytes
     uint64_t *len = nullptr, *off = nullptr, *tmp = nullptr;
     if (hipMalloc(&len, J * 8) != hipSuccess) return -1;

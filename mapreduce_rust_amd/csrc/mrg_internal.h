@@ -352,6 +352,6 @@ void mrg_wide_launch_dense(const uint64_t *keys, const uint64_t *ocnt, const uin
                            hipStream_t s);
 
 // ---- k_gen.hip
-int mrg_gen_zipf_impl(uint8_t *dst, uint64_t n, uint64_t seed, uint64_t file_index, uint32_t vocab, double s,
+int mrg_gen_zipf_impl(uint8_t *dst, uint64_t n, uint64_t seed, uint64_t file_index, uint32_t vocab, double s, uint32_t style,
                       hipStream_t st);
 int mrg_gen_unique_impl(uint8_t *dst, uint64_t n, uint64_t seed, uint64_t file_index, hipStream_t st);

@@ -1127,6 +1127,7 @@ void job_map(mrg_ctx *c) {
     c->st.long_tokens = c->h_cnt[CNT_LONG];
     c->st.map_records = c->h_cnt[CNT_REC];
     c->st.nonascii_tiles = c->h_cnt[CNT_NONASCII];
+    c->st.tail_records_16 = c->h_cnt[CNT_REC];  // every tail record is 16 bytes (wc) in this layout
     const uint64_t errpos = c->h_cnt[CNT_ERRPOS];
     auto release_map = [&]() {
         agg_put(c, spec);
@@ -2586,8 +2587,19 @@ int mrg_gen_zipf(mrg_ctx *c, uint8_t *d_dst, uint64_t n_bytes, uint64_t seed, ui
     return guard([&] {
         if (!c || (n_bytes && !d_dst)) raise(MRG_EINVAL, "null argument");
         HIPCHK(hipSetDevice(c->device));
-        if (mrg_gen_zipf_impl(d_dst, n_bytes, seed, file_index, vocab, s, c->stream))
+        if (mrg_gen_zipf_impl(d_dst, n_bytes, seed, file_index, vocab, s, 0, c->stream))
             raise(MRG_EHIP, "zipf generator failed: %s", hipGetErrorString(hipGetLastError()));
+    });
+}
+
+int mrg_gen_text(mrg_ctx *c, uint8_t *d_dst, uint64_t n_bytes, uint64_t seed, uint64_t file_index, uint32_t vocab,
+                 double s, uint32_t style) {
+    return guard([&] {
+        if (!c || (n_bytes && !d_dst)) raise(MRG_EINVAL, "null argument");
+        if (style > MRG_TEXT_GUTENBERG) raise(MRG_EINVAL, "unknown text style %u", style);
+        HIPCHK(hipSetDevice(c->device));
+        if (mrg_gen_zipf_impl(d_dst, n_bytes, seed, file_index, vocab, s, style, c->stream))
+            raise(MRG_EHIP, "text generator failed: %s", hipGetErrorString(hipGetLastError()));
     });
 }
 

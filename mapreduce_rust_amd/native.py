@@ -118,6 +118,7 @@ _SIGS = {
     "mrg_free": (None, [_vp]),
     "mrg_gen_zipf": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_double]),
     "mrg_gen_unique": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64]),
+    "mrg_gen_text": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_double, C.c_uint32]),
 }
 
 
@@ -333,6 +334,10 @@ class Context:
     # ---- synthetic inputs (bench)
     def gen_zipf(self, dev_ptr, n_bytes, seed, file_index, vocab=1 << 20, s=1.1):
         _check(load().mrg_gen_zipf(self.h, dev_ptr, n_bytes, seed, file_index, vocab, s))
+
+    def gen_text(self, dev_ptr, n_bytes, seed, file_index, vocab=1 << 20, s=1.1, style=1):
+        """style 0: ASCII (= gen_zipf); 1: Gutenberg-like Unicode (MRG_TEXT_GUTENBERG)."""
+        _check(load().mrg_gen_text(self.h, dev_ptr, n_bytes, seed, file_index, vocab, s, style))
 
     def gen_unique(self, dev_ptr, n_bytes, seed, file_index):
         _check(load().mrg_gen_unique(self.h, dev_ptr, n_bytes, seed, file_index))

@@ -19,6 +19,8 @@ pub const MRG_APP_WC: c_int = 0;
 pub const MRG_APP_INDEXER: c_int = 1;
 
 pub const MRG_FLAG_NO_COMPAT_DROP_LAST: u32 = 0x1;
+pub const MRG_TEXT_ASCII: u32 = 0;
+pub const MRG_TEXT_GUTENBERG: u32 = 1;
 pub const MRG_FLAG_FINAL_TXT: u32 = 0x2;
 pub const fn mrg_flag_debug_hash_bits(n: u32) -> u32 {
     (n & 0xFF) << 8
@@ -133,6 +135,8 @@ extern "C" {
 
     pub fn mrg_gen_zipf(ctx: *mut mrg_ctx, d_dst: *mut u8, n_bytes: u64, seed: u64, file_index: u64, vocab: u32,
                         s: f64) -> c_int;
+    pub fn mrg_gen_text(ctx: *mut mrg_ctx, d_dst: *mut u8, n_bytes: u64, seed: u64, file_index: u64, vocab: u32,
+                        s: f64, style: u32) -> c_int;
     pub fn mrg_gen_unique(ctx: *mut mrg_ctx, d_dst: *mut u8, n_bytes: u64, seed: u64, file_index: u64) -> c_int;
 }
 

@@ -270,6 +270,31 @@ def test_zipf_synthetic_vs_oracle(ctx):
     assert got == exp
 
 
+@pytest.mark.parametrize("vocab,R", [(1 << 16, 64), (1 << 10, 7)])
+def test_zipf_unicode_synthetic_vs_oracle(ctx, vocab, R):
+    """Gutenberg-like Unicode Zipf text (mrg_gen_text style 1): wc and the indexer against the oracle."""
+    import torch
+    import mapreduce_rust_amd as M
+    import oracle_lib as O
+    from gpu_util import run_wc
+    n = 12 << 20
+    t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
+    ctx.gen_text(t.data_ptr(), n, 0x5EED2026, 1, vocab, 1.1, 1)
+    host = t[:n].cpu().numpy().tobytes()
+    host.decode("utf-8")  # the generator writes valid UTF-8
+    assert sum(1 for i in range(0, n, 1024) if max(host[i:i + 1024]) >= 0x80) > 0.9 * (n // 1024)
+    ctx.job_begin(M.APP_WC, R)
+    ctx.set_input(t.data_ptr(), [0, n])
+    ctx.map()
+    ctx.reduce()
+    assert ctx.outputs() == O.wc([host], R, O.FAST)
+    docs = [host[i * (n // 4):(i + 1) * (n // 4)] for i in range(4)]
+    docs = [d[d.index(b" ") + 1:] if i else d for i, d in enumerate(docs)]  # whole codepoints per document
+    docs = [d[:d.rindex(b" ")] for d in docs]
+    names = [f"data/u-{i}.txt" for i in range(4)]
+    assert run_wc(ctx, docs, R, app=M.APP_INDEXER, names=names) == O.indexer(docs, names, R)
+
+
 def test_unique_synthetic_vs_oracle(ctx):
     import torch
     import mapreduce_rust_amd as M

@@ -451,3 +451,28 @@ def test_wide_many_partitions_vs_oracle(ctx, knobs):
     knobs(MRG_WIDE=1)
     for R in (5000, 4096):
         assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST), R
+
+
+def test_zipf_unicode_256mib_vs_oracle(ctx):
+    """The C3 text with Gutenberg-like Unicode (bench --workload zipf_u: U+2019 apostrophes, U+201C/D
+    quotes, U+2014 joining words, U+00E9 letters) -- 256 MiB, nearly every 1 KiB tile non-ASCII, R = 64:
+    byte-identical to the oracle (wc.rs:7-10 is Unicode-exact)."""
+    import torch
+    import mapreduce_rust_amd as M
+    import oracle_lib as O
+    n = 256 * MIB
+    t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
+    ctx.gen_text(t.data_ptr(), n, 0x5EED2026, 3, 1 << 20, 1.1, 1)
+    torch.cuda.synchronize()
+    host = np.empty(n, dtype=np.uint8)
+    torch.from_numpy(host).copy_(t[:n])
+    ctx.job_begin(M.APP_WC, 64)
+    ctx.set_input(t.data_ptr(), [0, n])
+    ctx.map()
+    ctx.reduce()
+    got = ctx.outputs()
+    st = ctx.stats()
+    del t
+    assert st["nonascii_tiles"] > 0.9 * (n // 1024), st
+    exp = O.wc_mt([host], 64, threads=THREADS)
+    assert [sha(g) for g in got] == [sha(e) for e in exp]

@@ -4,7 +4,7 @@
 mkdir -p gpurun_out/ab
 for v in ${VARIANTS:-lib_variants/A lib lib_variants/A lib}; do
   MRG_LIB=$PWD/mapreduce_rust_amd/$v/libmrgpu.so timeout -k 10 200 python -u bench.py --steps ${STEPS:-8} --warmup 2 \
-    --no-cpu-baseline --no-e2e ${BENCH_ARGS} > gpurun_out/ab/run.log 2>&1 || exit $?
+    --quick ${BENCH_ARGS} > gpurun_out/ab/run.log 2>&1 || exit $?
   python3 - "$v" <<'PY'
 import json, re, sys, statistics
 lines = open("gpurun_out/ab/run.log").read().splitlines()

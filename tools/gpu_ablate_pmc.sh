@@ -9,10 +9,10 @@ export TMPDIR=/tmp
 CTRS=${CTRS:-"SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"}
 for a in ${ABLS:-32 64 4 0}; do
   MRG_ABLATE=$a timeout -s KILL 120 rocprofv3 --pmc $CTRS -d gpurun_out/abl -o abl$a --output-format csv -- \
-    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-e2e --files-per-gpu 4 > gpurun_out/abl/abl$a.log 2>&1 || exit $?
+    python3 bench.py --steps 1 --warmup 1 --quick --files-per-gpu 4 > gpurun_out/abl/abl$a.log 2>&1 || exit $?
   python3 tools/pmc_summary.py --dir gpurun_out/abl --glob "abl${a}_counter_collection.csv" --only k_map | sed "s/^/abl=$a /"
 done
 for a in ${ABLS:-32 64 4 0}; do
-  MRG_ABLATE=$a timeout -k 10 200 python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-e2e > gpurun_out/abl/t$a.log 2>&1 || exit $?
+  MRG_ABLATE=$a timeout -k 10 200 python3 -u bench.py --steps 5 --warmup 1 --quick > gpurun_out/abl/t$a.log 2>&1 || exit $?
   echo "abl=$a $(grep -o 'kernel_ms_median": [0-9.]*' gpurun_out/abl/t$a.log)"
 done

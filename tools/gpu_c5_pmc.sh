@@ -2,7 +2,7 @@
 # PMC passes (one rocprofv3 --pmc run each) over a short C5 bench (near-unique keys, FILES x 256 MiB).
 mkdir -p gpurun_out/c5pmc
 export TMPDIR=/tmp
-ARGS="--workload unique --files-per-gpu ${FILES:-8} --steps 1 --warmup 1 --no-cpu-baseline --no-e2e"
+ARGS="--workload unique --files-per-gpu ${FILES:-8} --steps 1 --warmup 1 --quick"
 i=0
 for ctrs in "FETCH_SIZE" "WRITE_SIZE" \
   "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES" \

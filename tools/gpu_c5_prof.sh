@@ -3,7 +3,7 @@
 mkdir -p gpurun_out/c5p
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/c5p -o c5 --output-format csv -- \
-    python3 bench.py --workload unique --files-per-gpu ${FILES:-40} --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > gpurun_out/c5p.log 2>&1 || exit $?
+    python3 bench.py --workload unique --files-per-gpu ${FILES:-40} --steps 3 --warmup 1 --quick > gpurun_out/c5p.log 2>&1 || exit $?
 grep "step:" gpurun_out/c5p.log | tail -2
 python3 - <<'PY'
 import csv

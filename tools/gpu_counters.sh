@@ -11,4 +11,5 @@ mv gpurun_out/pmc gpurun_out/pmc_mix
 BENCH_ARGS="" bash tools/gpu_pmc.sh "FETCH_SIZE" "WRITE_SIZE" || exit $?
 mv gpurun_out/pmc gpurun_out/pmc_traffic
 python3 tools/pmc_summary.py --dir gpurun_out/pmc_mix > gpurun_out/pmc_mix_summary.txt
-python3 tools/pmc_summary.py --dir gpurun_out/pmc_traffic --traffic 10737418240 --out gpurun_out/map_traffic.json > gpurun_out/pmc_traffic_summary.txt
+python3 tools/pmc_summary.py --dir gpurun_out/pmc_traffic --traffic 10737418240 --out gpurun_out/map_traffic.json \
+  --stages 10737418240 --stages-out gpurun_out/stage_traffic.json > gpurun_out/pmc_traffic_summary.txt

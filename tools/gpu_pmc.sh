@@ -2,7 +2,7 @@
 # PMC counter passes (one rocprofv3 --pmc run each) over a short bench; CSV under gpurun_out/pmc.
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-e2e ${BENCH_ARGS}"
+ARGS="--steps 2 --warmup 1 --quick ${BENCH_ARGS}"
 i=0
 for ctrs in "$@"; do
   i=$((i+1))

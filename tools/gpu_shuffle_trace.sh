@@ -4,7 +4,7 @@
 mkdir -p gpurun_out/sht
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --runtime-trace --stats -d gpurun_out/sht -o sht --output-format csv -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --shuffle-1 ${BENCH_ARGS} > gpurun_out/sht.log 2>&1 || exit $?
+    python3 bench.py --steps 3 --warmup 1 --quick --shuffle-1 ${BENCH_ARGS} > gpurun_out/sht.log 2>&1 || exit $?
 grep "step:" gpurun_out/sht.log | tail -2
 ls gpurun_out/sht
 python3 tools/api_summary.py gpurun_out/sht > gpurun_out/sht_summary.txt 2>&1

@@ -2,4 +2,4 @@
 set -e
 name=$1; shift
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/kt_$name -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline "$@" > $GRAFT_REPO_ROOT/gpurun_out/kt_$name.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/kt_$name -o run -- python3 $GRAFT_REPO_ROOT/bench.py --quick "$@" > $GRAFT_REPO_ROOT/gpurun_out/kt_$name.log 2>&1
