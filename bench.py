@@ -330,6 +330,7 @@ def c2_latency(ctx, dev):
         off.append(off[-1] + len(b))
     buf = torch.frombuffer(bytearray(b"".join(c1) + bytes(64)), dtype=torch.uint8).to(dev)
     lat = []
+    ctx.set_timing(True)
     for i in range(6):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
@@ -341,6 +342,7 @@ def c2_latency(ctx, dev):
         if i:
             lat.append((time.perf_counter() - t0) * 1e3)
     st = ctx.stats()
+    ctx.set_timing(False)
     d = tempfile.mkdtemp(prefix="mrg_c2_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
         os.makedirs(os.path.join(d, "data"))

@@ -573,6 +573,11 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ unsigned long long s_tend[MRG_NBUCKET];  // end of that region
     __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
     __shared__ uint32_t s_next, s_ngen;                  // next block of the workgroup's share; list length
+    __shared__ uint32_t s_nuni;                          // non-ASCII tiles tokenized with UTF-8-exact masks
+    // the class table's blocks for U+0000..U+07FF (2-byte codepoints: Latin-1, Latin Extended, Greek,
+    // Cyrillic, ...) and U+2000..U+20FF (General Punctuation: the quotes and dashes of English text),
+    // 2 bits per codepoint; other codepoints read the global table
+    __shared__ uint8_t s_uc[9 * 64];
     __shared__ uint32_t s_tot[2];                        // workgroup totals: tokens, tail records
     __shared__ unsigned int s_fill;                      // table slots claimed
     __shared__ unsigned int s_door[MRG_MAP_DOOR ? LdsTable<CAP, IDX>::DW : 1];  // admission bitmap
@@ -598,9 +603,14 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     if (tid == 0) {
         s_next = 0;
         s_ngen = 0;
+        s_nuni = 0;
         s_tot[0] = 0;
         s_tot[1] = 0;
         s_fill = 0;
+    }
+    if (tid < 9 * 64) {
+        const uint32_t blk = tid < 512 ? (uint32_t)tid >> 6 : 0x20u;
+        s_uc[tid] = c_uclass_stage2[c_uclass_stage1[blk] * 64u + ((uint32_t)tid & 63u)];
     }
     if (tid < 512) {
         const uint32_t c = mrg_uclass((uint32_t)tid & 127u);
@@ -706,6 +716,85 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
 #else
 #define MRG_PT(i)
 #endif
+    // ---- UTF-8-exact byte classes for tiles with non-ASCII bytes (lane-divergent; only where a lane's
+    // bytes are not all ASCII).  Tile offsets t are relative to the tile start At; the wave's window
+    // holds [At - 16, At + 1024 + 64), and lo_t / hi_t bound it to the document.
+    auto wbyte = [&](int t) -> uint32_t { return (uint32_t)win[t + BEHIND]; };
+    auto uclass_lds = [&](uint32_t cp) -> uint32_t {
+        uint32_t byte;
+        if (cp < 0x800u) byte = s_uc[cp >> 2];
+        else if ((cp >> 8) == 0x20u) byte = s_uc[512u + ((cp & 255u) >> 2)];
+        else return mrg_uclass(cp);
+        return (byte >> (2u * (cp & 3u))) & 3u;
+    };
+    // the codepoint holding the non-ASCII byte at q: lead at most 3 bytes back (not before lo_t),
+    // length and class; false where the bytes are not valid UTF-8 (the exact walker reports them)
+    auto cp_at = [&](int q, int lo_t, int hi_t, int &lead, int &n, uint32_t &cls) -> bool {
+        int l = q, k = 0;
+        while (mrg_is_cont(wbyte(l))) {
+            if (k == 3 || l - 1 < lo_t) return false;
+            --l;
+            ++k;
+        }
+        uint32_t cp, raw;
+        auto rd = [&](uint64_t a) -> uint32_t { return (uint32_t)win[a]; };
+        n = mrg_utf8_decode(rd, (uint64_t)(l + BEHIND), (uint64_t)(hi_t + BEHIND), &cp, &raw);
+        if (n == 0 || l + n <= q) return false;
+        lead = l;
+        cls = uclass_lds(cp);
+        return true;
+    };
+    // W16 | S16 << 16 of the 16 bytes x at tile offset so: the LUT classes mlut for ASCII bytes, the
+    // class of their codepoint for the others
+    auto fix_seg = [&](const uint4 &x, int so, uint32_t mlut, int lo_t, int hi_t, bool &bad) -> uint32_t {
+        auto hb = [](uint32_t d) { return ((((d & 0x80808080u) >> 7) * 0x00204081u) >> 21) & 0xFu; };
+        uint32_t nam = hb(x.x) | (hb(x.y) << 4) | (hb(x.z) << 8) | (hb(x.w) << 12);
+        const int vlo = max(lo_t - so, 0), vhi = min(hi_t - so, 16);
+        nam &= vhi > vlo ? (((1u << vhi) - 1u) & ~((1u << vlo) - 1u)) : 0u;
+        uint32_t W = mlut & 0xFFFFu & ~nam, S = (mlut >> 16) & ~nam;
+        while (nam) {
+            const int p = __builtin_ctz(nam);
+            int lead = 0, n = 0;
+            uint32_t c = 0;
+            if (!cp_at(so + p, lo_t, hi_t, lead, n, c)) {
+                bad = true;
+                break;
+            }
+            const int e = min(lead + n - so, 16);
+            const uint32_t span = ((1u << e) - 1u) & ~((1u << p) - 1u);
+            if (c == MRG_CLS_W) W |= span;
+            else if (c == MRG_CLS_S) S |= span;
+            nam &= ~span;
+        }
+        return W | (S << 16);
+    };
+    // a tile with non-ASCII bytes: every lane's segment mask m, the mask ma of the 16 bytes after the
+    // tile (lane 63) and whether the byte before the tile is White_Space (pv, lane 0)
+    auto uni_masks = [&](const uint4 &x, uint32_t &m, uint32_t mafter_lut, uint64_t At, uint64_t doc_lo,
+                         uint64_t doc_hi, uint32_t &ma, uint32_t &pv, bool &bad) {
+        const int lo_t = doc_lo > At ? (int)(doc_lo - At) : -(int)umin64(At - doc_lo, (uint64_t)BEHIND);
+        const int hi_t = (int)umin64(doc_hi - At, (uint64_t)(TILE + HALO));
+        m = fix_seg(x, SEG * lane, m, lo_t, hi_t, bad);
+        ma = mafter_lut;
+        pv = 0;
+        if (lane == 63) ma = fix_seg(reinterpret_cast<const uint4 *>(win)[1 + 64], TILE, mafter_lut, lo_t, hi_t, bad);
+        if (lane == 0) {
+            if (At <= doc_lo) {
+                pv = 1u;  // the document starts here
+            } else {
+                const uint32_t b = wbyte(-1);
+                if (b < 0x80u) {
+                    pv = (s_lut[0][b] >> 4) & 1u;
+                } else {
+                    int lead = 0, n = 0;
+                    uint32_t c = 0;
+                    if (!cp_at(-1, lo_t, hi_t, lead, n, c)) bad = true;
+                    pv = c == MRG_CLS_S ? 1u : 0u;
+                }
+            }
+        }
+    };
+
     auto process_blk = [&](const BlkInfo &I, const Blk &X, uint64_t cblk, auto &&mid) {
         const uint64_t Ab = I.Ab, doc_lo = I.doc_lo, doc_hi = I.doc_hi;
         const uint32_t docid = I.docid;
@@ -776,7 +865,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const bool last = j == NSUB - 1;
             const uint4 x = j == 0 ? X.v0 : X.v1;
             const uint4 xh = j == 0 ? X.v1 : X.e;  // halo source
-            const uint32_t m = j == 0 ? m0 : m1;
+            const uint32_t mlut = j == 0 ? m0 : m1;
             const uint32_t mprev = m0;
             // non-ASCII anywhere the fast path reads: the tile, the first halo segment, the byte before
             const bool nx = j == 0 ? n0 : n1;
@@ -784,32 +873,53 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const bool np = j == 0 ? ne : n0;
             const uint32_t hl = last ? 1u : 0u;  // lane holding the first halo segment
             const bool nonascii = nx || ((uint32_t)lane == hl && nh) || ((uint32_t)lane == (j ? 63u : 0u) && np);
-            if (__any(nonascii)) {  // recorded; processed after the main loop
-                if (lane == 0) {
-                    const uint32_t k = atomicAdd(&s_ngen, 1u);
-                    glist[k] = (uint32_t)((cblk - wlo_b) * NSUB + j);
-                }
-                continue;
-            }
+            const bool uni = __any(nonascii);  // wave-uniform
             const uint64_t t1 = umin64(At + (uint64_t)TILE, doc_hi);
             const uint64_t whi = umin64(t1 + (uint64_t)HALO, doc_hi);
             const uint64_t wbase = At - (uint64_t)BEHIND;
+            const uint32_t mafter = !last ? lane_u32(m1, 0) : mh;  // the 16 bytes after the tile
 
             // stage the tile and its 64-byte halo (the previous tile's readers are done: program order)
             wave_sync_lds();
             reinterpret_cast<uint4 *>(win)[1 + lane] = x;
             if (!last ? lane < 4 : (lane >= 1 && lane < 5))
                 reinterpret_cast<uint4 *>(win)[65 + (!last ? lane : lane - 1)] = xh;
-            // masks: this lane's segment and the next one (lane 63: the first halo segment)
-            uint32_t mn = from_next_lane(m);
-            if (lane == 63) mn = !last ? lane_u32(m1, 0) : mh;
+            uint32_t m = mlut, mn, prev;
+            if (!uni) {
+                // masks: this lane's segment and the next one (lane 63: the first halo segment)
+                mn = from_next_lane(m);
+                if (lane == 63) mn = mafter;
+                // token starts of this lane's segment: the previous byte's class from lane l-1 (lane 0:
+                // the previous tile's last byte); each start gets a queue slot by a wave prefix sum
+                prev = from_prev_lane(m) >> 31;
+                if (lane == 0) prev = j == 0 ? prev_blk : (lane_u32(mprev, 63) >> 31);
+            } else {
+                // A non-ASCII byte where the fast path reads: the LUT classes of the lanes whose bytes
+                // are not all ASCII are replaced by UTF-8-exact ones (uni_masks), after which the tile
+                // is tokenized exactly like an ASCII tile -- every byte of a codepoint carries its
+                // class, so the W / S masks mean the same.  Invalid UTF-8 (or anything the exact
+                // walker must report) defers the tile to generic_tile after the main loop.
+                if (lane == (j ? 63 : 0)) reinterpret_cast<uint4 *>(win)[0] = j ? X.v0 : X.e;  // the bytes before
+                wave_sync_lds();
+                bool bad = false;
+                uint32_t ma = 0, pv = 0;
+                uni_masks(x, m, mafter, At, doc_lo, doc_hi, ma, pv, bad);
+                if (__any(bad)) {  // recorded; processed after the main loop
+                    if (lane == 0) {
+                        const uint32_t k = atomicAdd(&s_ngen, 1u);
+                        glist[k] = (uint32_t)((cblk - wlo_b) * NSUB + j);
+                    }
+                    continue;
+                }
+                if (lane == 0) atomicAdd(&s_nuni, 1u);
+                mn = from_next_lane(m);
+                if (lane == 63) mn = ma;
+                prev = from_prev_lane(m) >> 31;
+                if (lane == 0) prev = pv;
+            }
             const uint32_t Wpair = (m & 0xFFFFu) | (mn << 16);
             const uint32_t Spair = (m >> 16) | (mn & 0xFFFF0000u);
             mp[lane] = (uint64_t)Wpair | ((uint64_t)Spair << 32);
-            // token starts of this lane's segment: the previous byte's class from lane l-1 (lane 0:
-            // the previous tile's last byte); each start gets a queue slot by a wave prefix sum
-            uint32_t prev = from_prev_lane(m) >> 31;
-            if (lane == 0) prev = j == 0 ? prev_blk : (lane_u32(mprev, 63) >> 31);
             const uint32_t S = m >> 16;
             uint32_t st = ~S & ((S << 1) | prev) & 0xFFFFu;
             if (l16 >= (uint32_t)(t1 - At)) st = 0;
@@ -1087,7 +1197,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     if (tid == 0) {
         g_add(&A.counters[CNT_TOKENS], (unsigned long long)s_tot[0]);
         g_add(&A.counters[CNT_REC], (unsigned long long)s_tot[1]);
-        if (s_ngen) g_add(&A.counters[CNT_NONASCII], (unsigned long long)s_ngen);
+        if (s_ngen + s_nuni) g_add(&A.counters[CNT_NONASCII], (unsigned long long)(s_ngen + s_nuni));
     }
     MRG_PT(6);
 #ifdef MRG_MAP_PROF
