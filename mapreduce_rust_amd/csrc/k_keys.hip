@@ -74,6 +74,7 @@ __device__ __forceinline__ GASK T *gk(T *p) {
     return (GASK T *)p;
 }
 typedef uint64_t u64x2k __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x3k __attribute__((ext_vector_type(3), aligned(4)));  // a 12-byte wc tail record
 
 // the map kernel's key hash (k_map.hip key_hash): bucket = top 9 bits
 __device__ __forceinline__ uint32_t ba_hash(uint64_t a, uint64_t b, uint32_t d, uint32_t hash_bits) {
@@ -200,7 +201,8 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
     // takes chunks wv, wv + 16, ..., so at any time the workgroup's 16 waves read 16 neighbouring chunks
     // (one stream of the bucket per workgroup; with a region per wave the 256 workgroups kept 4096
     // streams open at once)
-    const GASK uint64_t *pool = gk(A.pool) + A.rbase[b] * RW;
+    // the bucket's regions: 12-byte records (wc) / 24-byte records (indexer)
+    const GASK uint8_t *pool = reinterpret_cast<const GASK uint8_t *>(gk(A.pool)) + A.rbase[b] * MRG_TAIL_BYTES(IDX);
     struct Chunk {
         u64x2k k[BA_U];
         uint32_t d[IDX ? BA_U : 1];
@@ -213,16 +215,18 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
     // unconditional loads: an index past the region's end reads its last record (masked later)
     auto load_chunk = [&](uint32_t r, uint32_t off, Chunk &X) {
         const uint32_t n = s_rn[r];
-        const GASK uint64_t *src = pool + (uint64_t)r * cap * RW;
+        const GASK uint8_t *src = pool + (uint64_t)r * cap * MRG_TAIL_BYTES(IDX);
 #pragma unroll
         for (int k = 0; k < BA_U; ++k) {
             const uint32_t i = min(off + 64u * k + (uint32_t)lane, n - 1u);
             if (IDX) {
-                X.k[k] = u64x2k{src[(uint64_t)i * 3], src[(uint64_t)i * 3 + 1]};
-                X.d[k] = (uint32_t)src[(uint64_t)i * 3 + 2];
+                const GASK uint64_t *rec = reinterpret_cast<const GASK uint64_t *>(src) + (uint64_t)i * 3;
+                X.k[k] = u64x2k{rec[0], rec[1]};
+                X.d[k] = (uint32_t)rec[2];
             } else {
-                // read once: non-temporal (A/B: aggregation -1.5 %)
-                X.k[k] = __builtin_nontemporal_load(reinterpret_cast<const GASK u64x2k *>(src + (uint64_t)i * 2));
+                // read once: non-temporal (A/B: aggregation -1.5 %); {k0, high word of k1}
+                const u32x3k v = __builtin_nontemporal_load(reinterpret_cast<const GASK u32x3k *>(src + (uint64_t)i * 12u));
+                X.k[k] = u64x2k{(uint64_t)v.x | ((uint64_t)v.y << 32), (uint64_t)v.z << 32};
             }
         }
     };
@@ -380,6 +384,28 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
                     }
                     if (__any(ovf)) overflow(ovf, a[u], c[u], d[u], n2[u]);
                 }
+            }
+        }
+    }
+    // ---- 3a. wc keys of 13..16 bytes: the bucket's 16-byte regions, wave wv taking regions wv, wv + 16, ..
+    if (!IDX) {
+        const uint32_t cap16 = gk(A.bcap16)[b];
+        const GASK uint64_t *p16 = gk(A.pool16) + 2ull * A.rbase16[b];
+        for (uint32_t r = (uint32_t)wv; r < nreg; r += BA_NW) {
+            const uint32_t n = min(gk(A.bcount16)[(uint64_t)r * MRG_NBUCKET + b], cap16);
+            const GASK uint64_t *src = p16 + 2ull * r * cap16;
+            for (uint32_t base = 0; base < n; base += 64) {
+                const uint32_t i = base + (uint32_t)lane;
+                bool ovf = false;
+                uint64_t a = 0, c = 0;
+                if (i < n) {
+                    const u64x2k v = *reinterpret_cast<const GASK u64x2k *>(src + 2ull * i);
+                    a = v.x;
+                    c = v.y;
+                    const uint32_t h = ba_hash(a, c, MRG_EMPTY_DOC, A.hash_bits);
+                    if (mine(h)) ovf = !ba_add<IDX, C32>(s_key, s_cnt, s_doc, a, c, MRG_EMPTY_DOC, 1ull, h);
+                }
+                if (__any(ovf)) overflow(ovf, a, c, MRG_EMPTY_DOC, 1);
             }
         }
     }
@@ -550,7 +576,8 @@ __global__ void k_partition(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t
 // and equal keys are summed by a segmented scan.  The key set then comes out in output order, so the
 // reduce-side sort (worker.rs:162-164) is skipped.  wc only (no doc component).
 //
-// Segments: [nreg * NB tail regions, s = b * nreg + w] [nreg flush regions] [NB overflow lists].
+// Segments: [nreg * NB tail regions (12-byte records), s = b * nreg + w] [nreg flush regions]
+// [NB overflow lists] [nreg * NB 16-byte tail regions].
 __global__ void k_wide_counts(BucketArgs A, uint64_t *cnt) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t nt = (uint64_t)A.nreg * MRG_NBUCKET;
@@ -563,6 +590,10 @@ __global__ void k_wide_counts(BucketArgs A, uint64_t *cnt) {
     } else if (s < nt + A.nreg + MRG_NBUCKET) {
         const uint32_t b = (uint32_t)(s - nt - A.nreg);
         cnt[s] = min(A.monext[b], A.mocap);
+    } else if (s < 2 * nt + A.nreg + MRG_NBUCKET) {
+        const uint64_t s2 = s - nt - A.nreg - MRG_NBUCKET;
+        const uint32_t b = (uint32_t)(s2 / A.nreg), w = (uint32_t)(s2 % A.nreg);
+        cnt[s] = min(A.bcount16[(uint64_t)w * MRG_NBUCKET + b], A.bcap16[b]);
     }
 }
 
@@ -577,8 +608,15 @@ __global__ void k_wide_gather(BucketArgs A, const uint64_t *off, uint32_t n_redu
         if (s < nt) {
             const uint32_t b = (uint32_t)(s / A.nreg), w = (uint32_t)(s % A.nreg);
             const uint64_t j = A.rbase[b] + (uint64_t)w * A.bcap[b] + i;
-            k0 = A.pool[2 * j];
-            k1 = A.pool[2 * j + 1];
+            const uint32_t *rec = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(A.pool) + 12u * j);
+            k0 = (uint64_t)rec[0] | ((uint64_t)rec[1] << 32);
+            k1 = (uint64_t)rec[2] << 32;
+        } else if (s >= nt + A.nreg + MRG_NBUCKET) {
+            const uint64_t s2 = s - nt - A.nreg - MRG_NBUCKET;
+            const uint32_t b = (uint32_t)(s2 / A.nreg), w = (uint32_t)(s2 % A.nreg);
+            const uint64_t j = A.rbase16[b] + (uint64_t)w * A.bcap16[b] + i;
+            k0 = A.pool16[2 * j];
+            k1 = A.pool16[2 * j + 1];
         } else if (s < nt + A.nreg) {
             const uint64_t j = (s - nt) * A.regcap + i;
             k0 = A.fk0[j];

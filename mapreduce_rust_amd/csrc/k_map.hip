@@ -347,14 +347,36 @@ __device__ __forceinline__ bool walk_token(const RD &rd, uint64_t a, uint64_t do
 struct TailRegions {
     unsigned long long *cur;
     const unsigned long long *end;
+    unsigned long long *cur16;  // wc keys of 13..16 bytes: their own regions of 16-byte records
+    const unsigned long long *end16;
 };
+typedef uint32_t u32x3a __attribute__((ext_vector_type(3), aligned(4)));  // one 12-byte tail record
+
+// wc tail record i: keys of <= 12 bytes as 12 bytes {k0, high word of k1} in pool, longer ones as
+// {k0, k1} in pool16; the indexer's {k0, k1, doc} (24 B) in pool
+template <bool IDX>
+__device__ __forceinline__ void store_tail(GAS uint64_t *pool, GAS uint64_t *pool16, bool w16, uint64_t i, uint64_t k0,
+                                           uint64_t k1, uint32_t doc) {
+    if (IDX) {
+        GAS uint64_t *dst = pool + i * 3u;
+        dst[0] = k0;
+        dst[1] = k1;
+        dst[2] = doc;
+    } else if (w16) {
+        *reinterpret_cast<GAS u64x2 *>(pool16 + 2u * i) = u64x2{k0, k1};
+    } else {
+        *reinterpret_cast<GAS u32x3a *>(reinterpret_cast<GAS uint8_t *>(pool) + 12u * i) =
+            u32x3a{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)(k1 >> 32)};
+    }
+}
 
 // Two tokens per lane (a and b) through the LDS table in one instruction stream: the tag reads,
 // key reads, count adds and tail-cursor adds of both are issued back to back, so every LDS round
 // trip is paid once for two tokens.  Same semantics as emit_fast() applied to a, then b.
 template <int CAP, bool IDX>
 __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint32_t hbits, LdsTable<CAP, IDX> &T,
-                                           TailRegions R, GAS uint64_t *pool, bool ha, uint64_t a0, uint64_t a1,
+                                           TailRegions R, GAS uint64_t *pool, GAS uint64_t *pool16, bool ha,
+                                           uint64_t a0, uint64_t a1,
                                            bool hb, uint64_t b0, uint64_t b1, uint32_t docid, bool may_claim) {
     constexpr uint32_t NS = LdsTable<CAP, IDX>::NS;
     const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
@@ -362,9 +384,11 @@ __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint3
     const bool actA = ha && !(abl & 2u), actB = hb && !(abl & 2u);
     const uint32_t sA = actA ? (hA & (NS - 1)) : 0u, sB = actB ? (hB & (NS - 1)) : 0u;
     const uint32_t bA = bucket_of(hA), bB = bucket_of(hB);
+    // wc keys longer than 12 bytes (k1 low word non-zero) take the 16-byte regions
+    const bool wA = !IDX && (uint32_t)a1 != 0u, wB = !IDX && (uint32_t)b1 != 0u;
     // both ways of both sets: four 16-byte reads in flight together, with the two region ends
     const KeyPair kA0 = T.key[sA], kA1 = T.key[sA + NS], kB0 = T.key[sB], kB1 = T.key[sB + NS];
-    const uint64_t endA = R.end[bA], endB = R.end[bB];
+    const uint64_t endA = (wA ? R.end16 : R.end)[bA], endB = (wB ? R.end16 : R.end)[bB];
     auto eq = [&](const KeyPair &k, uint64_t x, uint64_t y, uint32_t s) {
         return (((k.a ^ x) | (k.b ^ y)) == 0) & (!IDX || T.doc[s] == dkey);
     };
@@ -390,20 +414,12 @@ __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint3
     // both appends in one region (a lane adds 0 to the other token's cursor): one LDS round trip
     uint64_t iA = 0, iB = 0;
     if (tA || tB) {
-        iA = atomicAdd(&R.cur[bA], tA ? 1ull : 0ull);
-        iB = atomicAdd(&R.cur[bB], tB ? 1ull : 0ull);
+        iA = atomicAdd(&(wA ? R.cur16 : R.cur)[bA], tA ? 1ull : 0ull);
+        iB = atomicAdd(&(wB ? R.cur16 : R.cur)[bB], tB ? 1ull : 0ull);
     }
     const bool okA = tA && iA < endA, okB = tB && iB < endB;
-    if (okA) {
-        GAS uint64_t *dst = pool + iA * (IDX ? 3u : 2u);
-        if (IDX) { dst[0] = a0; dst[1] = a1; dst[2] = docid; }
-        else *reinterpret_cast<GAS u64x2 *>(dst) = u64x2{a0, a1};
-    }
-    if (okB) {
-        GAS uint64_t *dst = pool + iB * (IDX ? 3u : 2u);
-        if (IDX) { dst[0] = b0; dst[1] = b1; dst[2] = docid; }
-        else *reinterpret_cast<GAS u64x2 *>(dst) = u64x2{b0, b1};
-    }
+    if (okA) store_tail<IDX>(pool, pool16, wA, iA, a0, a1, docid);
+    if (okB) store_tail<IDX>(pool, pool16, wB, iB, b0, b1, docid);
     const bool oA = tA && !okA, oB = tB && !okB;
     if (__any(oA || oB)) {  // region full (rare): the bucket's shared overflow list
         auto spill = [&](uint32_t b, uint64_t k0, uint64_t k1) {
@@ -442,23 +458,20 @@ __device__ __forceinline__ void emit(const MapArgs &A, LdsTable<CAP, IDX> &table
     }
     if (tail && !(map_ablate(A) & 1u)) {
         const uint32_t b = bucket_of(h);
-        const uint64_t end = R.end[b];
-        const uint64_t idx = atomicAdd(&R.cur[b], 1ull);
-        GAS uint64_t *dst = nullptr;
+        const bool w16 = !IDX && (uint32_t)tk1 != 0u;
+        const uint64_t end = (w16 ? R.end16 : R.end)[b];
+        const uint64_t idx = atomicAdd(&(w16 ? R.cur16 : R.cur)[b], 1ull);
         if (idx < end) {
-            dst = gp(A.pool) + idx * (IDX ? 3u : 2u);
-        } else {  // region full (rare): the bucket's shared overflow list
+            store_tail<IDX>(gp(A.pool), gp(A.pool16), w16, idx, tk0, tk1, docid);
+        } else {  // region full (rare): the bucket's shared overflow list (16-byte records, any key)
             const uint32_t j = g_add(&A.onext[b], 1u);
-            if (j < A.ocap) dst = gp(A.ovf) + ((uint64_t)b * A.ocap + j) * (IDX ? 3u : 2u);
-            else g_add(&A.counters[CNT_OVF], 1ull);
-        }
-        if (dst) {
-            if (IDX) {
+            if (j < A.ocap) {
+                GAS uint64_t *dst = gp(A.ovf) + ((uint64_t)b * A.ocap + j) * (IDX ? 3u : 2u);
                 dst[0] = tk0;
                 dst[1] = tk1;
-                dst[2] = docid;
+                if (IDX) dst[2] = docid;
             } else {
-                *reinterpret_cast<GAS u64x2 *>(dst) = u64x2{tk0, tk1};  // one 16-byte store
+                g_add(&A.counters[CNT_OVF], 1ull);
             }
         }
     }
@@ -571,6 +584,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ __attribute__((aligned(16))) unsigned int s_doc[IDX ? CAP : 1];
     __shared__ unsigned long long s_tcur[MRG_NBUCKET];  // next pool record of (bucket, this WG)
     __shared__ unsigned long long s_tend[MRG_NBUCKET];  // end of that region
+    __shared__ unsigned long long s_tcur16[IDX ? 1 : MRG_NBUCKET];  // wc: the 16-byte regions
+    __shared__ unsigned long long s_tend16[IDX ? 1 : MRG_NBUCKET];
     __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
     __shared__ uint32_t s_next, s_ngen;                  // next block of the workgroup's share; list length
     __shared__ uint32_t s_nuni;                          // non-ASCII tiles tokenized with UTF-8-exact masks
@@ -578,7 +593,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // Cyrillic, ...) and U+2000..U+20FF (General Punctuation: the quotes and dashes of English text),
     // 2 bits per codepoint; other codepoints read the global table
     __shared__ uint8_t s_uc[9 * 64];
-    __shared__ uint32_t s_tot[2];                        // workgroup totals: tokens, tail records
+    __shared__ uint32_t s_tot[3];                        // workgroup totals: tokens, tail records, 16-byte ones
     __shared__ unsigned int s_fill;                      // table slots claimed
     __shared__ unsigned int s_door[MRG_MAP_DOOR ? LdsTable<CAP, IDX>::DW : 1];  // admission bitmap
     static_assert(sizeof(s_q) >= CAP * sizeof(uint16_t), "flush ranks reuse the queues");
@@ -599,6 +614,12 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const uint64_t base = gp(A.rbase)[b] + (uint64_t)blockIdx.x * cap;
         s_tcur[b] = base;
         s_tend[b] = base + cap;
+        if (!IDX) {
+            const uint32_t cap16 = gp(A.bcap16)[b];
+            const uint64_t base16 = gp(A.rbase16)[b] + (uint64_t)blockIdx.x * cap16;
+            s_tcur16[b] = base16;
+            s_tend16[b] = base16 + cap16;
+        }
     }
     if (tid == 0) {
         s_next = 0;
@@ -606,6 +627,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         s_nuni = 0;
         s_tot[0] = 0;
         s_tot[1] = 0;
+        s_tot[2] = 0;
         s_fill = 0;
     }
     if (tid < 9 * 64) {
@@ -630,7 +652,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         s_sel[L * 17u + g][j] = ((0x00010203u + (gm & 0x01010101u)) & ~zm) | (0x0C0C0C0Cu & zm);
     }
     LdsTable<CAP, IDX> table{s_key, s_cnt, s_doc, s_door, &s_fill};
-    const TailRegions tails{s_tcur, s_tend};
+    const TailRegions tails{s_tcur, s_tend, s_tcur16, s_tend16};
     uint32_t my_tokens = 0;
     // uniform job parameters used in the hot loop, read once
     // ablation knobs (MRG_ABLATE, timing only) exist in -DMRG_MAP_ABLATION builds; in the product
@@ -642,6 +664,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
 #endif
     const uint32_t hbits = A.hash_bits;
     GAS uint64_t *const pool = gp(A.pool);
+    GAS uint64_t *const pool16 = gp(A.pool16);
     uint8_t *win = s_win[wv];
     uint64_t *mp = s_mp[wv];
     uint16_t *queue = s_q[wv];
@@ -1041,7 +1064,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                     nslow += na + (uint32_t)__builtin_popcountll(mb);
                 }
                 my_tokens += (fa ? 1u : 0u) + (fb ? 1u : 0u);
-                emit_fast2(A, abl, hbits, table, tails, pool, fa, a0, a1, fb, b0, b1, docid, may_claim);
+                emit_fast2(A, abl, hbits, table, tails, pool, pool16, fa, a0, a1, fb, b0, b1, docid, may_claim);
             }
             // deferred slow tokens: the exact per-codepoint walker, one token per lane (forward
             // reads only: the staged bytes are [At, whi))
@@ -1142,11 +1165,17 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __syncthreads();
     uint16_t *s_rank = &s_q[0][0];
     GAS uint32_t *bcount = gp(A.bcount) + (uint64_t)blockIdx.x * MRG_NBUCKET;
-    uint32_t my_tail = 0;
+    uint32_t my_tail = 0, my_tail16 = 0;
     for (int b = tid; b < MRG_NBUCKET; b += WG) {  // appends made (may exceed the capacity)
         const uint32_t n = (uint32_t)(s_tcur[b] - (s_tend[b] - gp(A.bcap)[b]));
         my_tail += n;
         bcount[b] = n;
+        if (!IDX) {
+            const uint32_t n16 = (uint32_t)(s_tcur16[b] - (s_tend16[b] - gp(A.bcap16)[b]));
+            my_tail += n16;
+            my_tail16 += n16;
+            gp(A.bcount16)[(uint64_t)blockIdx.x * MRG_NBUCKET + b] = n16;
+        }
     }
     for (int b = tid; b <= MRG_NBUCKET; b += WG) s_hist[b] = 0;
     __syncthreads();
@@ -1184,19 +1213,22 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     }
     // token and tail totals: waves -> LDS -> one device atomic per workgroup and counter (a wave
     // atomic each put 8 K atomics on two counters at the very end of the launch)
-    uint32_t t = my_tokens, ttl = my_tail;
+    uint32_t t = my_tokens, ttl = my_tail, t16 = my_tail16;
     for (int off = 32; off > 0; off >>= 1) {
         t += __shfl_down(t, off);
         ttl += __shfl_down(ttl, off);
+        t16 += __shfl_down(t16, off);
     }
     if (lane == 0) {
         atomicAdd(&s_tot[0], t);
         atomicAdd(&s_tot[1], ttl);
+        if (t16) atomicAdd(&s_tot[2], t16);
     }
     __syncthreads();
     if (tid == 0) {
         g_add(&A.counters[CNT_TOKENS], (unsigned long long)s_tot[0]);
         g_add(&A.counters[CNT_REC], (unsigned long long)s_tot[1]);
+        if (s_tot[2]) g_add(&A.counters[CNT_REC16], (unsigned long long)s_tot[2]);
         if (s_ngen + s_nuni) g_add(&A.counters[CNT_NONASCII], (unsigned long long)(s_ngen + s_nuni));
     }
     MRG_PT(6);

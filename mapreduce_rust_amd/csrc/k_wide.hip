@@ -108,20 +108,42 @@ typedef SplitIndex<12, uint16_t> LeafIndex;   // L2: <= 1023 leaf splitters per 
 typedef SplitIndex<8, uint8_t> L1Index;       // L1: <= 63 splitters per partition
 
 // ---------------------------------------------------------------- the map's records (count 1)
-// main segments: the tail regions (bucket-major, map workgroup minor), then the per-bucket
-// overflow lists -- the order of mrg_launch_wmain_counts
+// main segments: the tail regions of 12-byte records (bucket-major, map workgroup minor), the
+// per-bucket overflow lists, then the 16-byte tail regions (keys of 13..16 bytes) -- the order of
+// mrg_launch_wmain_counts
 __device__ __forceinline__ void main_rec(const BucketArgs &A, uint64_t s, uint64_t i, uint64_t &k0, uint64_t &k1) {
     const uint64_t nt = (uint64_t)A.nreg * MRG_NBUCKET;
     const GASW uint64_t *p;
     if (s < nt) {
         const uint32_t b = (uint32_t)(s / A.nreg), w = (uint32_t)(s % A.nreg);
-        p = gw(A.pool) + 2 * (A.rbase[b] + (uint64_t)w * A.bcap[b] + i);
-    } else {
+        const GASW uint32_t *r = reinterpret_cast<const GASW uint32_t *>(
+            reinterpret_cast<const GASW uint8_t *>(gw(A.pool)) + 12u * (A.rbase[b] + (uint64_t)w * A.bcap[b] + i));
+        k0 = (uint64_t)r[0] | ((uint64_t)r[1] << 32);
+        k1 = (uint64_t)r[2] << 32;
+        return;
+    } else if (s < nt + MRG_NBUCKET) {
         p = gw(A.movf) + 2 * ((s - nt) * A.mocap + i);
+    } else {
+        const uint64_t s2 = s - nt - MRG_NBUCKET;
+        const uint32_t b = (uint32_t)(s2 / A.nreg), w = (uint32_t)(s2 % A.nreg);
+        p = gw(A.pool16) + 2 * (A.rbase16[b] + (uint64_t)w * A.bcap16[b] + i);
     }
     const uint64_t a = p[0], b = p[1];
     k0 = a;
     k1 = b;
+}
+
+// a record of a main segment whose first record is at `segptr` (bit 0 set: 12-byte records
+// {k0, high word of k1}; clear: 16-byte records {k0, k1}); 12-byte segments have 4 bytes of slack
+// after their last record, so both are one 16-byte load
+typedef uint64_t v2w __attribute__((ext_vector_type(2)));
+typedef uint32_t v4wu __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ void seg_rec(uint64_t segptr, uint64_t i, uint64_t &k0, uint64_t &k1) {
+    const bool w12 = segptr & 1u;
+    const uint64_t base = segptr & ~1ull;
+    const v4wu x = *reinterpret_cast<const GASW v4wu *>((const GASW uint8_t *)(base + (w12 ? 12u : 16u) * i));
+    k0 = (uint64_t)x.x | ((uint64_t)x.y << 32);
+    k1 = w12 ? (uint64_t)x.z << 32 : ((uint64_t)x.z | ((uint64_t)x.w << 32));
 }
 
 // s in [lo, hi) with off[s] <= i < off[s + 1]  (off non-decreasing; empty segments are skipped)
@@ -163,10 +185,15 @@ __global__ void k_wmain_counts(BucketArgs A, uint64_t *cnt, uint64_t *segptr) {
     if (s < nt) {
         const uint32_t b = (uint32_t)(s / A.nreg), w = (uint32_t)(s % A.nreg);
         cnt[s] = min(A.bcount[(uint64_t)w * MRG_NBUCKET + b], A.bcap[b]);
-        segptr[s] = (uint64_t)(A.pool + 2 * (A.rbase[b] + (uint64_t)w * A.bcap[b]));
+        segptr[s] = (uint64_t)((const uint8_t *)A.pool + 12u * (A.rbase[b] + (uint64_t)w * A.bcap[b])) | 1u;
     } else if (s < nt + MRG_NBUCKET) {
         cnt[s] = min(A.monext[s - nt], A.mocap);
         segptr[s] = (uint64_t)(A.movf + 2 * ((s - nt) * A.mocap));
+    } else if (s < 2 * nt + MRG_NBUCKET) {
+        const uint64_t s2 = s - nt - MRG_NBUCKET;
+        const uint32_t b = (uint32_t)(s2 / A.nreg), w = (uint32_t)(s2 % A.nreg);
+        cnt[s] = min(A.bcount16[(uint64_t)w * MRG_NBUCKET + b], A.bcap16[b]);
+        segptr[s] = (uint64_t)(A.pool16 + 2 * (A.rbase16[b] + (uint64_t)w * A.bcap16[b]));
     }
 }
 
@@ -292,12 +319,10 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl1(L1Args L) {
     // no per-record search (three dependent LDS reads before every load).
     constexpr int U = 4;
     auto seg_off = [&](uint64_t x) -> uint64_t { return cached ? s_off[x - slo] : L.off[x]; };
-    auto seg_ptr = [&](uint64_t x) -> const GASW uint64_t * {
-        return reinterpret_cast<const GASW uint64_t *>(cached ? s_ptr[x - slo] : L.segptr[x]);
-    };
+    auto seg_ptr = [&](uint64_t x) -> uint64_t { return cached ? s_ptr[x - slo] : L.segptr[x]; };
     uint64_t sg = seg_find(seg_off, slo, shi, min(t0 + tid, t1 - 1u));
     uint64_t seg_lo = seg_off(sg), seg_hi = seg_off(sg + 1);
-    const GASW uint64_t *seg_p = seg_ptr(sg);
+    uint64_t seg_p = seg_ptr(sg);
     for (uint64_t base = t0 + tid; base < t1; base += (uint64_t)U * W_WG) {
         uint64_t k0[U], k1[U];
 #pragma unroll
@@ -309,11 +334,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl1(L1Args L) {
                 seg_hi = seg_off(sg + 1);
                 seg_p = seg_ptr(sg);
             }
-            const GASW uint64_t *rp = seg_p + 2 * (i - seg_lo);
-            typedef uint64_t v2 __attribute__((ext_vector_type(2)));
-            const v2 x = *reinterpret_cast<const GASW v2 *>(rp);
-            k0[u] = x.x;
-            k1[u] = x.y;
+            seg_rec(seg_p, i - seg_lo, k0[u], k1[u]);
         }
         uint32_t bk[U];
         if (SCATTER) {   // the bucket the counting pass found (no SipHash, no splitter search again)
@@ -1812,7 +1833,7 @@ inline dim3 gridw(uint64_t n, int b = 256) { return dim3((unsigned)((n + b - 1) 
 // ================================================================ host launchers (mrgpu.cpp)
 void mrg_wide_launch_counts(const BucketArgs &a, uint64_t *cnt_main, uint64_t *segptr, uint64_t *cnt_flush,
                             hipStream_t s) {
-    const uint64_t nsm = (uint64_t)a.nreg * MRG_NBUCKET + MRG_NBUCKET;
+    const uint64_t nsm = 2ull * a.nreg * MRG_NBUCKET + MRG_NBUCKET;
     hipLaunchKernelGGL(k_wmain_counts, gridw(nsm), dim3(256), 0, s, a, cnt_main, segptr);
     hipLaunchKernelGGL(k_wflush_counts, gridw(a.nreg), dim3(256), 0, s, a, cnt_flush);
 }

@@ -20,6 +20,10 @@
 #endif
 #define MRG_NBUCKET (1 << MRG_NBUCKET_LOG2)
 #define MRG_BA_CAP 7680          // max LDS table slots of the per-bucket aggregation kernel (k_keys.hip ba_cap)
+// bytes of one tail record in MapArgs::pool: wc 12 ({k0, high word of k1}: keys of <= 12 bytes, whose
+// k1 low word is 0 -- keys never contain NUL), the indexer 24 ({k0, k1, doc}); wc keys of 13..16
+// bytes go to the 16-byte pool (MapArgs::pool16)
+#define MRG_TAIL_BYTES(idx) ((idx) ? 24u : 12u)
 
 // counters[] slots written by the kernels
 enum {
@@ -31,7 +35,8 @@ enum {
     CNT_OVF = 5,      // tail records that found neither region nor overflow-list room (rerun)
     CNT_OVF2 = 6,     // keys that did not fit their bucket's LDS table (exact overflow path)
     CNT_NONASCII = 7, // 1 KiB tiles that took the non-ASCII tokenizer
-    CNT_N = 8
+    CNT_REC16 = 8,    // of CNT_REC: 16-byte tail records (wc keys of 13..16 bytes)
+    CNT_N = 9
 };
 
 // Stream-ordered caching allocator interface (all work of a context runs on one stream, so a
@@ -50,11 +55,18 @@ struct MapArgs {
     uint32_t n_docs;
     uint64_t n_chunks;
     // tail records (LDS-table misses, count 1): map workgroup w appends the records of bucket b to
-    // pool records [rbase[b] + w * bcap[b], + bcap[b]); record i = pool[i * RECW .. + RECW)
+    // pool records [rbase[b] + w * bcap[b], + bcap[b]); record i = MRG_TAIL_BYTES(indexer) bytes at
+    // (uint8_t *)pool + i * MRG_TAIL_BYTES: wc {u64 k0, u32 high word of k1} for keys of <= 12 bytes,
+    // the indexer {k0, k1, doc} (24 B)
     uint64_t *pool;
     const uint64_t *rbase;       // [NBUCKET] first record of bucket b's regions
     const uint32_t *bcap;        // [NBUCKET] records per (bucket, workgroup) region
     uint32_t *bcount;            // [grid * NBUCKET] records appended (may exceed bcap)
+    // wc keys of 13..16 bytes: 16-byte records {k0, k1} in their own regions, the same layout
+    uint64_t *pool16;
+    const uint64_t *rbase16;
+    const uint32_t *bcap16;
+    uint32_t *bcount16;
     // records beyond their region's capacity: bucket b's overflow list, records
     // [b * ocap, b * ocap + min(onext[b], ocap)) of `ovf` (a full list forces a rerun)
     uint64_t *ovf;
@@ -147,9 +159,12 @@ void mrg_launch_long_gather(const uint8_t *base, const uint64_t *start, const ui
 
 // ---- k_keys.hip
 struct BucketArgs {
-    const uint64_t *pool;
+    const uint64_t *pool;        // MapArgs::pool (MRG_TAIL_BYTES records) and pool16 (wc, 16-byte records)
     const uint64_t *rbase;
     const uint32_t *bcap, *bcount;
+    const uint64_t *pool16;
+    const uint64_t *rbase16;
+    const uint32_t *bcap16, *bcount16;
     const uint64_t *movf;        // map-side overflow lists (MapArgs::ovf / onext / ocap)
     const uint32_t *monext;
     uint32_t mocap;

@@ -206,6 +206,7 @@ struct mrg_ctx {
     uint64_t long_hint = 0, ovf_hint = 0;
     uint32_t agg_nsub = 1;  // bucket-aggregation workgroups per bucket (grown when the tables overflow)
     std::vector<double> bcap_rate;  // tail records per (bucket, map workgroup) per input byte of the workgroup
+    std::vector<double> bcap16_rate;  // the same for the 16-byte regions (wc keys of 13..16 bytes)
     uint64_t ocap_hint = 0;         // records per bucket overflow list
     bool spec_agg = false, spec_c32 = false;  // last wc job took the bucket path (with 32-bit counts)
     // job
@@ -417,6 +418,8 @@ void aggregate(mrg_ctx *c, const ShortSrc &src, LongItems li) {
 struct MapBufs {
     uint64_t *pool = nullptr, *rbase = nullptr;
     uint32_t *bcap = nullptr, *bcount = nullptr;
+    uint64_t *pool16 = nullptr, *rbase16 = nullptr;
+    uint32_t *bcap16 = nullptr, *bcount16 = nullptr;
     MapArgs *dargs = nullptr;
     uint64_t *ovf = nullptr;
     uint32_t *onext = nullptr;
@@ -429,6 +432,7 @@ struct MapBufs {
     void release(Pool &p) {
         p.put(prof);
         p.put(pool); p.put(rbase); p.put(bcap); p.put(bcount); p.put(dargs); p.put(ovf); p.put(onext);
+        p.put(pool16); p.put(rbase16); p.put(bcap16); p.put(bcount16);
         p.put(fk0); p.put(fk1); p.put(fcnt); p.put(fdoc); p.put(foff);
         p.put(lstart); p.put(llen); p.put(ldoc); p.put(gbits);
         *this = MapBufs{};
@@ -459,6 +463,7 @@ AggLaunch agg_launch(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regca
     AggLaunch L;
     BucketArgs &B = L.B;
     B.pool = A.pool; B.rbase = A.rbase; B.bcap = A.bcap; B.bcount = A.bcount;
+    B.pool16 = A.pool16; B.rbase16 = A.rbase16; B.bcap16 = A.bcap16; B.bcount16 = A.bcount16;
     B.movf = A.ovf; B.monext = A.onext; B.mocap = A.ocap;
     B.fk0 = A.fk0; B.fk1 = A.fk1; B.fcnt = A.fcnt; B.fdoc = A.fdoc; B.foff = A.foff;
     B.nreg = nreg; B.regcap = regcap;
@@ -599,10 +604,11 @@ void wide_aggregate_radix(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t 
     hipStream_t s = c->stream;
     BucketArgs B{};
     B.pool = A.pool; B.rbase = A.rbase; B.bcap = A.bcap; B.bcount = A.bcount;
+    B.pool16 = A.pool16; B.rbase16 = A.rbase16; B.bcap16 = A.bcap16; B.bcount16 = A.bcount16;
     B.movf = A.ovf; B.monext = A.onext; B.mocap = A.ocap;
     B.fk0 = A.fk0; B.fk1 = A.fk1; B.fcnt = A.fcnt; B.fdoc = A.fdoc; B.foff = A.foff;
     B.nreg = nreg; B.regcap = regcap;
-    const uint64_t nseg = (uint64_t)nreg * MRG_NBUCKET + nreg + MRG_NBUCKET;
+    const uint64_t nseg = 2ull * nreg * MRG_NBUCKET + nreg + MRG_NBUCKET;
     uint64_t *segc = pget<uint64_t>(p, nseg + 1), *sego = pget<uint64_t>(p, nseg + 1);
     uint64_t *stmp1 = pget<uint64_t>(p, mrg_scan_tmp_elems(nseg + 1));
     HIPCHK(hipMemsetAsync(segc + nseg, 0, 8, s));
@@ -686,6 +692,7 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     hipStream_t s = c->stream;
     BucketArgs B{};
     B.pool = A.pool; B.rbase = A.rbase; B.bcap = A.bcap; B.bcount = A.bcount;
+    B.pool16 = A.pool16; B.rbase16 = A.rbase16; B.bcap16 = A.bcap16; B.bcount16 = A.bcount16;
     B.movf = A.ovf; B.monext = A.onext; B.mocap = A.ocap;
     B.fk0 = A.fk0; B.fk1 = A.fk1; B.fcnt = A.fcnt; B.fdoc = A.fdoc; B.foff = A.foff;
     B.nreg = nreg; B.regcap = regcap;
@@ -700,7 +707,7 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     };
     mark();
     // ---- segment sizes: main (count 1) and flushed tables (weighted)
-    const uint64_t nsm = (uint64_t)nreg * MRG_NBUCKET + MRG_NBUCKET;
+    const uint64_t nsm = 2ull * nreg * MRG_NBUCKET + MRG_NBUCKET;  // 12-byte regions, overflow lists, 16-byte regions
     uint64_t *cm = pget<uint64_t>(p, nsm + 1), *om = pget<uint64_t>(p, nsm + 1), *segptr = pget<uint64_t>(p, nsm);
     uint64_t *cf = pget<uint64_t>(p, nreg + 1), *of = pget<uint64_t>(p, nreg + 1);
     uint64_t *st1 = pget<uint64_t>(p, mrg_scan_tmp_elems(nsm + 1));
@@ -963,11 +970,17 @@ void job_map(mrg_ctx *c) {
     // records per (bucket, workgroup) tail region: ~1 in 20 input bytes is a tail record (combine
     // misses), spread evenly over the buckets; grown per bucket to the measured demand on a rerun
     const double per_wg = (double)std::max<uint64_t>(total, 1) / grid;
-    std::vector<uint64_t> bcap(MRG_NBUCKET);
+    // wc keys of 13..16 bytes (rare in text) get regions of 16-byte records a sixteenth that size
+    std::vector<uint64_t> bcap(MRG_NBUCKET), bcap16(MRG_NBUCKET, 0);
     for (int b = 0; b < MRG_NBUCKET; ++b) {
         double est = per_wg / 20.0 / MRG_NBUCKET;
         if (c->bcap_rate.size() == MRG_NBUCKET) est = std::max(est, c->bcap_rate[b] * per_wg);
         bcap[b] = (uint64_t)(est * 1.25) + 32;
+        if (!idx) {
+            double est16 = per_wg / 20.0 / MRG_NBUCKET / 16.0;
+            if (c->bcap16_rate.size() == MRG_NBUCKET) est16 = std::max(est16, c->bcap16_rate[b] * per_wg);
+            bcap16[b] = (uint64_t)(est16 * 1.25) + 16;
+        }
     }
     // per-bucket overflow lists absorb the run-to-run variation of the regions' demand (the LDS
     // table's contents depend on wave timing: a frequent key that finds its set full in one
@@ -975,25 +988,35 @@ void job_map(mrg_ctx *c) {
     // up.  Sized at a quarter of the default region total per bucket (C3: 2 GiB, only touched as
     // far as used); at 1/16 about one step in ten reran the whole map.
     uint64_t ocap = std::max<uint64_t>(c->ocap_hint, std::max<uint64_t>(1024, total / 20 / MRG_NBUCKET / 4));
-    if (const uint64_t t = env_u64("MRG_TEST_TAIL_CAP", 0)) bcap.assign(MRG_NBUCKET, t);  // test knobs
+    if (const uint64_t t = env_u64("MRG_TEST_TAIL_CAP", 0)) {  // test knobs
+        bcap.assign(MRG_NBUCKET, t);
+        if (!idx) bcap16.assign(MRG_NBUCKET, t);
+    }
     if (const uint64_t t = env_u64("MRG_TEST_OVF_CAP", 0)) ocap = t;
     MapArgs A{};
     MapBufs M;
     AggLaunch spec;  // the aggregation launched right behind the map (wc, the last job took the bucket path)
     uint32_t launches = 0;
     for (;;) {
-        std::vector<uint64_t> rbase(MRG_NBUCKET, 0);
-        std::vector<uint32_t> bcap32(MRG_NBUCKET);
-        uint64_t rtot = 0;
+        std::vector<uint64_t> rbase(MRG_NBUCKET, 0), rbase16(MRG_NBUCKET, 0);
+        std::vector<uint32_t> bcap32(MRG_NBUCKET), bcap16_32(MRG_NBUCKET);
+        uint64_t rtot = 0, rtot16 = 0;
         for (int b = 0; b < MRG_NBUCKET; ++b) {
-            if (bcap[b] > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
+            if (bcap[b] > 0xFFFFFFF0ull || bcap16[b] > 0xFFFFFFF0ull)
+                raise(MRG_ENOMEM, "input too large for one map launch");
             bcap32[b] = (uint32_t)bcap[b];
             rbase[b] = rtot;
             rtot += (uint64_t)grid * bcap[b];
+            bcap16_32[b] = (uint32_t)bcap16[b];
+            rbase16[b] = rtot16;
+            rtot16 += (uint64_t)grid * bcap16[b];
         }
         M.rbase = pget<uint64_t>(p, MRG_NBUCKET);
         M.bcap = pget<uint32_t>(p, MRG_NBUCKET);
         M.bcount = pget<uint32_t>(p, (uint64_t)grid * MRG_NBUCKET);
+        M.rbase16 = pget<uint64_t>(p, MRG_NBUCKET);
+        M.bcap16 = pget<uint32_t>(p, MRG_NBUCKET);
+        M.bcount16 = pget<uint32_t>(p, (uint64_t)grid * MRG_NBUCKET);
         M.dargs = pget<MapArgs>(p, 1);
         if (ocap > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
         M.ovf = pget<uint64_t>(p, (uint64_t)MRG_NBUCKET * ocap * RW);
@@ -1001,13 +1024,17 @@ void job_map(mrg_ctx *c) {
         HIPCHK(hipMemsetAsync(M.onext, 0, 4ull * MRG_NBUCKET, s));
         h2d(c, M.rbase, rbase.data(), 8ull * MRG_NBUCKET);
         h2d(c, M.bcap, bcap32.data(), 4ull * MRG_NBUCKET);
+        h2d(c, M.rbase16, rbase16.data(), 8ull * MRG_NBUCKET);
+        h2d(c, M.bcap16, bcap16_32.data(), 4ull * MRG_NBUCKET);
         A.in = c->d_in;
         A.doc_off = d_doc_off;
         A.chunk_base = d_cb;
         A.doc_id = d_ids;
         A.n_docs = nd;
         A.n_chunks = n_chunks;
-        M.pool = pget<uint64_t>(p, rtot * RW);
+        // 12-byte (wc) / 24-byte (indexer) records, + 16 bytes: readers may load a 12-byte record as 16
+        M.pool = pget<uint64_t>(p, (rtot * MRG_TAIL_BYTES(idx) + 16 + 7) / 8);
+        M.pool16 = pget<uint64_t>(p, 2 * rtot16 + 2);
         M.fk0 = pget<uint64_t>(p, (uint64_t)grid * cap);
         M.fk1 = pget<uint64_t>(p, (uint64_t)grid * cap);
         M.fcnt = pget<uint32_t>(p, (uint64_t)grid * cap);
@@ -1017,6 +1044,7 @@ void job_map(mrg_ctx *c) {
         M.llen = pget<uint32_t>(p, lcap);
         M.ldoc = pget<uint32_t>(p, lcap);
         A.pool = M.pool; A.rbase = M.rbase; A.bcap = M.bcap; A.bcount = M.bcount;
+        A.pool16 = M.pool16; A.rbase16 = M.rbase16; A.bcap16 = M.bcap16; A.bcount16 = M.bcount16;
         A.ovf = M.ovf; A.onext = M.onext; A.ocap = (uint32_t)ocap;
         A.fk0 = M.fk0; A.fk1 = M.fk1; A.fcnt = M.fcnt; A.fdoc = M.fdoc; A.foff = M.foff;
         A.lstart = M.lstart; A.llen = M.llen; A.ldoc = M.ldoc; A.lcap = lcap;
@@ -1098,15 +1126,24 @@ void job_map(mrg_ctx *c) {
         agg_put(c, spec);
         // capacity exceeded: grow each bucket's regions to its demand (remembered), run again
         if (c->h_cnt[CNT_OVF]) {
-            std::vector<uint32_t> cnt((uint64_t)grid * MRG_NBUCKET);
+            std::vector<uint32_t> cnt((uint64_t)grid * MRG_NBUCKET), cnt16((uint64_t)grid * MRG_NBUCKET, 0);
             HIPCHK(hipMemcpyAsync(cnt.data(), M.bcount, 4ull * cnt.size(), hipMemcpyDeviceToHost, s));
+            if (!idx) HIPCHK(hipMemcpyAsync(cnt16.data(), M.bcount16, 4ull * cnt16.size(), hipMemcpyDeviceToHost, s));
             sync(c);
             c->bcap_rate.assign(MRG_NBUCKET, 0.0);
+            c->bcap16_rate.assign(MRG_NBUCKET, 0.0);
             for (int b = 0; b < MRG_NBUCKET; ++b) {
-                uint64_t mx = 0;
-                for (int g = 0; g < grid; ++g) mx = std::max<uint64_t>(mx, cnt[(uint64_t)g * MRG_NBUCKET + b]);
+                uint64_t mx = 0, mx16 = 0;
+                for (int g = 0; g < grid; ++g) {
+                    mx = std::max<uint64_t>(mx, cnt[(uint64_t)g * MRG_NBUCKET + b]);
+                    mx16 = std::max<uint64_t>(mx16, cnt16[(uint64_t)g * MRG_NBUCKET + b]);
+                }
                 bcap[b] = std::max<uint64_t>(bcap[b], mx + mx / 4 + 64);
                 c->bcap_rate[b] = (double)mx / per_wg;
+                if (!idx) {
+                    bcap16[b] = std::max<uint64_t>(bcap16[b], mx16 + mx16 / 4 + 16);
+                    c->bcap16_rate[b] = (double)mx16 / per_wg;
+                }
             }
             ocap = c->ocap_hint = 4 * ocap;
         }
@@ -1127,7 +1164,7 @@ void job_map(mrg_ctx *c) {
     c->st.long_tokens = c->h_cnt[CNT_LONG];
     c->st.map_records = c->h_cnt[CNT_REC];
     c->st.nonascii_tiles = c->h_cnt[CNT_NONASCII];
-    c->st.tail_records_16 = c->h_cnt[CNT_REC];  // every tail record is 16 bytes (wc) in this layout
+    c->st.tail_records_16 = is_idx(c) ? c->h_cnt[CNT_REC] : c->h_cnt[CNT_REC16];  // the indexer's are 24 B
     const uint64_t errpos = c->h_cnt[CNT_ERRPOS];
     auto release_map = [&]() {
         agg_put(c, spec);

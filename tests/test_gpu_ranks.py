@@ -267,7 +267,7 @@ def test_import_replaces_wide_map_result(ctx, corpus):
 
 def test_c5_forced_collisions_vs_oracle(ctx):
     """SURVEY §8(d) C5's forced-collision run: a 512 MiB near-unique slice (4e7 keys, the wide path)
-    plus 200 000 distinct long keys (the fingerprint sort), every internal hash truncated to 20 bits
+    plus 260 000 distinct keys of 13..30 bytes (16-byte tail records and the long-key fingerprint sort), every internal hash truncated to 20 bits
     (MRG_FLAG_DEBUG_HASH_BITS(20): map-table sets, tail buckets, HBM tables and the long-key
     fingerprints all collide massively); output byte-identical to the oracle."""
     import random
@@ -278,7 +278,8 @@ def test_c5_forced_collisions_vs_oracle(ctx):
     buf = _gen(ctx, "unique", [100, 101], fb)
     rng = random.Random(5)
     alpha = "abcdefghijklmnopqrstuvwxyz0123456789"
-    longs = " ".join("".join(rng.choice(alpha) for _ in range(rng.randint(17, 30))) for _ in range(200_000))
+    # 13..16-byte keys (the map's 16-byte tail regions, read by the wide path's L1) and long keys
+    longs = " ".join("".join(rng.choice(alpha) for _ in range(rng.randint(13, 30))) for _ in range(260_000))
     longs = (longs + "\n").encode()
     host = np.empty(nf * fb + len(longs), dtype=np.uint8)
     torch.from_numpy(host[:nf * fb]).copy_(buf[:nf * fb])
@@ -295,6 +296,7 @@ def test_c5_forced_collisions_vs_oracle(ctx):
     st = ctx.stats()
     del t
     exp = O.wc_mt([host[:fb], host[fb:2 * fb], host[2 * fb:]], 64, threads=THREADS)
-    assert st["distinct_keys"] > 40_000_000 and st["long_tokens"] >= 200_000, st
+    assert st["distinct_keys"] > 40_000_000 and st["long_tokens"] >= 150_000, st
+    assert st["tail_records_16"] > 30_000 and st["agg_path"] == 2, st
     for r in range(64):
         assert got[r] == exp[r], r

@@ -106,6 +106,15 @@ def test_c5_slice_vs_oracle(ctx):
         assert got[r] == exp[r], r
 
 
+def _mixed_keys_doc(seed, n_words=200_000):
+    """Words of 1..20 letters (a few thousand distinct per length): the map's tail records are then
+    a mix of 12-byte records (keys of <= 12 bytes), 16-byte records (13..16 bytes) and long keys."""
+    import random
+    rng = random.Random(seed)
+    vocab = ["".join(rng.choice("abcdefghij") for _ in range(L)) for L in range(1, 21) for _ in range(3000)]
+    return " ".join(rng.choice(vocab) for _ in range(n_words)).encode()
+
+
 @pytest.fixture
 def knobs():
     keys = ["MRG_TEST_TAIL_CAP", "MRG_TEST_OVF_CAP", "MRG_TEST_AGG_OCAP", "MRG_WIDE", "MRG_TEST_LEAF_CAP",
@@ -137,16 +146,20 @@ def test_map_spill_and_rerun_vs_oracle(ctx, corpus, knobs, wide):
     n = 16 * MIB
     t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
     ctx.gen_zipf(t.data_ptr(), n, 0x5EED2026, 7, 1 << 16, 1.1)
-    docs = corpus[:3] + [t[:n].cpu().numpy().tobytes()]
-    exp = O.wc(docs, 10, O.FAST)
-    knobs(MRG_TEST_TAIL_CAP=1, MRG_TEST_OVF_CAP=1 << 22, MRG_WIDE=wide)
-    assert run_wc(ctx, docs, 10) == exp
-    st = ctx.stats()
-    assert st["map_launches"] == 1 and st["map_spill"] > 100_000, st
-    knobs(MRG_TEST_TAIL_CAP=1, MRG_TEST_OVF_CAP=16, MRG_WIDE=wide)
-    assert run_wc(ctx, docs, 10) == exp
-    st = ctx.stats()
-    assert st["map_launches"] >= 2, st
+    docs = corpus[:3] + [t[:n].cpu().numpy().tobytes(), _mixed_keys_doc(1)]
+    for R in (10, 64):
+        exp = O.wc(docs, R, O.FAST)
+        knobs(MRG_TEST_TAIL_CAP=1, MRG_TEST_OVF_CAP=1 << 22, MRG_WIDE=wide)
+        assert run_wc(ctx, docs, R) == exp
+        st = ctx.stats()
+        assert st["map_launches"] == 1 and st["map_spill"] > 100_000, st
+        knobs(MRG_TEST_TAIL_CAP=1, MRG_TEST_OVF_CAP=16, MRG_WIDE=wide)
+        assert run_wc(ctx, docs, R) == exp
+        st = ctx.stats()
+        assert st["map_launches"] >= 2 and st["tail_records_16"] > 1000, st
+        knobs(MRG_WIDE=wide)                                         # regions sized from the rerun's demand
+        assert run_wc(ctx, docs, R) == exp
+        assert ctx.stats()["tail_records_16"] > 1000
 
 
 def test_speculative_aggregation_paths_vs_oracle(ctx, corpus, knobs):
@@ -201,10 +214,11 @@ def test_aggregation_overflow_regrow_vs_oracle(ctx, corpus, knobs):
     import oracle_lib as O
     from gpu_util import run_wc
     knobs(MRG_TEST_AGG_OCAP=1000, MRG_WIDE=0)
-    got = run_wc(ctx, corpus, 10, flags=M.debug_hash_bits(4))
+    docs = corpus + [_mixed_keys_doc(3, 50_000)]
+    got = run_wc(ctx, docs, 64, flags=M.debug_hash_bits(4))
     st = ctx.stats()
-    assert st["agg_launches"] >= 2 and st["overflow_keys"] > 1000, st
-    assert got == O.wc(corpus, 10, O.FAST)
+    assert st["agg_launches"] >= 2 and st["overflow_keys"] > 1000 and st["tail_records_16"] > 100, st
+    assert got == O.wc(docs, 64, O.FAST)
 
 
 @pytest.mark.parametrize("lcap", ["1", "48", "2048"])
@@ -236,9 +250,10 @@ def test_bucket_subranges_vs_oracle(ctx, corpus, knobs, nsub):
     n = 8 * MIB
     t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
     ctx.gen_zipf(t.data_ptr(), n, 0x5EED2026, 3, 1 << 18, 1.1)
-    docs = corpus + [t[:n].cpu().numpy().tobytes()]
+    docs = corpus + [t[:n].cpu().numpy().tobytes(), _mixed_keys_doc(2)]
     knobs(MRG_TEST_AGG_NSUB=nsub, MRG_WIDE=0)
-    assert run_wc(ctx, docs, 10) == O.wc(docs, 10, O.FAST)
+    for R in (10, 64):
+        assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST)
 
 
 def test_bucket_overflow_falls_back_to_wide_vs_oracle(ctx, corpus, knobs):
