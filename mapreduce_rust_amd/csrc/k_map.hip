@@ -795,7 +795,10 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // tile (lane 63) and whether the byte before the tile is White_Space (pv, lane 0)
     auto uni_masks = [&](const uint4 &x, uint32_t &m, uint32_t mafter_lut, uint64_t At, uint64_t doc_lo,
                          uint64_t doc_hi, uint32_t &ma, uint32_t &pv, bool &bad) {
-        const int lo_t = doc_lo > At ? (int)(doc_lo - At) : -(int)umin64(At - doc_lo, (uint64_t)BEHIND);
+        // document bounds in tile offsets: lo_t in [-16, 16) (the first tile of a document starts up to
+        // 15 bytes before it), hi_t in (0, 1088]
+        const int64_t dl = (int64_t)(doc_lo - At);  // two's complement: negative when the document started earlier
+        const int lo_t = (int)(dl < -(int64_t)BEHIND ? -(int64_t)BEHIND : dl);
         const int hi_t = (int)umin64(doc_hi - At, (uint64_t)(TILE + HALO));
         m = fix_seg(x, SEG * lane, m, lo_t, hi_t, bad);
         ma = mafter_lut;
