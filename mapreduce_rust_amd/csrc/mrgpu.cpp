@@ -2491,7 +2491,7 @@ void run_job(const char *const *files, size_t n_files, uint32_t R, int app, cons
     }
     g_run.ms_open = ms_since(t0);
     // ---- map phase: GPU g reads and maps files m with m % G == g (coordinator.rs:137-176)
-    const int readers = (int)std::max<uint64_t>(1, env_u64("MRG_READ_THREADS", std::max(1, std::min(8, 16 / G))));
+    const int readers = (int)std::max<uint64_t>(1, env_u64("MRG_READ_THREADS", std::max(1, std::min(16, 32 / G))));
     std::vector<double> t_read(G, 0.0);
     t0 = Clock::now();
     run_ranks(rs, false, [&](RankState &r) {

@@ -107,12 +107,15 @@ def test_c5_slice_vs_oracle(ctx):
 
 
 def _mixed_keys_doc(seed, n_words=200_000):
-    """Words of 1..20 letters (a few thousand distinct per length): the map's tail records are then
-    a mix of 12-byte records (keys of <= 12 bytes), 16-byte records (13..16 bytes) and long keys."""
+    """Words of 1..16 letters (a few thousand distinct per length) and one word in 100 of 17..20: the
+    map's tail records are then a mix of 12-byte records (keys of <= 12 bytes) and 16-byte records
+    (13..16 bytes), with a few long keys (fewer than the map's default long-key capacity, so they
+    cause no rerun of their own)."""
     import random
     rng = random.Random(seed)
-    vocab = ["".join(rng.choice("abcdefghij") for _ in range(L)) for L in range(1, 21) for _ in range(3000)]
-    return " ".join(rng.choice(vocab) for _ in range(n_words)).encode()
+    vocab = ["".join(rng.choice("abcdefghij") for _ in range(L)) for L in range(1, 17) for _ in range(3000)]
+    longs = ["".join(rng.choice("abcdefghij") for _ in range(L)) for L in range(17, 21) for _ in range(100)]
+    return " ".join(rng.choice(longs) if i % 100 == 99 else rng.choice(vocab) for i in range(n_words)).encode()
 
 
 @pytest.fixture
