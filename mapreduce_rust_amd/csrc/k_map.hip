@@ -560,6 +560,105 @@ __device__ __forceinline__ uint32_t generic_tile(const MapArgs &A, LdsTable<CAP,
     return my_tokens;
 }
 
+// ---- UTF-8-exact byte classes for tiles with non-ASCII bytes (lane-divergent; only where a lane's
+// bytes are not all ASCII).  Tile offsets t are relative to the tile start At; the wave's LDS window
+// holds [At - 16, At + 1024 + 64), and lo_t / hi_t bound it to the document.  Not inlined: the
+// k_map main loop keeps its registers (inlined, this path cost the loop 20 more spilled SGPRs).
+#define LDS __attribute__((address_space(3)))
+struct UniCtx {
+    const LDS uint8_t *win;  // the wave's window (byte 0 = At - 16)
+    const LDS uint8_t *uc;   // class-table blocks of U+0000..07FF and U+20xx (s_uc)
+    int lo_t, hi_t;
+};
+__device__ __forceinline__ uint32_t uni_byte(const UniCtx &u, int t) { return (uint32_t)u.win[t + BEHIND]; }
+__device__ __forceinline__ uint32_t uni_class(const UniCtx &u, uint32_t cp) {
+    uint32_t byte;
+    if (cp < 0x800u) byte = u.uc[cp >> 2];
+    else if ((cp >> 8) == 0x20u) byte = u.uc[512u + ((cp & 255u) >> 2)];
+    else return mrg_uclass(cp);
+    return (byte >> (2u * (cp & 3u))) & 3u;
+}
+// the codepoint holding the non-ASCII byte at q: lead at most 3 bytes back (not before lo_t), length
+// and class; false where the bytes are not valid UTF-8 (the exact walker reports them)
+__device__ __forceinline__ bool uni_cp_at(const UniCtx &u, int q, int &lead, int &n, uint32_t &cls) {
+    int l = q, k = 0;
+    while (mrg_is_cont(uni_byte(u, l))) {
+        if (k == 3 || l - 1 < u.lo_t) return false;
+        --l;
+        ++k;
+    }
+    uint32_t cp, raw;
+    auto rd = [&](uint64_t a) -> uint32_t { return (uint32_t)u.win[a]; };
+    n = mrg_utf8_decode(rd, (uint64_t)(l + BEHIND), (uint64_t)(u.hi_t + BEHIND), &cp, &raw);
+    if (n == 0 || l + n <= q) return false;
+    lead = l;
+    cls = uni_class(u, cp);
+    return true;
+}
+// W16 | S16 << 16 of the 16 bytes x at tile offset so: the LUT classes mlut for ASCII bytes, the
+// class of their codepoint for the others
+__device__ __forceinline__ uint32_t uni_fix_seg(const UniCtx &u, uint4 x, int so, uint32_t mlut, bool &bad) {
+    auto hb = [](uint32_t d) { return ((((d & 0x80808080u) >> 7) * 0x00204081u) >> 21) & 0xFu; };
+    uint32_t nam = hb(x.x) | (hb(x.y) << 4) | (hb(x.z) << 8) | (hb(x.w) << 12);
+    const int vlo = max(u.lo_t - so, 0), vhi = min(u.hi_t - so, 16);
+    nam &= vhi > vlo ? (((1u << vhi) - 1u) & ~((1u << vlo) - 1u)) : 0u;
+    uint32_t W = mlut & 0xFFFFu & ~nam, S = (mlut >> 16) & ~nam;
+    while (nam) {
+        const int p = __builtin_ctz(nam);
+        int lead = 0, n = 0;
+        uint32_t c = 0;
+        if (!uni_cp_at(u, so + p, lead, n, c)) {
+            bad = true;
+            break;
+        }
+        const int e = min(lead + n - so, 16);
+        const uint32_t span = ((1u << e) - 1u) & ~((1u << p) - 1u);
+        if (c == MRG_CLS_W) W |= span;
+        else if (c == MRG_CLS_S) S |= span;
+        nam &= ~span;
+    }
+    return W | (S << 16);
+}
+// A tile with non-ASCII bytes: this lane's segment mask (out.x), the mask of the 16 bytes after the
+// tile (out.y, lane 63), whether the byte before the tile is White_Space (out.z, lane 0; 1 at the
+// document start), and out.w = 1 where the bytes are not valid UTF-8.  dl = doc_lo - At and
+// dh = doc_hi - At as two's-complement differences.
+__device__ __noinline__ uint4 uni_masks(const LDS uint8_t *win, const LDS uint8_t *uc, const LDS uint8_t *lut0,
+                                        uint4 x, uint32_t m, uint32_t mafter_lut, int64_t dl, uint64_t dh,
+                                        int lane) {
+    // document bounds in tile offsets: lo_t in [-16, 16) (the first tile of a document starts up to
+    // 15 bytes before it), hi_t in (0, 1088].  (A select on doc_lo > At lost its first case in the
+    // compiled code: keep this a clamped signed difference.)
+    UniCtx u{win, uc, (int)(dl < -(int64_t)BEHIND ? -(int64_t)BEHIND : dl),
+             (int)(dh < (uint64_t)(TILE + HALO) ? dh : (uint64_t)(TILE + HALO))};
+    bool bad = false;
+    uint4 out;
+    out.x = uni_fix_seg(u, x, SEG * lane, m, bad);
+    out.y = mafter_lut;
+    out.z = 0;
+    if (lane == 63) {
+        const u32x4 a = *reinterpret_cast<const LDS u32x4 *>(win + BEHIND + TILE);  // the 16 bytes after the tile
+        out.y = uni_fix_seg(u, uint4{a.x, a.y, a.z, a.w}, TILE, mafter_lut, bad);
+    }
+    if (lane == 0) {
+        if (dl >= 0) {
+            out.z = 1u;  // the document starts here
+        } else {
+            const uint32_t b = uni_byte(u, -1);
+            if (b < 0x80u) {
+                out.z = (lut0[b] >> 4) & 1u;
+            } else {
+                int lead = 0, n = 0;
+                uint32_t c = 0;
+                if (!uni_cp_at(u, -1, lead, n, c)) bad = true;
+                out.z = c == MRG_CLS_S ? 1u : 0u;
+            }
+        }
+    }
+    out.w = bad ? 1u : 0u;
+    return out;
+}
+
 template <int CAP, bool IDX>
 __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // the arguments live in device memory (not the kernarg segment): fields are loaded where they
@@ -739,88 +838,6 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
 #else
 #define MRG_PT(i)
 #endif
-    // ---- UTF-8-exact byte classes for tiles with non-ASCII bytes (lane-divergent; only where a lane's
-    // bytes are not all ASCII).  Tile offsets t are relative to the tile start At; the wave's window
-    // holds [At - 16, At + 1024 + 64), and lo_t / hi_t bound it to the document.
-    auto wbyte = [&](int t) -> uint32_t { return (uint32_t)win[t + BEHIND]; };
-    auto uclass_lds = [&](uint32_t cp) -> uint32_t {
-        uint32_t byte;
-        if (cp < 0x800u) byte = s_uc[cp >> 2];
-        else if ((cp >> 8) == 0x20u) byte = s_uc[512u + ((cp & 255u) >> 2)];
-        else return mrg_uclass(cp);
-        return (byte >> (2u * (cp & 3u))) & 3u;
-    };
-    // the codepoint holding the non-ASCII byte at q: lead at most 3 bytes back (not before lo_t),
-    // length and class; false where the bytes are not valid UTF-8 (the exact walker reports them)
-    auto cp_at = [&](int q, int lo_t, int hi_t, int &lead, int &n, uint32_t &cls) -> bool {
-        int l = q, k = 0;
-        while (mrg_is_cont(wbyte(l))) {
-            if (k == 3 || l - 1 < lo_t) return false;
-            --l;
-            ++k;
-        }
-        uint32_t cp, raw;
-        auto rd = [&](uint64_t a) -> uint32_t { return (uint32_t)win[a]; };
-        n = mrg_utf8_decode(rd, (uint64_t)(l + BEHIND), (uint64_t)(hi_t + BEHIND), &cp, &raw);
-        if (n == 0 || l + n <= q) return false;
-        lead = l;
-        cls = uclass_lds(cp);
-        return true;
-    };
-    // W16 | S16 << 16 of the 16 bytes x at tile offset so: the LUT classes mlut for ASCII bytes, the
-    // class of their codepoint for the others
-    auto fix_seg = [&](const uint4 &x, int so, uint32_t mlut, int lo_t, int hi_t, bool &bad) -> uint32_t {
-        auto hb = [](uint32_t d) { return ((((d & 0x80808080u) >> 7) * 0x00204081u) >> 21) & 0xFu; };
-        uint32_t nam = hb(x.x) | (hb(x.y) << 4) | (hb(x.z) << 8) | (hb(x.w) << 12);
-        const int vlo = max(lo_t - so, 0), vhi = min(hi_t - so, 16);
-        nam &= vhi > vlo ? (((1u << vhi) - 1u) & ~((1u << vlo) - 1u)) : 0u;
-        uint32_t W = mlut & 0xFFFFu & ~nam, S = (mlut >> 16) & ~nam;
-        while (nam) {
-            const int p = __builtin_ctz(nam);
-            int lead = 0, n = 0;
-            uint32_t c = 0;
-            if (!cp_at(so + p, lo_t, hi_t, lead, n, c)) {
-                bad = true;
-                break;
-            }
-            const int e = min(lead + n - so, 16);
-            const uint32_t span = ((1u << e) - 1u) & ~((1u << p) - 1u);
-            if (c == MRG_CLS_W) W |= span;
-            else if (c == MRG_CLS_S) S |= span;
-            nam &= ~span;
-        }
-        return W | (S << 16);
-    };
-    // a tile with non-ASCII bytes: every lane's segment mask m, the mask ma of the 16 bytes after the
-    // tile (lane 63) and whether the byte before the tile is White_Space (pv, lane 0)
-    auto uni_masks = [&](const uint4 &x, uint32_t &m, uint32_t mafter_lut, uint64_t At, uint64_t doc_lo,
-                         uint64_t doc_hi, uint32_t &ma, uint32_t &pv, bool &bad) {
-        // document bounds in tile offsets: lo_t in [-16, 16) (the first tile of a document starts up to
-        // 15 bytes before it), hi_t in (0, 1088]
-        const int64_t dl = (int64_t)(doc_lo - At);  // two's complement: negative when the document started earlier
-        const int lo_t = (int)(dl < -(int64_t)BEHIND ? -(int64_t)BEHIND : dl);
-        const int hi_t = (int)umin64(doc_hi - At, (uint64_t)(TILE + HALO));
-        m = fix_seg(x, SEG * lane, m, lo_t, hi_t, bad);
-        ma = mafter_lut;
-        pv = 0;
-        if (lane == 63) ma = fix_seg(reinterpret_cast<const uint4 *>(win)[1 + 64], TILE, mafter_lut, lo_t, hi_t, bad);
-        if (lane == 0) {
-            if (At <= doc_lo) {
-                pv = 1u;  // the document starts here
-            } else {
-                const uint32_t b = wbyte(-1);
-                if (b < 0x80u) {
-                    pv = (s_lut[0][b] >> 4) & 1u;
-                } else {
-                    int lead = 0, n = 0;
-                    uint32_t c = 0;
-                    if (!cp_at(-1, lo_t, hi_t, lead, n, c)) bad = true;
-                    pv = c == MRG_CLS_S ? 1u : 0u;
-                }
-            }
-        }
-    };
-
     auto process_blk = [&](const BlkInfo &I, const Blk &X, uint64_t cblk, auto &&mid) {
         const uint64_t Ab = I.Ab, doc_lo = I.doc_lo, doc_hi = I.doc_hi;
         const uint32_t docid = I.docid;
@@ -920,6 +937,14 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 prev = from_prev_lane(m) >> 31;
                 if (lane == 0) prev = j == 0 ? prev_blk : (lane_u32(mprev, 63) >> 31);
             } else {
+#ifdef MRG_MAP_NO_UNI
+                // A/B builds only (-DMRG_MAP_NO_UNI): every non-ASCII tile to the exact walker
+                if (lane == 0) {
+                    const uint32_t k = atomicAdd(&s_ngen, 1u);
+                    glist[k] = (uint32_t)((cblk - wlo_b) * NSUB + j);
+                }
+                continue;
+#endif
                 // A non-ASCII byte where the fast path reads: the LUT classes of the lanes whose bytes
                 // are not all ASCII are replaced by UTF-8-exact ones (uni_masks), after which the tile
                 // is tokenized exactly like an ASCII tile -- every byte of a codepoint carries its
@@ -927,10 +952,12 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 // walker must report) defers the tile to generic_tile after the main loop.
                 if (lane == (j ? 63 : 0)) reinterpret_cast<uint4 *>(win)[0] = j ? X.v0 : X.e;  // the bytes before
                 wave_sync_lds();
-                bool bad = false;
-                uint32_t ma = 0, pv = 0;
-                uni_masks(x, m, mafter, At, doc_lo, doc_hi, ma, pv, bad);
-                if (__any(bad)) {  // recorded; processed after the main loop
+                const uint4 um = uni_masks((const LDS uint8_t *)win, (const LDS uint8_t *)s_uc,
+                                           (const LDS uint8_t *)s_lut[0], x, m, mafter,
+                                           (int64_t)(doc_lo - At), doc_hi - At, lane);
+                m = um.x;
+                const uint32_t ma = um.y, pv = um.z;
+                if (__any(um.w != 0u)) {  // recorded; processed after the main loop
                     if (lane == 0) {
                         const uint32_t k = atomicAdd(&s_ngen, 1u);
                         glist[k] = (uint32_t)((cblk - wlo_b) * NSUB + j);
