@@ -560,103 +560,72 @@ __device__ __forceinline__ uint32_t generic_tile(const MapArgs &A, LdsTable<CAP,
     return my_tokens;
 }
 
-// ---- UTF-8-exact byte classes for tiles with non-ASCII bytes (lane-divergent; only where a lane's
-// bytes are not all ASCII).  Tile offsets t are relative to the tile start At; the wave's LDS window
-// holds [At - 16, At + 1024 + 64), and lo_t / hi_t bound it to the document.  Not inlined: the
-// k_map main loop keeps its registers (inlined, this path cost the loop 20 more spilled SGPRs).
+// ---- UTF-8-exact byte classes for blocks with a non-ASCII byte where the fast path reads (the
+// block's two tiles, the first segment of its halo, the byte before it).  Per lane and only where its
+// own bytes are not all ASCII, the codepoints covering them are decoded from a 24-byte register window
+// [so - 4, so + 20) -- the 4 bytes before the segment (its neighbour lane's last word), its 16 bytes
+// and the 4 after -- and every byte of a codepoint gets the codepoint's class (W, S or deleted).
+// Offsets are block-relative; [lo, hi) is the document clamped to the staged range.
 #define LDS __attribute__((address_space(3)))
-struct UniCtx {
-    const LDS uint8_t *win;  // the wave's window (byte 0 = At - 16)
-    const LDS uint8_t *uc;   // class-table blocks of U+0000..07FF and U+20xx (s_uc)
-    int lo_t, hi_t;
+struct SegWin {
+    uint32_t w0, w1, w2, w3, w4, w5;
 };
-__device__ __forceinline__ uint32_t uni_byte(const UniCtx &u, int t) { return (uint32_t)u.win[t + BEHIND]; }
-__device__ __forceinline__ uint32_t uni_class(const UniCtx &u, uint32_t cp) {
+// bytes [idx, idx + 4) of the window, idx in [0, 20) (first byte in bits 0..7)
+__device__ __forceinline__ uint32_t seg_win4(const SegWin &s, int idx) {
+    const int d = idx >> 2;
+    const uint32_t lo = d == 0 ? s.w0 : d == 1 ? s.w1 : d == 2 ? s.w2 : d == 3 ? s.w3 : s.w4;
+    const uint32_t hi = d == 0 ? s.w1 : d == 1 ? s.w2 : d == 2 ? s.w3 : d == 3 ? s.w4 : s.w5;
+    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(idx & 3));
+}
+// class of codepoint cp: U+0080..07FF and U+2000..20FF from the LDS copy uc, the rest from the table
+__device__ __forceinline__ uint32_t uni_class(const LDS uint8_t *uc, uint32_t cp) {
     uint32_t byte;
-    if (cp < 0x800u) byte = u.uc[cp >> 2];
-    else if ((cp >> 8) == 0x20u) byte = u.uc[512u + ((cp & 255u) >> 2)];
+    if (cp < 0x800u) byte = uc[cp >> 2];
+    else if ((cp >> 8) == 0x20u) byte = uc[512u + ((cp & 255u) >> 2)];
     else return mrg_uclass(cp);
     return (byte >> (2u * (cp & 3u))) & 3u;
 }
-// the codepoint holding the non-ASCII byte at q: lead at most 3 bytes back (not before lo_t), length
-// and class; false where the bytes are not valid UTF-8 (the exact walker reports them)
-__device__ __forceinline__ bool uni_cp_at(const UniCtx &u, int q, int &lead, int &n, uint32_t &cls) {
-    int l = q, k = 0;
-    while (mrg_is_cont(uni_byte(u, l))) {
-        if (k == 3 || l - 1 < u.lo_t) return false;
-        --l;
-        ++k;
-    }
-    uint32_t cp, raw;
-    auto rd = [&](uint64_t a) -> uint32_t { return (uint32_t)u.win[a]; };
-    n = mrg_utf8_decode(rd, (uint64_t)(l + BEHIND), (uint64_t)(u.hi_t + BEHIND), &cp, &raw);
-    if (n == 0 || l + n <= q) return false;
-    lead = l;
-    cls = uni_class(u, cp);
-    return true;
-}
-// W16 | S16 << 16 of the 16 bytes x at tile offset so: the LUT classes mlut for ASCII bytes, the
-// class of their codepoint for the others
-__device__ __forceinline__ uint32_t uni_fix_seg(const UniCtx &u, uint4 x, int so, uint32_t mlut, bool &bad) {
+// W16 | S16 << 16 of the 16 bytes at block offset so (window s): mlut for ASCII bytes and for bytes
+// outside [lo, hi) or below position pmin, the codepoint's class for the others; bad = not valid UTF-8
+__device__ __forceinline__ uint32_t uni_fix(const SegWin &s, int so, uint32_t mlut, int lo, int hi, int pmin,
+                                            const LDS uint8_t *uc, bool &bad) {
     auto hb = [](uint32_t d) { return ((((d & 0x80808080u) >> 7) * 0x00204081u) >> 21) & 0xFu; };
-    uint32_t nam = hb(x.x) | (hb(x.y) << 4) | (hb(x.z) << 8) | (hb(x.w) << 12);
-    const int vlo = max(u.lo_t - so, 0), vhi = min(u.hi_t - so, 16);
+    uint32_t nam = hb(s.w1) | (hb(s.w2) << 4) | (hb(s.w3) << 8) | (hb(s.w4) << 12);
+    const int vlo = max(max(lo - so, 0), pmin), vhi = min(hi - so, 16);
     nam &= vhi > vlo ? (((1u << vhi) - 1u) & ~((1u << vlo) - 1u)) : 0u;
     uint32_t W = mlut & 0xFFFFu & ~nam, S = (mlut >> 16) & ~nam;
     while (nam) {
         const int p = __builtin_ctz(nam);
-        int lead = 0, n = 0;
-        uint32_t c = 0;
-        if (!uni_cp_at(u, so + p, lead, n, c)) {
+        int lead = p;
+        if ((seg_win4(s, p + 4) & 0xC0u) == 0x80u) {  // a continuation: its lead is 1..3 bytes back
+            const uint32_t back = seg_win4(s, p + 1);  // bytes p - 3 .. p
+            int k = 0;
+            if (mrg_is_cont((back >> 16) & 0xFFu)) {
+                k = 1;
+                if (mrg_is_cont((back >> 8) & 0xFFu)) k = (mrg_is_cont(back & 0xFFu)) ? 3 : 2;
+            }
+            lead = p - 1 - k;
+            if (k == 3 || so + lead < lo) {
+                bad = true;
+                break;
+            }
+        }
+        const uint32_t v = seg_win4(s, lead + 4);
+        auto rd = [&](uint64_t a) -> uint32_t { return (v >> (8u * (uint32_t)a)) & 0xFFu; };
+        uint32_t cp = 0, raw;
+        const int n = mrg_utf8_decode(rd, 0ull, (uint64_t)min(hi - (so + lead), 4), &cp, &raw);
+        if (n == 0 || lead + n <= p) {
             bad = true;
             break;
         }
-        const int e = min(lead + n - so, 16);
+        const uint32_t c = uni_class(uc, cp);
+        const int e = min(lead + n, 16);
         const uint32_t span = ((1u << e) - 1u) & ~((1u << p) - 1u);
         if (c == MRG_CLS_W) W |= span;
         else if (c == MRG_CLS_S) S |= span;
         nam &= ~span;
     }
     return W | (S << 16);
-}
-// A tile with non-ASCII bytes: this lane's segment mask (out.x), the mask of the 16 bytes after the
-// tile (out.y, lane 63), whether the byte before the tile is White_Space (out.z, lane 0; 1 at the
-// document start), and out.w = 1 where the bytes are not valid UTF-8.  dl = doc_lo - At and
-// dh = doc_hi - At as two's-complement differences.
-__device__ __noinline__ uint4 uni_masks(const LDS uint8_t *win, const LDS uint8_t *uc, const LDS uint8_t *lut0,
-                                        uint4 x, uint32_t m, uint32_t mafter_lut, int64_t dl, uint64_t dh,
-                                        int lane) {
-    // document bounds in tile offsets: lo_t in [-16, 16) (the first tile of a document starts up to
-    // 15 bytes before it), hi_t in (0, 1088].  (A select on doc_lo > At lost its first case in the
-    // compiled code: keep this a clamped signed difference.)
-    UniCtx u{win, uc, (int)(dl < -(int64_t)BEHIND ? -(int64_t)BEHIND : dl),
-             (int)(dh < (uint64_t)(TILE + HALO) ? dh : (uint64_t)(TILE + HALO))};
-    bool bad = false;
-    uint4 out;
-    out.x = uni_fix_seg(u, x, SEG * lane, m, bad);
-    out.y = mafter_lut;
-    out.z = 0;
-    if (lane == 63) {
-        const u32x4 a = *reinterpret_cast<const LDS u32x4 *>(win + BEHIND + TILE);  // the 16 bytes after the tile
-        out.y = uni_fix_seg(u, uint4{a.x, a.y, a.z, a.w}, TILE, mafter_lut, bad);
-    }
-    if (lane == 0) {
-        if (dl >= 0) {
-            out.z = 1u;  // the document starts here
-        } else {
-            const uint32_t b = uni_byte(u, -1);
-            if (b < 0x80u) {
-                out.z = (lut0[b] >> 4) & 1u;
-            } else {
-                int lead = 0, n = 0;
-                uint32_t c = 0;
-                if (!uni_cp_at(u, -1, lead, n, c)) bad = true;
-                out.z = c == MRG_CLS_S ? 1u : 0u;
-            }
-        }
-    }
-    out.w = bad ? 1u : 0u;
-    return out;
 }
 
 template <int CAP, bool IDX>
@@ -872,7 +841,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         };
         auto na = [](const uint4 &x) { return ((x.x | x.y | x.z | x.w) & 0x80808080u) != 0u; };
         const uint32_t l16 = (uint32_t)lane * SEG;
-        const uint32_t m0 = classify(X.v0, l16), m1 = classify(X.v1, 1024u + l16);
+        uint32_t m0 = classify(X.v0, l16), m1 = classify(X.v1, 1024u + l16);
         // the first halo segment (lane 1's e) by 16 lanes, one byte each, through two ballots
         uint32_t mh;
         {
@@ -888,14 +857,66 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         }
         const bool n0 = na(X.v0), n1 = na(X.v1), ne = na(X.e);
         // class of the byte before the block (lane 0's e, byte 15)
-        const uint32_t prev_blk =
+        uint32_t prev_blk =
             Ab > doc_lo ? (uint32_t)(s_lut[0][(lane_u32(X.e.w, 0) >> 24) & 0x7Fu] >> 4) : 1u;
+        // A non-ASCII byte where the fast path reads (either tile, the first halo segment, the bytes
+        // before the block): the LUT classes of the non-ASCII bytes are replaced by UTF-8-exact ones,
+        // after which both tiles are tokenized exactly like ASCII tiles -- every byte of a codepoint
+        // carries its class, so the W / S masks mean the same.  Invalid UTF-8 defers the block's tiles
+        // to generic_tile after the main loop (which reports the first bad byte).
+        bool defer_blk = false;
+        if (__any(n0 || n1 || (lane <= 1 && ne))) {
+#ifdef MRG_MAP_NO_UNI
+            defer_blk = true;  // A/B builds only: every such block to the exact walker, as in r03
+#else
+            // neighbour words, in uniform control flow (DPP and readlane before the divergent decode)
+            const uint32_t p0 = from_prev_lane(X.v0.w), q0 = from_next_lane(X.v0.x);
+            const uint32_t p1 = from_prev_lane(X.v1.w), q1 = from_next_lane(X.v1.x);
+            const uint32_t before = lane_u32(X.e.w, 0);   // block bytes -4..-1
+            const uint32_t t0last = lane_u32(X.v0.w, 63), t1first = lane_u32(X.v1.x, 0);
+            const uint32_t h0 = lane_u32(X.e.x, 1), h1 = lane_u32(X.e.y, 1), h2 = lane_u32(X.e.z, 1),
+                           h3 = lane_u32(X.e.w, 1), h4 = lane_u32(X.e.x, 2);  // halo bytes 0..19
+            const int64_t dlo = (int64_t)(doc_lo - Ab);  // two's complement (see lo below)
+            // the document in block offsets: lo in [-16, 16), hi in (0, 2112].  (A select on
+            // doc_lo > Ab lost its first case in the compiled code: keep a clamped signed difference.)
+            const int lo = (int)(dlo < -(int64_t)BEHIND ? -(int64_t)BEHIND : dlo);
+            const int hi = (int)umin64(doc_hi - Ab, (uint64_t)(BLK + HALO));
+            const LDS uint8_t *uc = (const LDS uint8_t *)s_uc;
+            bool bad = false;
+            const SegWin s0{lane == 0 ? before : p0, X.v0.x, X.v0.y, X.v0.z, X.v0.w, lane == 63 ? t1first : q0};
+            const SegWin s1{lane == 0 ? t0last : p1, X.v1.x, X.v1.y, X.v1.z, X.v1.w, lane == 63 ? h0 : q1};
+            m0 = uni_fix(s0, (int)l16, m0, lo, hi, 0, uc, bad);
+            m1 = uni_fix(s1, (int)(1024u + l16), m1, lo, hi, 0, uc, bad);
+            uint32_t mh_l = mh, pb_l = prev_blk;
+            if (lane == 63) {  // the first halo segment
+                const SegWin sh{X.v1.w, h0, h1, h2, h3, h4};
+                mh_l = uni_fix(sh, BLK, mh, lo, hi, 0, uc, bad);
+            }
+            if (lane == 0 && dlo < 0 && (before >> 24) >= 0x80u) {  // the byte before the block: its codepoint
+                const SegWin sb{0u, X.e.x, X.e.y, X.e.z, X.e.w, X.v0.x};
+                pb_l = uni_fix(sb, -16, 0u, lo, hi, 12, uc, bad) >> 31;
+            }
+            mh = lane_u32(mh_l, 63);
+            prev_blk = lane_u32(pb_l, 0);
+            defer_blk = __any(bad);
+            if (!defer_blk && lane == 0) atomicAdd(&s_nuni, Ab + (uint64_t)TILE < doc_hi ? 2u : 1u);
+#endif
+        }
         MRG_PT(1);
         // the next block's registers are waited for HERE, before this block's tail stores are
         // issued: vmcnt also counts stores, so a wait placed after them would wait for their
         // acknowledgements too
         mid();
         MRG_PT(0);
+        if (defer_blk) {  // recorded; processed after the main loop
+            if (lane == 0) {
+                for (uint32_t j = 0; j < NSUB && Ab + (uint64_t)j * TILE < doc_hi; ++j) {
+                    const uint32_t k = atomicAdd(&s_ngen, 1u);
+                    glist[k] = (uint32_t)((cblk - wlo_b) * NSUB + j);
+                }
+            }
+            return;
+        }
         if (abl & 32u) {  // timing only: classification alone
             my_tokens += (m0 ^ m1 ^ mh ^ prev_blk) & 1u;
             return;
@@ -910,66 +931,23 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const uint4 xh = j == 0 ? X.v1 : X.e;  // halo source
             const uint32_t mlut = j == 0 ? m0 : m1;
             const uint32_t mprev = m0;
-            // non-ASCII anywhere the fast path reads: the tile, the first halo segment, the byte before
-            const bool nx = j == 0 ? n0 : n1;
-            const bool nh = j == 0 ? n1 : ne;
-            const bool np = j == 0 ? ne : n0;
-            const uint32_t hl = last ? 1u : 0u;  // lane holding the first halo segment
-            const bool nonascii = nx || ((uint32_t)lane == hl && nh) || ((uint32_t)lane == (j ? 63u : 0u) && np);
-            const bool uni = __any(nonascii);  // wave-uniform
             const uint64_t t1 = umin64(At + (uint64_t)TILE, doc_hi);
             const uint64_t whi = umin64(t1 + (uint64_t)HALO, doc_hi);
             const uint64_t wbase = At - (uint64_t)BEHIND;
-            const uint32_t mafter = !last ? lane_u32(m1, 0) : mh;  // the 16 bytes after the tile
 
             // stage the tile and its 64-byte halo (the previous tile's readers are done: program order)
             wave_sync_lds();
             reinterpret_cast<uint4 *>(win)[1 + lane] = x;
             if (!last ? lane < 4 : (lane >= 1 && lane < 5))
                 reinterpret_cast<uint4 *>(win)[65 + (!last ? lane : lane - 1)] = xh;
-            uint32_t m = mlut, mn, prev;
-            if (!uni) {
-                // masks: this lane's segment and the next one (lane 63: the first halo segment)
-                mn = from_next_lane(m);
-                if (lane == 63) mn = mafter;
-                // token starts of this lane's segment: the previous byte's class from lane l-1 (lane 0:
-                // the previous tile's last byte); each start gets a queue slot by a wave prefix sum
-                prev = from_prev_lane(m) >> 31;
-                if (lane == 0) prev = j == 0 ? prev_blk : (lane_u32(mprev, 63) >> 31);
-            } else {
-#ifdef MRG_MAP_NO_UNI
-                // A/B builds only (-DMRG_MAP_NO_UNI): every non-ASCII tile to the exact walker
-                if (lane == 0) {
-                    const uint32_t k = atomicAdd(&s_ngen, 1u);
-                    glist[k] = (uint32_t)((cblk - wlo_b) * NSUB + j);
-                }
-                continue;
-#endif
-                // A non-ASCII byte where the fast path reads: the LUT classes of the lanes whose bytes
-                // are not all ASCII are replaced by UTF-8-exact ones (uni_masks), after which the tile
-                // is tokenized exactly like an ASCII tile -- every byte of a codepoint carries its
-                // class, so the W / S masks mean the same.  Invalid UTF-8 (or anything the exact
-                // walker must report) defers the tile to generic_tile after the main loop.
-                if (lane == (j ? 63 : 0)) reinterpret_cast<uint4 *>(win)[0] = j ? X.v0 : X.e;  // the bytes before
-                wave_sync_lds();
-                const uint4 um = uni_masks((const LDS uint8_t *)win, (const LDS uint8_t *)s_uc,
-                                           (const LDS uint8_t *)s_lut[0], x, m, mafter,
-                                           (int64_t)(doc_lo - At), doc_hi - At, lane);
-                m = um.x;
-                const uint32_t ma = um.y, pv = um.z;
-                if (__any(um.w != 0u)) {  // recorded; processed after the main loop
-                    if (lane == 0) {
-                        const uint32_t k = atomicAdd(&s_ngen, 1u);
-                        glist[k] = (uint32_t)((cblk - wlo_b) * NSUB + j);
-                    }
-                    continue;
-                }
-                if (lane == 0) atomicAdd(&s_nuni, 1u);
-                mn = from_next_lane(m);
-                if (lane == 63) mn = ma;
-                prev = from_prev_lane(m) >> 31;
-                if (lane == 0) prev = pv;
-            }
+            // masks: this lane's segment and the next one (lane 63: the first halo segment)
+            const uint32_t m = mlut;
+            uint32_t mn = from_next_lane(m);
+            if (lane == 63) mn = !last ? lane_u32(m1, 0) : mh;
+            // token starts of this lane's segment: the previous byte's class from lane l-1 (lane 0:
+            // the previous tile's last byte); each start gets a queue slot by a wave prefix sum
+            uint32_t prev = from_prev_lane(m) >> 31;
+            if (lane == 0) prev = j == 0 ? prev_blk : (lane_u32(mprev, 63) >> 31);
             const uint32_t Wpair = (m & 0xFFFFu) | (mn << 16);
             const uint32_t Spair = (m >> 16) | (mn & 0xFFFF0000u);
             mp[lane] = (uint64_t)Wpair | ((uint64_t)Spair << 32);
