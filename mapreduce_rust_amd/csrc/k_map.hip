@@ -207,12 +207,26 @@ struct alignas(16) KeyPair {
     uint64_t a, b;
 };
 
+// A combine-table slot (r04): a key of at most 12 bytes -- k0 and the high word of k1 (its low word
+// is 0 for such keys) -- and its count: 16 bytes, one ds_read_b128 per way, 64 KiB for 4096 slots
+// (was 16-byte keys + a count array, 80 KiB).  Keys of 13..16 bytes never enter the table (the
+// 16-byte tail regions take them).
+#define MRG_EMPTY_HI 0xFFFFFFFFu  // high word of k1 while a claim is in progress (0xFF bytes: never UTF-8)
+struct alignas(16) Slot {
+    uint64_t a;    // k0 (MRG_EMPTY_K0: empty)
+    uint32_t b;    // high word of k1
+    uint32_t cnt;
+};
+__device__ __forceinline__ bool slot_eq(const Slot &k, uint64_t a, uint64_t b) {
+    return ((k.a ^ a) | (uint64_t)(k.b ^ (uint32_t)(b >> 32)) | (b & 0xFFFFFFFFull)) == 0ull;
+}
+
 // Workgroup LDS combine table: 2-way sets -- slots s and s + NS of set s = low
 // hash bits (way-major: way 0 of the 2048 sets, then way 1, so a wave's 16-byte reads of one way
 // spread over all 64 banks instead of half of them; A/B -0.5 % map).  A probe reads both keys at
 // once (one LDS round trip: no tag step) and adds 1 to the
 // matching slot's count.  A new key claims an empty way by a 64-bit CAS on k0 (EMPTY -> k0), then
-// writes k1 (and doc) and adds its first count; slots only ever go EMPTY -> (k0, EMPTY) -> (k0, k1),
+// writes k1's high word (and doc) and adds its first count; slots only ever go EMPTY -> (k0, EMPTY) -> (k0, k1),
 // so a slot read equal to the full key is that key's slot for good.  A reader that sees a half
 // written slot, or a claimer that loses its CAS to the same k0, just misses -- harmless: misses go
 // to the tail and every slot is flushed and summed exactly; at worst a key occupies both ways.
@@ -239,8 +253,8 @@ struct LdsTable {
     static constexpr uint32_t NS = CAP / 2;
     // the indexer's table has a doc word per slot: its bitmap stays at 32 Kibit to fit the LDS
     static constexpr uint32_t DW = (IDX && MRG_MAP_DOOR_WORDS > 1024) ? 1024u : (uint32_t)MRG_MAP_DOOR_WORDS;
-    KeyPair *key;
-    unsigned int *cnt, *doc;
+    Slot *slot;
+    unsigned int *doc;
     unsigned int *door;
     unsigned int *fill;  // slots claimed so far (never decreases: a claimed slot keeps its key)
 
@@ -265,10 +279,6 @@ struct LdsTable {
         return (atomicOr(w, hi) & hi) != 0u;
     }
 
-    __device__ __forceinline__ bool matches(uint32_t s, uint64_t a, uint64_t b, uint32_t d) const {
-        const KeyPair k = key[s];  // one 16-byte LDS read
-        return ((k.a ^ a) | (k.b ^ b)) == 0 && (!IDX || doc[s] == d);
-    }
 
     // claim an empty way of set s0 (ways seen empty: e0, e1); true if the key got a slot and its count
     __device__ __forceinline__ bool claim(uint32_t s0, bool e0, bool e1, uint64_t a, uint64_t b, uint32_t d,
@@ -277,11 +287,11 @@ struct LdsTable {
         for (uint32_t w = 0; w < 2; ++w) {
             if (!(w ? e1 : e0)) continue;
             const uint32_t s = s0 + w * NS;  // way w of set s0: way-major layout
-            const unsigned long long old = atomicCAS(&key[s].a, (unsigned long long)MRG_EMPTY_K0, (unsigned long long)a);
+            const unsigned long long old = atomicCAS(&slot[s].a, (unsigned long long)MRG_EMPTY_K0, (unsigned long long)a);
             if (old == MRG_EMPTY_K0) {
-                key[s].b = b;
+                slot[s].b = (uint32_t)(b >> 32);
                 if (IDX) doc[s] = d;
-                atomicAdd(&cnt[s], 1u);
+                atomicAdd(&slot[s].cnt, 1u);
                 atomicAdd(fill, 1u);
                 return true;
             }
@@ -290,15 +300,16 @@ struct LdsTable {
         return false;
     }
 
-    // one probe per lane (slow path: one token per lane)
+    // one probe per lane (slow path: one token per lane); keys of more than 12 bytes always miss
     __device__ __forceinline__ bool insert_wave(bool act, uint64_t a, uint64_t b, uint32_t d, uint32_t h,
                                                 uint32_t abl = 0) {
+        act = act && (uint32_t)b == 0u;
         const uint32_t s0 = act ? (h & (NS - 1)) : 0u;
-        const KeyPair k0 = key[s0], k1 = key[s0 + NS];
-        const bool m0 = act & (((k0.a ^ a) | (k0.b ^ b)) == 0) & (!IDX || doc[s0] == d);
-        const bool m1 = act & !m0 & (((k1.a ^ a) | (k1.b ^ b)) == 0) & (!IDX || doc[s0 + NS] == d);
+        const Slot k0 = slot[s0], k1 = slot[s0 + NS];
+        const bool m0 = act & slot_eq(k0, a, b) & (!IDX || doc[s0] == d);
+        const bool m1 = act & !m0 & slot_eq(k1, a, b) & (!IDX || doc[s0 + NS] == d);
         bool hit = m0 | m1;
-        if (hit && !(abl & 16u)) atomicAdd(&cnt[m0 ? s0 : s0 + NS], 1u);
+        if (hit && !(abl & 16u)) atomicAdd(&slot[m0 ? s0 : s0 + NS].cnt, 1u);
         const bool e0 = k0.a == MRG_EMPTY_K0, e1 = k1.a == MRG_EMPTY_K0;
         const bool need = act && !hit && (e0 || e1);
         if (__any(need)) {
@@ -381,23 +392,24 @@ __device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint3
     constexpr uint32_t NS = LdsTable<CAP, IDX>::NS;
     const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
     const uint32_t hA = key_hash(a0, a1, dkey, hbits), hB = key_hash(b0, b1, dkey, hbits);
-    const bool actA = ha && !(abl & 2u), actB = hb && !(abl & 2u);
+    // keys of more than 12 bytes (k1 low word non-zero) have no table slot: straight to the tail
+    const bool actA = ha && !(abl & 2u) && (uint32_t)a1 == 0u, actB = hb && !(abl & 2u) && (uint32_t)b1 == 0u;
     const uint32_t sA = actA ? (hA & (NS - 1)) : 0u, sB = actB ? (hB & (NS - 1)) : 0u;
     const uint32_t bA = bucket_of(hA), bB = bucket_of(hB);
     // wc keys longer than 12 bytes (k1 low word non-zero) take the 16-byte regions
     const bool wA = !IDX && (uint32_t)a1 != 0u, wB = !IDX && (uint32_t)b1 != 0u;
     // both ways of both sets: four 16-byte reads in flight together, with the two region ends
-    const KeyPair kA0 = T.key[sA], kA1 = T.key[sA + NS], kB0 = T.key[sB], kB1 = T.key[sB + NS];
+    const Slot kA0 = T.slot[sA], kA1 = T.slot[sA + NS], kB0 = T.slot[sB], kB1 = T.slot[sB + NS];
     const uint64_t endA = (wA ? R.end16 : R.end)[bA], endB = (wB ? R.end16 : R.end)[bB];
-    auto eq = [&](const KeyPair &k, uint64_t x, uint64_t y, uint32_t s) {
-        return (((k.a ^ x) | (k.b ^ y)) == 0) & (!IDX || T.doc[s] == dkey);
+    auto eq = [&](const Slot &k, uint64_t x, uint64_t y, uint32_t s) {
+        return slot_eq(k, x, y) & (!IDX || T.doc[s] == dkey);
     };
     const bool mA0 = actA & eq(kA0, a0, a1, sA), mA1 = actA & !mA0 & eq(kA1, a0, a1, sA + NS);
     const bool mB0 = actB & eq(kB0, b0, b1, sB), mB1 = actB & !mB0 & eq(kB1, b0, b1, sB + NS);
     bool hitA = mA0 | mA1, hitB = mB0 | mB1;
     if (!(abl & 16u)) {
-        if (hitA) atomicAdd(&T.cnt[mA0 ? sA : sA + NS], 1u);
-        if (hitB) atomicAdd(&T.cnt[mB0 ? sB : sB + NS], 1u);
+        if (hitA) atomicAdd(&T.slot[mA0 ? sA : sA + NS].cnt, 1u);
+        if (hitB) atomicAdd(&T.slot[mB0 ? sB : sB + NS].cnt, 1u);
     }
     // empty ways exist only until the table has filled (wave-uniform: a stale count only means
     // an unneeded test)
@@ -647,8 +659,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // v_perm selectors per (key length, 1-byte gap position; 16 = none) over the r-aligned window
     __shared__ __attribute__((aligned(16))) uint32_t s_sel[17 * 17][4];
     // workgroup: combine table + tail-region cursors
-    __shared__ KeyPair s_key[CAP];
-    __shared__ unsigned int s_cnt[CAP];
+    __shared__ Slot s_slot[CAP];
     __shared__ __attribute__((aligned(16))) unsigned int s_doc[IDX ? CAP : 1];
     __shared__ unsigned long long s_tcur[MRG_NBUCKET];  // next pool record of (bucket, this WG)
     __shared__ unsigned long long s_tend[MRG_NBUCKET];  // end of that region
@@ -671,8 +682,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // index, document bounds) is wave-uniform and keeps it in SGPRs
     const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int i = tid; i < CAP; i += WG) {
-        s_key[i] = KeyPair{MRG_EMPTY_K0, MRG_EMPTY_K1};
-        s_cnt[i] = 0;
+        s_slot[i] = Slot{MRG_EMPTY_K0, MRG_EMPTY_HI, 0u};
         if (IDX) s_doc[i] = MRG_EMPTY_DOC;
     }
     if (MRG_MAP_DOOR)
@@ -719,7 +729,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const uint32_t zm = zmask(L, j), gm = zmask(g, j);
         s_sel[L * 17u + g][j] = ((0x00010203u + (gm & 0x01010101u)) & ~zm) | (0x0C0C0C0Cu & zm);
     }
-    LdsTable<CAP, IDX> table{s_key, s_cnt, s_doc, s_door, &s_fill};
+    LdsTable<CAP, IDX> table{s_slot, s_doc, s_door, &s_fill};
     const TailRegions tails{s_tcur, s_tend, s_tcur16, s_tend16};
     uint32_t my_tokens = 0;
     // uniform job parameters used in the hot loop, read once
@@ -1188,9 +1198,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     for (int b = tid; b <= MRG_NBUCKET; b += WG) s_hist[b] = 0;
     __syncthreads();
     for (int i = tid; i < CAP; i += WG) {
-        const KeyPair k = s_key[i];
+        const Slot k = s_slot[i];
         if (k.a == MRG_EMPTY_K0) continue;
-        const uint32_t b = bucket_of(key_hash(k.a, k.b, IDX ? s_doc[i] : MRG_EMPTY_DOC, A.hash_bits));
+        const uint32_t b = bucket_of(key_hash(k.a, (uint64_t)k.b << 32, IDX ? s_doc[i] : MRG_EMPTY_DOC, A.hash_bits));
         s_rank[i] = (uint16_t)atomicAdd(&s_hist[b], 1u);
     }
     __syncthreads();
@@ -1209,14 +1219,15 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     for (int b = tid; b <= MRG_NBUCKET; b += WG) foff[b] = s_hist[b];
     const uint64_t reg = (uint64_t)blockIdx.x * CAP;
     for (int i = tid; i < CAP; i += WG) {
-        const KeyPair k = s_key[i];
+        const Slot k = s_slot[i];
         if (k.a == MRG_EMPTY_K0) continue;
         const uint32_t d = IDX ? s_doc[i] : MRG_EMPTY_DOC;
-        const uint32_t b = bucket_of(key_hash(k.a, k.b, d, A.hash_bits));
+        const uint64_t k1 = (uint64_t)k.b << 32;
+        const uint32_t b = bucket_of(key_hash(k.a, k1, d, A.hash_bits));
         const uint64_t pos2 = reg + s_hist[b] + s_rank[i];
         gp(A.fk0)[pos2] = k.a;
-        gp(A.fk1)[pos2] = k.b;
-        gp(A.fcnt)[pos2] = s_cnt[i];
+        gp(A.fk1)[pos2] = k1;
+        gp(A.fcnt)[pos2] = k.cnt;
         if (IDX) gp(A.fdoc)[pos2] = d;
     }
     // token and tail totals: waves -> LDS -> one device atomic per workgroup and counter (a wave
