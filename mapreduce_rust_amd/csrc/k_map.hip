@@ -39,16 +39,26 @@
 
 namespace {
 
-constexpr int NW = MRG_MAP_WAVES;
-constexpr int WG = MRG_MAP_WG;
+// Block rounds (r04, MRG_MAP_BR=1): both tiles of a block are staged together (one window of the
+// 2 KiB block + halo, 128 mask pairs, one queue of the block's starts) and tokenized by rounds of
+// FOUR tokens per lane -- four independent LDS chains in one instruction stream, one round for a
+// typical block (~245 tokens at C3) -- with 12 waves per workgroup (3 per SIMD, up to 168 VGPRs).
+// MRG_MAP_BR=0: the r03 structure, tile by tile, two tokens per lane, 16 waves.
+#ifndef MRG_MAP_BR
+#define MRG_MAP_BR 1
+#endif
+constexpr int NW = MRG_MAP_BR ? 12 : MRG_MAP_WAVES;
+constexpr int WG = 64 * NW;
 constexpr int SEG = MRG_MAP_SEG;
 constexpr int TILE = MRG_MAP_TILE;
 constexpr int HALO = MRG_MAP_HALO;
 constexpr int BEHIND = MRG_MAP_BEHIND;
-constexpr int WIN = BEHIND + TILE + HALO + 48;  // staged window + slack for 5-dword key reads
-constexpr int QCAP = TILE / 2;                   // a start needs a space before it: <= 512 per tile
 constexpr int NSUB = MRG_MAP_NSUB;               // 1 KiB tiles per block
 constexpr int BLK = NSUB * TILE;                 // bytes per wave iteration
+// staged window + slack for the 5-dword key reads (a key starts within 31 bytes of a token start)
+constexpr int WIN = MRG_MAP_BR ? BEHIND + BLK + HALO + 16 : BEHIND + TILE + HALO + 48;
+constexpr int QCAP = MRG_MAP_BR ? BLK / 2 : TILE / 2;  // a start needs a space before it
+constexpr int NMP = MRG_MAP_BR ? 2 * 64 : 64;          // mask pairs per wave (one per staged segment)
 static_assert(TILE == 64 * SEG, "one segment per lane");
 static_assert(WIN % 16 == 0, "16-byte window rows");
 
@@ -381,72 +391,101 @@ __device__ __forceinline__ void store_tail(GAS uint64_t *pool, GAS uint64_t *poo
     }
 }
 
-// Two tokens per lane (a and b) through the LDS table in one instruction stream: the tag reads,
-// key reads, count adds and tail-cursor adds of both are issued back to back, so every LDS round
-// trip is paid once for two tokens.  Same semantics as emit_fast() applied to a, then b.
-template <int CAP, bool IDX>
-__device__ __forceinline__ void emit_fast2(const MapArgs &A, uint32_t abl, uint32_t hbits, LdsTable<CAP, IDX> &T,
-                                           TailRegions R, GAS uint64_t *pool, GAS uint64_t *pool16, bool ha,
-                                           uint64_t a0, uint64_t a1,
-                                           bool hb, uint64_t b0, uint64_t b1, uint32_t docid, bool may_claim) {
+// N tokens per lane through the LDS table in one instruction stream: the set reads, count adds and
+// tail-cursor adds of all N are issued back to back, so every LDS round trip is paid once for N
+// independent chains.  Same semantics as emit() applied to token 0, then 1, ...
+template <int N, int CAP, bool IDX>
+__device__ __forceinline__ void emit_fastN(const MapArgs &A, uint32_t abl, uint32_t hbits, LdsTable<CAP, IDX> &T,
+                                           TailRegions R, GAS uint64_t *pool, GAS uint64_t *pool16,
+                                           const bool (&has)[N], const uint64_t (&k0)[N], const uint64_t (&k1)[N],
+                                           uint32_t docid, bool may_claim) {
     constexpr uint32_t NS = LdsTable<CAP, IDX>::NS;
     const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
-    const uint32_t hA = key_hash(a0, a1, dkey, hbits), hB = key_hash(b0, b1, dkey, hbits);
-    // keys of more than 12 bytes (k1 low word non-zero) have no table slot: straight to the tail
-    const bool actA = ha && !(abl & 2u) && (uint32_t)a1 == 0u, actB = hb && !(abl & 2u) && (uint32_t)b1 == 0u;
-    const uint32_t sA = actA ? (hA & (NS - 1)) : 0u, sB = actB ? (hB & (NS - 1)) : 0u;
-    const uint32_t bA = bucket_of(hA), bB = bucket_of(hB);
-    // wc keys longer than 12 bytes (k1 low word non-zero) take the 16-byte regions
-    const bool wA = !IDX && (uint32_t)a1 != 0u, wB = !IDX && (uint32_t)b1 != 0u;
-    // both ways of both sets: four 16-byte reads in flight together, with the two region ends
-    const Slot kA0 = T.slot[sA], kA1 = T.slot[sA + NS], kB0 = T.slot[sB], kB1 = T.slot[sB + NS];
-    const uint64_t endA = (wA ? R.end16 : R.end)[bA], endB = (wB ? R.end16 : R.end)[bB];
-    auto eq = [&](const Slot &k, uint64_t x, uint64_t y, uint32_t s) {
-        return slot_eq(k, x, y) & (!IDX || T.doc[s] == dkey);
-    };
-    const bool mA0 = actA & eq(kA0, a0, a1, sA), mA1 = actA & !mA0 & eq(kA1, a0, a1, sA + NS);
-    const bool mB0 = actB & eq(kB0, b0, b1, sB), mB1 = actB & !mB0 & eq(kB1, b0, b1, sB + NS);
-    bool hitA = mA0 | mA1, hitB = mB0 | mB1;
+    uint32_t h[N], s[N], b[N];
+    bool act[N], w16[N], hit[N], m0[N];
+    Slot kw0[N], kw1[N];
+    uint64_t end[N];
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+        h[t] = key_hash(k0[t], k1[t], dkey, hbits);
+        // keys of more than 12 bytes (k1 low word non-zero) have no table slot: straight to the tail
+        act[t] = has[t] && !(abl & 2u) && (uint32_t)k1[t] == 0u;
+        s[t] = act[t] ? (h[t] & (NS - 1)) : 0u;
+        b[t] = bucket_of(h[t]);
+        w16[t] = !IDX && (uint32_t)k1[t] != 0u;  // wc keys of 13..16 bytes: the 16-byte regions
+    }
+    // both ways of every set: 2N 16-byte reads in flight together, with the region ends
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+        kw0[t] = T.slot[s[t]];
+        kw1[t] = T.slot[s[t] + NS];
+        end[t] = (w16[t] ? R.end16 : R.end)[b[t]];
+    }
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+        m0[t] = act[t] & slot_eq(kw0[t], k0[t], k1[t]) & (!IDX || T.doc[s[t]] == dkey);
+        const bool m1 = act[t] & !m0[t] & slot_eq(kw1[t], k0[t], k1[t]) & (!IDX || T.doc[s[t] + NS] == dkey);
+        hit[t] = m0[t] | m1;
+    }
     if (!(abl & 16u)) {
-        if (hitA) atomicAdd(&T.slot[mA0 ? sA : sA + NS].cnt, 1u);
-        if (hitB) atomicAdd(&T.slot[mB0 ? sB : sB + NS].cnt, 1u);
+#pragma unroll
+        for (int t = 0; t < N; ++t)
+            if (hit[t]) atomicAdd(&T.slot[m0[t] ? s[t] : s[t] + NS].cnt, 1u);
     }
     // empty ways exist only until the table has filled (wave-uniform: a stale count only means
     // an unneeded test)
     if (may_claim) {
-        const bool eA0 = kA0.a == MRG_EMPTY_K0, eA1 = kA1.a == MRG_EMPTY_K0;
-        const bool eB0 = kB0.a == MRG_EMPTY_K0, eB1 = kB1.a == MRG_EMPTY_K0;
-        const bool nA = actA && !hitA && (eA0 || eA1), nB = actB && !hitB && (eB0 || eB1);
-        if (__any(nA || nB)) {
-            if (nA) hitA = T.claim(sA, eA0, eA1, a0, a1, dkey, hA);
-            if (nB) hitB = T.claim(sB, eB0, eB1, b0, b1, dkey, hB);
+        bool e0[N], e1[N], need[N], any = false;
+#pragma unroll
+        for (int t = 0; t < N; ++t) {
+            e0[t] = kw0[t].a == MRG_EMPTY_K0;
+            e1[t] = kw1[t].a == MRG_EMPTY_K0;
+            need[t] = act[t] && !hit[t] && (e0[t] || e1[t]);
+            any = any || need[t];
+        }
+        if (__any(any)) {
+#pragma unroll
+            for (int t = 0; t < N; ++t)
+                if (need[t]) hit[t] = T.claim(s[t], e0[t], e1[t], k0[t], k1[t], dkey, h[t]);
         }
     }
-    const bool tA = ha && !hitA && !(abl & 1u), tB = hb && !hitB && !(abl & 1u);
-    // both appends in one region (a lane adds 0 to the other token's cursor): one LDS round trip
-    uint64_t iA = 0, iB = 0;
-    if (tA || tB) {
-        iA = atomicAdd(&(wA ? R.cur16 : R.cur)[bA], tA ? 1ull : 0ull);
-        iB = atomicAdd(&(wB ? R.cur16 : R.cur)[bB], tB ? 1ull : 0ull);
+    bool tl[N], anyt = false;
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+        tl[t] = has[t] && !hit[t] && !(abl & 1u);
+        anyt = anyt || tl[t];
     }
-    const bool okA = tA && iA < endA, okB = tB && iB < endB;
-    if (okA) store_tail<IDX>(pool, pool16, wA, iA, a0, a1, docid);
-    if (okB) store_tail<IDX>(pool, pool16, wB, iB, b0, b1, docid);
-    const bool oA = tA && !okA, oB = tB && !okB;
-    if (__any(oA || oB)) {  // region full (rare): the bucket's shared overflow list
-        auto spill = [&](uint32_t b, uint64_t k0, uint64_t k1) {
-            const uint32_t j = g_add(&A.onext[b], 1u);
+    // every token's append in one LDS round trip (a lane adds 0 for a token that hit)
+    uint64_t idx[N];
+    if (anyt) {
+#pragma unroll
+        for (int t = 0; t < N; ++t) idx[t] = atomicAdd(&(w16[t] ? R.cur16 : R.cur)[b[t]], tl[t] ? 1ull : 0ull);
+    } else {
+#pragma unroll
+        for (int t = 0; t < N; ++t) idx[t] = 0;
+    }
+    bool anyo = false, ovf[N];
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+        const bool ok = tl[t] && idx[t] < end[t];
+        if (ok) store_tail<IDX>(pool, pool16, w16[t], idx[t], k0[t], k1[t], docid);
+        ovf[t] = tl[t] && !ok;
+        anyo = anyo || ovf[t];
+    }
+    if (__any(anyo)) {  // region full (rare): the bucket's shared overflow list
+#pragma unroll
+        for (int t = 0; t < N; ++t) {
+            if (!ovf[t]) continue;
+            const uint32_t j = g_add(&A.onext[b[t]], 1u);
             if (j < A.ocap) {
-                GAS uint64_t *dst = gp(A.ovf) + ((uint64_t)b * A.ocap + j) * (IDX ? 3u : 2u);
-                dst[0] = k0;
-                dst[1] = k1;
+                GAS uint64_t *dst = gp(A.ovf) + ((uint64_t)b[t] * A.ocap + j) * (IDX ? 3u : 2u);
+                dst[0] = k0[t];
+                dst[1] = k1[t];
                 if (IDX) dst[2] = docid;
             } else {
                 g_add(&A.counters[CNT_OVF], 1ull);
             }
-        };
-        if (oA) spill(bA, a0, a1);
-        if (oB) spill(bB, b0, b1);
+        }
     }
 }
 
@@ -647,7 +686,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     const MapArgs &A = *Ap;
     // per wave: staged window, 2-segment mask windows, token queue (waves work on their own tiles)
     __shared__ __attribute__((aligned(16))) uint8_t s_win[NW][WIN];
-    __shared__ __attribute__((aligned(8))) uint64_t s_mp[NW][64];  // W(g)|W(g+1)<<16 | (S(g)|S(g+1)<<16)<<32
+    __shared__ __attribute__((aligned(8))) uint64_t s_mp[NW][NMP];  // W(g)|W(g+1)<<16 | (S(g)|S(g+1)<<16)<<32
     __shared__ uint16_t s_q[NW][QCAP];
     // LUT and length masks first in LDS (highest alignment): their base then fits the 16-bit
     // offset field of ds_read, so a lookup needs no separate address add
@@ -817,6 +856,76 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
 #else
 #define MRG_PT(i)
 #endif
+    // A token of the wave's queue: entry q (of total) holds its start s (block offset); its raw
+    // length, \w span and deleted bytes come from one 8-byte mask-pair read, its key bytes from the
+    // window.  fast: a key of <= 16 bytes ending inside the 2-segment window; slow: the rest (the
+    // exact walker).  Returns the deleted-byte runs still to squeeze out (more than one).
+    auto extract = [&](uint32_t q, uint32_t sraw, uint32_t total, bool &fast, bool &slow, uint32_t &s,
+                       uint64_t &tk0, uint64_t &tk1) -> uint32_t {
+        const bool act = q < total;
+        s = act ? sraw : 0u;
+        const uint64_t mw = mp[s >> 4];
+        const uint32_t Wp = (uint32_t)mw, Sp = (uint32_t)(mw >> 32);
+        const uint32_t i = s & 15u;
+        const uint32_t Sr = Sp >> i;
+        const uint32_t n = (uint32_t)__builtin_ctz(Sr | 0x80000000u);  // raw length (if Sr != 0)
+        const bool ended = Sr != 0u;                                     // end inside the 2 segments
+        const uint32_t w = __builtin_amdgcn_ubfe(Wp, i, n);              // \w bits of the raw token
+        const uint32_t first = (uint32_t)__builtin_ctz(w | 0x80000000u);
+        const uint32_t last = 31u - (uint32_t)__builtin_clz(w | 1u);
+        const uint32_t span = last - first + 1u;
+        // bitwise on purpose: lane masks combined by SALU, no per-lane selects
+        const bool wz = w == 0u, big = span > 16u;
+        fast = act & ended & !wz & !big;
+        slow = act & (!ended | (!wz & big));
+        // deleted bytes inside the token ("don't"): one 1-byte gap is folded into the selectors
+        // below (key bytes from the gap on come from one window byte later); tokens with more
+        // gaps squeeze them out afterwards
+        const uint32_t gaps = fast ? (~(w >> first) & ((1u << span) - 1u)) : 0u;
+        const bool one_gap = gaps != 0u && (gaps & (gaps - 1u)) == 0u;
+        const uint32_t ga = one_gap ? (uint32_t)__builtin_ctz(gaps) : 16u;
+        uint32_t tlen = one_gap ? span - 1u : span;
+        // key bytes of the window from s + first, big-endian packed, zero padded: output byte p
+        // of word j is key byte 4j + 3 - p (selector r + 3 - p [+ 1 past the gap], 0x0C = zero)
+        // the 17 window bytes from the key's first byte as five dwords: one unaligned 16-byte
+        // LDS read and one 4-byte read (gfx950 runs in unaligned access mode: no dword
+        // alignment, no v_alignbyte), then one selector word per output word
+        const uint32_t off = (uint32_t)BEHIND + s + first;
+        const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
+        const uint32_t dw = off >> 2, r = off & 3u;
+        const uint32_t d0 = win32[dw], d1 = win32[dw + 1], d2 = win32[dw + 2], d3 = win32[dw + 3],
+                       d4 = win32[dw + 4];
+        const u32x4 sl = *reinterpret_cast<const u32x4 *>(s_sel[(fast ? tlen : 0u) * 17u + ga]);
+        const uint32_t a0 = __builtin_amdgcn_alignbyte(d1, d0, r), a1 = __builtin_amdgcn_alignbyte(d2, d1, r),
+                       a2 = __builtin_amdgcn_alignbyte(d3, d2, r), a3 = __builtin_amdgcn_alignbyte(d4, d3, r),
+                       a4 = __builtin_amdgcn_alignbyte(0u, d4, r);
+        const uint32_t o0 = __builtin_amdgcn_perm(a1, a0, sl.x);
+        const uint32_t o1 = __builtin_amdgcn_perm(a2, a1, sl.y);
+        const uint32_t o2 = __builtin_amdgcn_perm(a3, a2, sl.z);
+        const uint32_t o3 = __builtin_amdgcn_perm(a4, a3, sl.w);
+        tk0 = ((uint64_t)o0 << 32) | o1;
+        tk1 = ((uint64_t)o2 << 32) | o3;
+        return one_gap ? 0u : gaps;  // gaps still to squeeze out
+    };
+    // squeeze out the remaining gaps (more than one deleted run inside the token; rare)
+    auto squeeze = [](uint32_t mgaps, uint64_t &tk0, uint64_t &tk1) {
+        while (mgaps) {
+            const uint32_t ga2 = (uint32_t)__builtin_ctz(mgaps);          // gap start (key byte)
+            const uint32_t gl = (uint32_t)__builtin_ctz(~(mgaps >> ga2)); // gap length
+            const uint32_t sh = 8u * gl;                                  // 8..120 bits
+            // shifted = (tk0:tk1) << sh; keep the top ga2 bytes, take the rest from shifted
+            uint64_t s0v, s1v;
+            if (sh >= 64u) { s0v = tk1 << (sh - 64u); s1v = 0; }
+            else { s0v = (tk0 << sh) | (tk1 >> (64u - sh)); s1v = tk1 << sh; }
+            const uint32_t kb = 8u * ga2;                                 // kept bits
+            const uint64_t k0m = kb >= 64u ? ~0ull : (kb ? ~0ull << (64u - kb) : 0ull);
+            const uint64_t k1m = kb <= 64u ? 0ull : ~0ull << (128u - kb);
+            tk0 = (tk0 & k0m) | (s0v & ~k0m);
+            tk1 = (tk1 & k1m) | (s1v & ~k1m);
+            mgaps = (mgaps >> (ga2 + gl)) << ga2;
+        }
+    };
+
     auto process_blk = [&](const BlkInfo &I, const Blk &X, uint64_t cblk, auto &&mid) {
         const uint64_t Ab = I.Ab, doc_lo = I.doc_lo, doc_hi = I.doc_hi;
         const uint32_t docid = I.docid;
@@ -932,6 +1041,131 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             return;
         }
 
+#if MRG_MAP_BR
+        {
+            // ---- the whole block: window [Ab - 16, Ab + 2048 + 64), staged bytes [Ab, whi)
+            const uint64_t whi = umin64(Ab + (uint64_t)(BLK + HALO), doc_hi);
+            const uint64_t wbase = Ab - (uint64_t)BEHIND;
+            const uint32_t tend = (uint32_t)umin64(doc_hi - Ab, (uint64_t)BLK);  // token starts only before this
+            const uint32_t m1_first = lane_u32(m1, 0), m0_last = lane_u32(m0, 63);
+            wave_sync_lds();  // the previous block's readers are done (program order)
+            reinterpret_cast<uint4 *>(win)[1 + lane] = X.v0;
+            reinterpret_cast<uint4 *>(win)[65 + lane] = X.v1;
+            if (lane >= 1 && lane < 5) reinterpret_cast<uint4 *>(win)[128 + lane] = X.e;  // the halo
+            // masks of this lane's segment and the next one, tile 0 (pairs 0..63) and tile 1 (64..127)
+            uint32_t mn0 = from_next_lane(m0), mn1 = from_next_lane(m1);
+            uint32_t pv0 = from_prev_lane(m0) >> 31, pv1 = from_prev_lane(m1) >> 31;
+            if (lane == 63) {
+                mn0 = m1_first;
+                mn1 = mh;
+            }
+            if (lane == 0) {
+                pv0 = prev_blk;
+                pv1 = m0_last >> 31;
+            }
+            mp[lane] = (uint64_t)((m0 & 0xFFFFu) | (mn0 << 16)) | ((uint64_t)((m0 >> 16) | (mn0 & 0xFFFF0000u)) << 32);
+            mp[64 + lane] = (uint64_t)((m1 & 0xFFFFu) | (mn1 << 16)) | ((uint64_t)((m1 >> 16) | (mn1 & 0xFFFF0000u)) << 32);
+            // token starts (a non-space byte after a space), both tiles' counts in one wave prefix sum
+            const uint32_t S0 = m0 >> 16, S1 = m1 >> 16;
+            uint32_t st0 = ~S0 & ((S0 << 1) | pv0) & 0xFFFFu, st1 = ~S1 & ((S1 << 1) | pv1) & 0xFFFFu;
+            if (l16 >= tend) st0 = 0;
+            if (1024u + l16 >= tend) st1 = 0;
+            const uint32_t c0 = __builtin_popcount(st0), c1 = __builtin_popcount(st1);
+            const uint32_t incl = wave_incl_scan(c0 | (c1 << 16));
+            const uint32_t tot = lane_u32(incl, 63);
+            uint32_t pos0 = (incl & 0xFFFFu) - c0, pos1 = (tot & 0xFFFFu) + (incl >> 16) - c1;
+            if (abl & 64u) {  // timing only: no queue writes, no tokens
+                my_tokens += (st0 ^ st1) & 1u;
+                st0 = st1 = 0;
+            }
+            while (st0) {
+                const uint32_t kb = (uint32_t)__builtin_ctz(st0);
+                st0 &= st0 - 1u;
+                queue[pos0++] = (uint16_t)(l16 + kb);
+            }
+            while (st1) {
+                const uint32_t kb = (uint32_t)__builtin_ctz(st1);
+                st1 &= st1 - 1u;
+                queue[pos1++] = (uint16_t)(1024u + l16 + kb);
+            }
+            const uint32_t total = (abl & 68u) ? 0u : (tot & 0xFFFFu) + (tot >> 16);
+            MRG_PT(2);
+            uint32_t nslow = 0;
+            const bool may_claim =
+                __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+                (uint32_t)CAP;
+            my_tokens += (abl & 4u) ? c0 + c1 : 0u;
+            wave_sync_lds();
+            // FOUR tokens per lane per round (entries q, q + 64, q + 128, q + 192); the queue, the masks
+            // and the window are read-only now
+            for (uint32_t base = 0; base < total; base += 256) {
+                bool fs[4], sl[4];
+                uint32_t sv[4], gp4[4];
+                uint64_t a0[4], a1[4];
+                uint32_t rq[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    rq[t] = queue[min(base + (uint32_t)lane + 64u * t, (uint32_t)QCAP - 1u)];
+                bool anyg = false;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    gp4[t] = extract(base + (uint32_t)lane + 64u * t, rq[t], total, fs[t], sl[t], sv[t], a0[t], a1[t]);
+                    anyg = anyg || gp4[t] != 0u;
+                }
+                if (__any(anyg)) {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) squeeze(gp4[t], a0[t], a1[t]);
+                }
+                // slow tokens (past the 2-segment window, or > 16 raw key bytes) are deferred: their
+                // starts go to the consumed front of the queue
+                uint64_t ms[4];
+                bool anys = false;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    ms[t] = __ballot(sl[t]);
+                    anys = anys || ms[t] != 0ull;
+                }
+                if (anys) {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(ms[t] >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)ms[t], 0u));
+                        if (sl[t]) queue[nslow + rk] = (uint16_t)sv[t];
+                        nslow += (uint32_t)__builtin_popcountll(ms[t]);
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) my_tokens += fs[t] ? 1u : 0u;
+                emit_fastN<4>(A, abl, hbits, table, tails, pool, pool16, fs, a0, a1, docid, may_claim);
+            }
+            // deferred slow tokens: the exact per-codepoint walker, one token per lane (forward
+            // reads only: the staged bytes are [Ab, whi))
+            MRG_PT(3);
+            if (nslow) {
+                wave_sync_lds();
+                auto rd = [&](uint64_t a) -> uint32_t {
+                    if (a >= Ab && a < whi) return (uint32_t)win[a - wbase];
+                    return (uint32_t)gp(A.in)[a];
+                };
+                for (uint32_t base = 0; base < nslow; base += 64) {
+                    const uint32_t q = base + (uint32_t)lane;
+                    bool have = false;
+                    uint64_t tk0 = 0, tk1 = 0, a = 0;
+                    uint32_t tlen = 0, traw = 0;
+                    if (q < nslow) {
+                        a = Ab + queue[q];
+                        uint64_t e2;
+                        if (walk_token(rd, a, doc_hi, A.counters, tk0, tk1, tlen, e2) && tlen > 0) {
+                            have = true;
+                            traw = (uint32_t)(e2 - a);
+                        }
+                    }
+                    my_tokens += have ? 1u : 0u;
+                    emit(A, table, tails, have, tk0, tk1, tlen, a, traw, docid);
+                }
+            }
+        }
+#else
 #pragma unroll
         for (uint32_t j = 0; j < NSUB; ++j) {
             const uint64_t At = Ab + (uint64_t)j * TILE;
@@ -988,73 +1222,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             wave_sync_lds();
 
             // tokens of the queue, TWO per lane per round (entries q and q + 64: two independent LDS
-            // dependency chains in one instruction stream, so each wait covers both); the queue, masks
-            // and window are read-only now
-            auto extract = [&](uint32_t q, uint32_t sraw, bool &fast, bool &slow, uint32_t &s, uint64_t &tk0,
-                               uint64_t &tk1) {
-                const bool act = q < total;
-                s = act ? sraw : 0u;
-                const uint64_t mw = mp[s >> 4];
-                const uint32_t Wp = (uint32_t)mw, Sp = (uint32_t)(mw >> 32);
-                const uint32_t i = s & 15u;
-                const uint32_t Sr = Sp >> i;
-                const uint32_t n = (uint32_t)__builtin_ctz(Sr | 0x80000000u);  // raw length (if Sr != 0)
-                const bool ended = Sr != 0u;                                     // end inside the 2 segments
-                const uint32_t w = __builtin_amdgcn_ubfe(Wp, i, n);              // \w bits of the raw token
-                const uint32_t first = (uint32_t)__builtin_ctz(w | 0x80000000u);
-                const uint32_t last = 31u - (uint32_t)__builtin_clz(w | 1u);
-                const uint32_t span = last - first + 1u;
-                // bitwise on purpose: lane masks combined by SALU, no per-lane selects
-                const bool wz = w == 0u, big = span > 16u;
-                fast = act & ended & !wz & !big;
-                slow = act & (!ended | (!wz & big));
-                // deleted bytes inside the token ("don't"): one 1-byte gap is folded into the selectors
-                // below (key bytes from the gap on come from one window byte later); tokens with more
-                // gaps squeeze them out afterwards
-                const uint32_t gaps = fast ? (~(w >> first) & ((1u << span) - 1u)) : 0u;
-                const bool one_gap = gaps != 0u && (gaps & (gaps - 1u)) == 0u;
-                const uint32_t ga = one_gap ? (uint32_t)__builtin_ctz(gaps) : 16u;
-                uint32_t tlen = one_gap ? span - 1u : span;
-                // key bytes of the window from s + first, big-endian packed, zero padded: output byte p
-                // of word j is key byte 4j + 3 - p (selector r + 3 - p [+ 1 past the gap], 0x0C = zero)
-                // the 17 window bytes from the key's first byte as five dwords: one unaligned 16-byte
-                // LDS read and one 4-byte read (gfx950 runs in unaligned access mode: no dword
-                // alignment, no v_alignbyte), then one selector word per output word
-                const uint32_t off = (uint32_t)BEHIND + s + first;
-                const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
-                const uint32_t dw = off >> 2, r = off & 3u;
-                const uint32_t d0 = win32[dw], d1 = win32[dw + 1], d2 = win32[dw + 2], d3 = win32[dw + 3],
-                               d4 = win32[dw + 4];
-                const u32x4 sl = *reinterpret_cast<const u32x4 *>(s_sel[(fast ? tlen : 0u) * 17u + ga]);
-                const uint32_t a0 = __builtin_amdgcn_alignbyte(d1, d0, r), a1 = __builtin_amdgcn_alignbyte(d2, d1, r),
-                               a2 = __builtin_amdgcn_alignbyte(d3, d2, r), a3 = __builtin_amdgcn_alignbyte(d4, d3, r),
-                               a4 = __builtin_amdgcn_alignbyte(0u, d4, r);
-                const uint32_t o0 = __builtin_amdgcn_perm(a1, a0, sl.x);
-                const uint32_t o1 = __builtin_amdgcn_perm(a2, a1, sl.y);
-                const uint32_t o2 = __builtin_amdgcn_perm(a3, a2, sl.z);
-                const uint32_t o3 = __builtin_amdgcn_perm(a4, a3, sl.w);
-                tk0 = ((uint64_t)o0 << 32) | o1;
-                tk1 = ((uint64_t)o2 << 32) | o3;
-                return one_gap ? 0u : gaps;  // gaps still to squeeze out
-            };
-            // squeeze out the remaining gaps (more than one deleted run inside the token; rare)
-            auto squeeze = [](uint32_t mgaps, uint64_t &tk0, uint64_t &tk1) {
-                while (mgaps) {
-                    const uint32_t ga2 = (uint32_t)__builtin_ctz(mgaps);          // gap start (key byte)
-                    const uint32_t gl = (uint32_t)__builtin_ctz(~(mgaps >> ga2)); // gap length
-                    const uint32_t sh = 8u * gl;                                  // 8..120 bits
-                    // shifted = (tk0:tk1) << sh; keep the top ga2 bytes, take the rest from shifted
-                    uint64_t s0v, s1v;
-                    if (sh >= 64u) { s0v = tk1 << (sh - 64u); s1v = 0; }
-                    else { s0v = (tk0 << sh) | (tk1 >> (64u - sh)); s1v = tk1 << sh; }
-                    const uint32_t kb = 8u * ga2;                                 // kept bits
-                    const uint64_t k0m = kb >= 64u ? ~0ull : (kb ? ~0ull << (64u - kb) : 0ull);
-                    const uint64_t k1m = kb <= 64u ? 0ull : ~0ull << (128u - kb);
-                    tk0 = (tk0 & k0m) | (s0v & ~k0m);
-                    tk1 = (tk1 & k1m) | (s1v & ~k1m);
-                    mgaps = (mgaps >> (ga2 + gl)) << ga2;
-                }
-            };
+            // dependency chains in one instruction stream, so each wait covers both)
             for (uint32_t base = 0; base < total; base += 128) {
                 bool fa, sa, fb, sb;
                 uint32_t sA, sB;
@@ -1063,8 +1231,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 // bounds), so the two chains share every LDS wait
                 const uint32_t qa = base + (uint32_t)lane, qb = qa + 64u;
                 const uint32_t ra = queue[min(qa, (uint32_t)QCAP - 1u)], rb = queue[min(qb, (uint32_t)QCAP - 1u)];
-                uint32_t ga = extract(qa, ra, fa, sa, sA, a0, a1);
-                uint32_t gb = extract(qb, rb, fb, sb, sB, b0, b1);
+                uint32_t ga = extract(qa, ra, total, fa, sa, sA, a0, a1);
+                uint32_t gb = extract(qb, rb, total, fb, sb, sB, b0, b1);
                 if (__any((ga | gb) != 0u)) {
                     squeeze(ga, a0, a1);
                     squeeze(gb, b0, b1);
@@ -1082,7 +1250,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                     nslow += na + (uint32_t)__builtin_popcountll(mb);
                 }
                 my_tokens += (fa ? 1u : 0u) + (fb ? 1u : 0u);
-                emit_fast2(A, abl, hbits, table, tails, pool, pool16, fa, a0, a1, fb, b0, b1, docid, may_claim);
+                const bool hv[2] = {fa, fb};
+                const uint64_t kk0[2] = {a0, b0}, kk1[2] = {a1, b1};
+                emit_fastN<2>(A, abl, hbits, table, tails, pool, pool16, hv, kk0, kk1, docid, may_claim);
             }
             // deferred slow tokens: the exact per-codepoint walker, one token per lane (forward
             // reads only: the staged bytes are [At, whi))
@@ -1111,6 +1281,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 }
             }
         }
+#endif
         MRG_PT(4);
     };
 

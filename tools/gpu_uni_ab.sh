@@ -1,7 +1,8 @@
 #!/bin/bash
-# tools/gpu_uni.sh, then an A/B of the C3 (ASCII) map against lib_variants/nouni (the same sources
-# built with -DMRG_MAP_NO_UNI: non-ASCII tiles to the exact walker, as in r03).
+# tools/gpu_uni.sh (tests + C3 / zipf_u / C5 benches), then A/Bs of the map against
+# lib_variants/tile (-DMRG_MAP_BR=0: tile-by-tile rounds, 16 waves) on C3 and on zipf_u.
 bash tools/gpu_uni.sh; rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-VARIANTS="lib_variants/nouni lib lib_variants/nouni lib" STEPS=6 bash tools/gpu_ab.sh || exit $?
+VARIANTS="lib_variants/tile lib lib_variants/tile lib" STEPS=6 bash tools/gpu_ab.sh || exit $?
+VARIANTS="lib_variants/tile lib" STEPS=4 BENCH_ARGS="--workload zipf_u" bash tools/gpu_ab.sh || exit $?
 exit $rc
