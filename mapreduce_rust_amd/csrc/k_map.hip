@@ -45,7 +45,7 @@ namespace {
 // typical block (~245 tokens at C3) -- with 12 waves per workgroup (3 per SIMD, up to 168 VGPRs).
 // MRG_MAP_BR=0: the r03 structure, tile by tile, two tokens per lane, 16 waves.
 #ifndef MRG_MAP_BR
-#define MRG_MAP_BR 1
+#define MRG_MAP_BR 0
 #endif
 constexpr int NW = MRG_MAP_BR ? 12 : MRG_MAP_WAVES;
 constexpr int WG = 64 * NW;
