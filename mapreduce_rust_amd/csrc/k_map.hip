@@ -39,15 +39,11 @@
 
 namespace {
 
-// Block rounds (r04, MRG_MAP_BR=1): both tiles of a block are staged together (one window of the
-// 2 KiB block + halo, 128 mask pairs, one queue of the block's starts) and tokenized by rounds of
-// FOUR tokens per lane -- four independent LDS chains in one instruction stream, one round for a
-// typical block (~245 tokens at C3) -- with 12 waves per workgroup (3 per SIMD, up to 168 VGPRs).
-// MRG_MAP_BR=0: the r03 structure, tile by tile, two tokens per lane, 16 waves.
-#ifndef MRG_MAP_BR
-#define MRG_MAP_BR 0
-#endif
-constexpr int NW = MRG_MAP_BR ? 12 : MRG_MAP_WAVES;
+// Block rounds (r04, MRG_MAP_BR=1 in commit 5e363df, since removed): both tiles of a block tokenized
+// by rounds of four tokens per lane with 12 waves per workgroup -- slower (157 VGPRs, 3 waves per
+// SIMD).  The block's bytes are staged together (one window of the 2 KiB
+// block, the 16 bytes before it and the halo), then its tiles are tokenized one by one.
+constexpr int NW = MRG_MAP_WAVES;
 constexpr int WG = 64 * NW;
 constexpr int SEG = MRG_MAP_SEG;
 constexpr int TILE = MRG_MAP_TILE;
@@ -56,9 +52,9 @@ constexpr int BEHIND = MRG_MAP_BEHIND;
 constexpr int NSUB = MRG_MAP_NSUB;               // 1 KiB tiles per block
 constexpr int BLK = NSUB * TILE;                 // bytes per wave iteration
 // staged window + slack for the 5-dword key reads (a key starts within 31 bytes of a token start)
-constexpr int WIN = MRG_MAP_BR ? BEHIND + BLK + HALO + 16 : BEHIND + TILE + HALO + 48;
-constexpr int QCAP = MRG_MAP_BR ? BLK / 2 : TILE / 2;  // a start needs a space before it
-constexpr int NMP = MRG_MAP_BR ? 2 * 64 : 64;          // mask pairs per wave (one per staged segment)
+constexpr int WIN = BEHIND + BLK + HALO + 48;
+constexpr int QCAP = TILE / 2 + 16;  // a start needs a space before it; <= 520 codepoint leads
+constexpr int NMP = 64;         // mask pairs per wave (one per segment of the tile)
 static_assert(TILE == 64 * SEG, "one segment per lane");
 static_assert(WIN % 16 == 0, "16-byte window rows");
 
@@ -612,22 +608,8 @@ __device__ __forceinline__ uint32_t generic_tile(const MapArgs &A, LdsTable<CAP,
 }
 
 // ---- UTF-8-exact byte classes for blocks with a non-ASCII byte where the fast path reads (the
-// block's two tiles, the first segment of its halo, the byte before it).  Per lane and only where its
-// own bytes are not all ASCII, the codepoints covering them are decoded from a 24-byte register window
-// [so - 4, so + 20) -- the 4 bytes before the segment (its neighbour lane's last word), its 16 bytes
-// and the 4 after -- and every byte of a codepoint gets the codepoint's class (W, S or deleted).
-// Offsets are block-relative; [lo, hi) is the document clamped to the staged range.
+// block's two tiles, the first segment of its halo, the byte before it): see k_map's block step.
 #define LDS __attribute__((address_space(3)))
-struct SegWin {
-    uint32_t w0, w1, w2, w3, w4, w5;
-};
-// bytes [idx, idx + 4) of the window, idx in [0, 20) (first byte in bits 0..7)
-__device__ __forceinline__ uint32_t seg_win4(const SegWin &s, int idx) {
-    const int d = idx >> 2;
-    const uint32_t lo = d == 0 ? s.w0 : d == 1 ? s.w1 : d == 2 ? s.w2 : d == 3 ? s.w3 : s.w4;
-    const uint32_t hi = d == 0 ? s.w1 : d == 1 ? s.w2 : d == 2 ? s.w3 : d == 3 ? s.w4 : s.w5;
-    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(idx & 3));
-}
 // class of codepoint cp: U+0080..07FF and U+2000..20FF from the LDS copy uc, the rest from the table
 __device__ __forceinline__ uint32_t uni_class(const LDS uint8_t *uc, uint32_t cp) {
     uint32_t byte;
@@ -636,49 +618,6 @@ __device__ __forceinline__ uint32_t uni_class(const LDS uint8_t *uc, uint32_t cp
     else return mrg_uclass(cp);
     return (byte >> (2u * (cp & 3u))) & 3u;
 }
-// W16 | S16 << 16 of the 16 bytes at block offset so (window s): mlut for ASCII bytes and for bytes
-// outside [lo, hi) or below position pmin, the codepoint's class for the others; bad = not valid UTF-8
-__device__ __forceinline__ uint32_t uni_fix(const SegWin &s, int so, uint32_t mlut, int lo, int hi, int pmin,
-                                            const LDS uint8_t *uc, bool &bad) {
-    auto hb = [](uint32_t d) { return ((((d & 0x80808080u) >> 7) * 0x00204081u) >> 21) & 0xFu; };
-    uint32_t nam = hb(s.w1) | (hb(s.w2) << 4) | (hb(s.w3) << 8) | (hb(s.w4) << 12);
-    const int vlo = max(max(lo - so, 0), pmin), vhi = min(hi - so, 16);
-    nam &= vhi > vlo ? (((1u << vhi) - 1u) & ~((1u << vlo) - 1u)) : 0u;
-    uint32_t W = mlut & 0xFFFFu & ~nam, S = (mlut >> 16) & ~nam;
-    while (nam) {
-        const int p = __builtin_ctz(nam);
-        int lead = p;
-        if ((seg_win4(s, p + 4) & 0xC0u) == 0x80u) {  // a continuation: its lead is 1..3 bytes back
-            const uint32_t back = seg_win4(s, p + 1);  // bytes p - 3 .. p
-            int k = 0;
-            if (mrg_is_cont((back >> 16) & 0xFFu)) {
-                k = 1;
-                if (mrg_is_cont((back >> 8) & 0xFFu)) k = (mrg_is_cont(back & 0xFFu)) ? 3 : 2;
-            }
-            lead = p - 1 - k;
-            if (k == 3 || so + lead < lo) {
-                bad = true;
-                break;
-            }
-        }
-        const uint32_t v = seg_win4(s, lead + 4);
-        auto rd = [&](uint64_t a) -> uint32_t { return (v >> (8u * (uint32_t)a)) & 0xFFu; };
-        uint32_t cp = 0, raw;
-        const int n = mrg_utf8_decode(rd, 0ull, (uint64_t)min(hi - (so + lead), 4), &cp, &raw);
-        if (n == 0 || lead + n <= p) {
-            bad = true;
-            break;
-        }
-        const uint32_t c = uni_class(uc, cp);
-        const int e = min(lead + n, 16);
-        const uint32_t span = ((1u << e) - 1u) & ~((1u << p) - 1u);
-        if (c == MRG_CLS_W) W |= span;
-        else if (c == MRG_CLS_S) S |= span;
-        nam &= ~span;
-    }
-    return W | (S << 16);
-}
-
 template <int CAP, bool IDX>
 __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // the arguments live in device memory (not the kernarg segment): fields are loaded where they
@@ -856,11 +795,11 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
 #else
 #define MRG_PT(i)
 #endif
-    // A token of the wave's queue: entry q (of total) holds its start s (block offset); its raw
+    // A token of the wave's queue: entry q (of total) holds its start s (tile offset); its raw
     // length, \w span and deleted bytes come from one 8-byte mask-pair read, its key bytes from the
     // window.  fast: a key of <= 16 bytes ending inside the 2-segment window; slow: the rest (the
     // exact walker).  Returns the deleted-byte runs still to squeeze out (more than one).
-    auto extract = [&](uint32_t q, uint32_t sraw, uint32_t total, bool &fast, bool &slow, uint32_t &s,
+    auto extract = [&](uint32_t tb, uint32_t q, uint32_t sraw, uint32_t total, bool &fast, bool &slow, uint32_t &s,
                        uint64_t &tk0, uint64_t &tk1) -> uint32_t {
         const bool act = q < total;
         s = act ? sraw : 0u;
@@ -890,7 +829,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         // the 17 window bytes from the key's first byte as five dwords: one unaligned 16-byte
         // LDS read and one 4-byte read (gfx950 runs in unaligned access mode: no dword
         // alignment, no v_alignbyte), then one selector word per output word
-        const uint32_t off = (uint32_t)BEHIND + s + first;
+        const uint32_t off = (uint32_t)BEHIND + tb + s + first;  // tb = the tile's block offset
         const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
         const uint32_t dw = off >> 2, r = off & 3u;
         const uint32_t d0 = win32[dw], d1 = win32[dw + 1], d2 = win32[dw + 2], d3 = win32[dw + 3],
@@ -924,6 +863,46 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             tk1 = (tk1 & k1m) | (s1v & ~k1m);
             mgaps = (mgaps >> (ga2 + gl)) << ga2;
         }
+    };
+
+    // A deferred slow token through the tile's byte classes (r04): the mask pairs mp[] hold W16 / S16
+    // of every segment of the tile, exact for UTF-8 too (pair k = segments k and k + 1, so the last
+    // pair's high halves are the first halo segment), and the window holds its bytes -- the token's
+    // end and key need no codepoint decoding: the key is the W bytes before the first S byte.  s = the
+    // token's tile offset, tb the tile's block offset, nseg = the tile's segments.  False when the token runs past the first halo
+    // segment (then the codepoint walker).
+    auto mask_walk = [&](uint32_t tb, uint32_t s, uint32_t nseg, uint64_t &tk0, uint64_t &tk1, uint32_t &tlen,
+                         uint32_t &traw) -> bool {
+        tk0 = 0;
+        tk1 = 0;
+        tlen = 0;
+        const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
+        uint32_t i = s & 15u;
+        for (uint32_t seg = s >> 4; seg <= nseg; ++seg, i = 0) {
+            const uint64_t mw = mp[seg < nseg ? seg : nseg - 1u];
+            const uint32_t sh = seg < nseg ? 0u : 16u;
+            uint32_t W = ((((uint32_t)mw >> sh) & 0xFFFFu) >> i) << i;
+            const uint32_t S = ((((uint32_t)(mw >> 32) >> sh) & 0xFFFFu) >> i) << i;
+            const uint32_t e = S ? (uint32_t)__builtin_ctz(S) : 16u;
+            W &= (1u << e) - 1u;
+            if (W && tlen < 16u) {  // key bytes (only the first 16 are packed)
+                const uint32_t o = ((uint32_t)BEHIND + tb) / 4u + 4u * seg;
+                const uint32_t d0 = win32[o], d1 = win32[o + 1], d2 = win32[o + 2], d3 = win32[o + 3];
+                while (W && tlen < 16u) {
+                    const uint32_t b = (uint32_t)__builtin_ctz(W);
+                    W &= W - 1u;
+                    const uint32_t d = (b & 8u) ? ((b & 4u) ? d3 : d2) : ((b & 4u) ? d1 : d0);
+                    mrg_key_append(tk0, tk1, tlen, __builtin_amdgcn_ubfe(d, 8u * (b & 3u), 8));
+                    ++tlen;
+                }
+            }
+            tlen += (uint32_t)__builtin_popcount(W);
+            if (S) {
+                traw = 16u * seg + e - s;
+                return true;
+            }
+        }
+        return false;
     };
 
     auto process_blk = [&](const BlkInfo &I, const Blk &X, uint64_t cblk, auto &&mid) {
@@ -983,18 +962,26 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         // after which both tiles are tokenized exactly like ASCII tiles -- every byte of a codepoint
         // carries its class, so the W / S masks mean the same.  Invalid UTF-8 defers the block's tiles
         // to generic_tile after the main loop (which reports the first bad byte).
+        // stage the block: the 16 bytes before it, both tiles, the 64-byte halo (the previous block's
+        // readers are done: program order)
+        wave_sync_lds();
+        reinterpret_cast<uint4 *>(win)[1 + lane] = X.v0;
+        reinterpret_cast<uint4 *>(win)[65 + lane] = X.v1;
+        if (lane < 5) reinterpret_cast<uint4 *>(win)[lane == 0 ? 0 : 128 + lane] = X.e;
         bool defer_blk = false;
         if (__any(n0 || n1 || (lane <= 1 && ne))) {
 #ifdef MRG_MAP_NO_UNI
             defer_blk = true;  // A/B builds only: every such block to the exact walker, as in r03
 #else
-            // neighbour words, in uniform control flow (DPP and readlane before the divergent decode)
-            const uint32_t p0 = from_prev_lane(X.v0.w), q0 = from_next_lane(X.v0.x);
-            const uint32_t p1 = from_prev_lane(X.v1.w), q1 = from_next_lane(X.v1.x);
-            const uint32_t before = lane_u32(X.e.w, 0);   // block bytes -4..-1
-            const uint32_t t0last = lane_u32(X.v0.w, 63), t1first = lane_u32(X.v1.x, 0);
-            const uint32_t h0 = lane_u32(X.e.x, 1), h1 = lane_u32(X.e.y, 1), h2 = lane_u32(X.e.z, 1),
-                           h3 = lane_u32(X.e.w, 1), h4 = lane_u32(X.e.x, 2);  // halo bytes 0..19
+            // UTF-8-exact classes by codepoint compaction: every lane lists the codepoint leads (bytes
+            // >= 0xC0 inside the document) of its segments, a wave prefix sum packs them into the
+            // queue, and each lane decodes ONE codepoint per round from the staged window -- one round
+            // for up to 64 codepoints (a per-lane walk over its segment's codepoints made the wave wait
+            // for its busiest lane, once per segment kind).  The owners read their leads' lengths and
+            // classes back in order; a codepoint's last bytes may lie in the next segment (DPP).  Every
+            // non-ASCII byte must be covered by a decoded codepoint, else the block holds invalid UTF-8
+            // and is deferred.  Two chunks (tile 0 with the codepoint holding the byte before the block,
+            // tile 1 with the first halo segment) keep the queue at <= 520 entries.
             const int64_t dlo = (int64_t)(doc_lo - Ab);  // two's complement (see lo below)
             // the document in block offsets: lo in [-16, 16), hi in (0, 2112].  (A select on
             // doc_lo > Ab lost its first case in the compiled code: keep a clamped signed difference.)
@@ -1002,19 +989,124 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const int hi = (int)umin64(doc_hi - Ab, (uint64_t)(BLK + HALO));
             const LDS uint8_t *uc = (const LDS uint8_t *)s_uc;
             bool bad = false;
-            const SegWin s0{lane == 0 ? before : p0, X.v0.x, X.v0.y, X.v0.z, X.v0.w, lane == 63 ? t1first : q0};
-            const SegWin s1{lane == 0 ? t0last : p1, X.v1.x, X.v1.y, X.v1.z, X.v1.w, lane == 63 ? h0 : q1};
-            m0 = uni_fix(s0, (int)l16, m0, lo, hi, 0, uc, bad);
-            m1 = uni_fix(s1, (int)(1024u + l16), m1, lo, hi, 0, uc, bad);
-            uint32_t mh_l = mh, pb_l = prev_blk;
-            if (lane == 63) {  // the first halo segment
-                const SegWin sh{X.v1.w, h0, h1, h2, h3, h4};
-                mh_l = uni_fix(sh, BLK, mh, lo, hi, 0, uc, bad);
+            auto hb = [](uint32_t d) { return ((((d & 0x80808080u) >> 7) * 0x00204081u) >> 21) & 0xFu; };
+            // non-ASCII bytes and leads of the 16 bytes x at block offset so, inside [lo, hi)
+            auto seg_masks = [&](const uint4 &x, int so, uint32_t &nam, uint32_t &lead) {
+                const int vlo = max(lo - so, 0), vhi = min(hi - so, 16);
+                const uint32_t rm = vhi > vlo ? (((1u << vhi) - 1u) & ~((1u << vlo) - 1u)) : 0u;
+                nam = (hb(x.x) | (hb(x.y) << 4) | (hb(x.z) << 8) | (hb(x.w) << 12)) & rm;
+                lead = (hb(x.x & (x.x << 1)) | (hb(x.y & (x.y << 1)) << 4) | (hb(x.z & (x.z << 1)) << 8) |
+                        (hb(x.w & (x.w << 1)) << 12)) & rm;
+            };
+            uint32_t nam0, ld0, nam1, ld1, namh, ldh;
+            seg_masks(X.v0, (int)l16, nam0, ld0);
+            seg_masks(X.v1, 1024 + (int)l16, nam1, ld1);
+            const uint4 xh{lane_u32(X.e.x, 1), lane_u32(X.e.y, 1), lane_u32(X.e.z, 1), lane_u32(X.e.w, 1)};
+            seg_masks(xh, BLK, namh, ldh);  // the first halo segment: lane 63's
+            if (lane != 63) namh = ldh = 0u;
+            // the byte before the block (inside the document and not ASCII): the lead of its codepoint,
+            // 1..4 bytes back (wave-uniform)
+            const uint32_t before = lane_u32(X.e.w, 0);  // block bytes -4..-1
+            int pbp = 0;
+            bool has_b = false;
+            if (dlo < 0 && (before >> 24) >= 0x80u) {
+                uint32_t bb = before >> 24;
+                pbp = -1;
+                for (int k = 2; k <= 4 && (bb & 0xC0u) == 0x80u; ++k) {
+                    bb = (before >> (8 * (4 - k))) & 0xFFu;
+                    pbp = -k;
+                }
+                if (bb < 0xC0u || pbp < lo) bad = true;
+                else has_b = true;
             }
-            if (lane == 0 && dlo < 0 && (before >> 24) >= 0x80u) {  // the byte before the block: its codepoint
-                const SegWin sb{0u, X.e.x, X.e.y, X.e.z, X.e.w, X.v0.x};
-                pb_l = uni_fix(sb, -16, 0u, lo, hi, 12, uc, bad) >> 31;
+            const uint32_t hasb = (lane == 0 && has_b) ? 1u : 0u;
+            const uint32_t c0 = (uint32_t)__builtin_popcount(ld0) + hasb;
+            const uint32_t c1 = (uint32_t)__builtin_popcount(ld1) + (uint32_t)__builtin_popcount(ldh);
+            const uint32_t incl = wave_incl_scan(c0 | (c1 << 16));
+            const uint32_t tot = lane_u32(incl, 63);
+            const uint32_t e0 = (incl & 0xFFFFu) - c0, e1 = (incl >> 16) - c1;  // first slots
+            // decode queue entries [0, n): block offset + 16 in, length | class << 3 out (0: invalid)
+            auto decode = [&](uint32_t n) {
+                wave_sync_lds();
+                const uint32_t *w32 = reinterpret_cast<const uint32_t *>(win);
+                for (uint32_t base = 0; base < n; base += 64) {
+                    const uint32_t j = base + (uint32_t)lane;
+                    if (j < n) {
+                        const uint32_t e = queue[j];
+                        const uint32_t v = __builtin_amdgcn_alignbyte(w32[(e >> 2) + 1u], w32[e >> 2], e & 3u);
+                        auto rd = [&](uint64_t a) -> uint32_t { return (v >> (8u * (uint32_t)a)) & 0xFFu; };
+                        uint32_t cp = 0, raw;
+                        const int ln = mrg_utf8_decode(rd, 0ull, (uint64_t)min(hi - ((int)e - BEHIND), 4), &cp, &raw);
+                        queue[j] = (uint16_t)(ln > 0 ? (uint32_t)ln | (uni_class(uc, cp) << 3) : 0u);
+                    }
+                }
+                wave_sync_lds();
+            };
+            // the decoded codepoints of leads ld (first slot k) as W, S and covered-byte masks; bits 16..18
+            // are bytes of the next segment
+            auto own = [&](uint32_t ld, uint32_t k, uint32_t &W, uint32_t &S, uint32_t &C) {
+                W = S = C = 0u;
+                for (uint32_t m = ld; m; m &= m - 1u, ++k) {
+                    const uint32_t r = queue[k], n = r & 7u, cl = r >> 3;
+                    bad |= n == 0u;
+                    const uint32_t span = ((1u << n) - 1u) << __builtin_ctz(m);
+                    C |= span;
+                    W |= cl == MRG_CLS_W ? span : 0u;
+                    S |= cl == MRG_CLS_S ? span : 0u;
+                }
+            };
+            // chunk 0: the codepoint before the block, tile 0
+            {
+                uint32_t k = e0;
+                if (hasb) queue[k++] = (uint16_t)(BEHIND + pbp);
+                for (uint32_t m = ld0; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + l16 + __builtin_ctz(m));
             }
+            decode(tot & 0xFFFFu);
+            uint32_t W0, S0, C0, bsp = 0, pb_l = prev_blk;
+            if (hasb) {  // its bytes from 0 on spill into tile 0's first segment; byte -1 gives prev_blk
+                const uint32_t r = queue[e0], n = r & 7u, cl = r >> 3;
+                const int end = pbp + (int)n;
+                if (n == 0u || end < 0) {
+                    bad = true;
+                } else {
+                    const uint32_t sp = (1u << end) - 1u;
+                    bsp = sp | ((cl == MRG_CLS_W ? sp : 0u) << 4) | ((cl == MRG_CLS_S ? sp : 0u) << 8);
+                    pb_l = cl == MRG_CLS_S ? 1u : 0u;
+                }
+            }
+            own(ld0, e0 + hasb, W0, S0, C0);
+            // chunk 1: tile 1, the first halo segment (the queue is reused: chunk 0 is read)
+            wave_sync_lds();
+            {
+                uint32_t k = e1;
+                for (uint32_t m = ld1; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + 1024u + l16 + __builtin_ctz(m));
+                for (uint32_t m = ldh; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + BLK + __builtin_ctz(m));
+            }
+            decode(tot >> 16);
+            uint32_t W1, S1, C1, Wh, Sh, Ch;
+            own(ld1, e1, W1, S1, C1);
+            own(ldh, e1 + (uint32_t)__builtin_popcount(ld1), Wh, Sh, Ch);
+            // spills (C | W << 4 | S << 8 of bits 16..18) into the next segment: lane l+1, tile 1's lane
+            // 0 after tile 0's lane 63, the halo segment after tile 1's lane 63 (same lane)
+            auto pack = [](uint32_t W, uint32_t S, uint32_t C) { return (C >> 16) | ((W >> 16) << 4) | ((S >> 16) << 8); };
+            const uint32_t sp0 = pack(W0, S0, C0), sp1 = pack(W1, S1, C1);
+            uint32_t in0 = from_prev_lane(sp0), in1 = from_prev_lane(sp1);
+            const uint32_t sp0_last = lane_u32(sp0, 63);
+            if (lane == 0) {
+                in0 = bsp;
+                in1 = sp0_last;
+            }
+            auto fix = [&](uint32_t m, uint32_t nam, uint32_t W, uint32_t S, uint32_t C, uint32_t in) -> uint32_t {
+                W = (W | ((in >> 4) & 0xFu)) & 0xFFFFu;
+                S = (S | ((in >> 8) & 0xFu)) & 0xFFFFu;
+                C = (C | (in & 0xFu)) & 0xFFFFu;
+                bad |= C != nam;
+                return ((m & 0xFFFFu & ~nam) | W) | ((((m >> 16) & ~nam) | S) << 16);
+            };
+            m0 = fix(m0, nam0, W0, S0, C0, in0);
+            m1 = fix(m1, nam1, W1, S1, C1, in1);
+            uint32_t mh_l = mh;
+            if (lane == 63) mh_l = fix(mh, namh, Wh, Sh, Ch, sp1);
             mh = lane_u32(mh_l, 63);
             prev_blk = lane_u32(pb_l, 0);
             defer_blk = __any(bad);
@@ -1041,149 +1133,17 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             return;
         }
 
-#if MRG_MAP_BR
-        {
-            // ---- the whole block: window [Ab - 16, Ab + 2048 + 64), staged bytes [Ab, whi)
-            const uint64_t whi = umin64(Ab + (uint64_t)(BLK + HALO), doc_hi);
-            const uint64_t wbase = Ab - (uint64_t)BEHIND;
-            const uint32_t tend = (uint32_t)umin64(doc_hi - Ab, (uint64_t)BLK);  // token starts only before this
-            const uint32_t m1_first = lane_u32(m1, 0), m0_last = lane_u32(m0, 63);
-            wave_sync_lds();  // the previous block's readers are done (program order)
-            reinterpret_cast<uint4 *>(win)[1 + lane] = X.v0;
-            reinterpret_cast<uint4 *>(win)[65 + lane] = X.v1;
-            if (lane >= 1 && lane < 5) reinterpret_cast<uint4 *>(win)[128 + lane] = X.e;  // the halo
-            // masks of this lane's segment and the next one, tile 0 (pairs 0..63) and tile 1 (64..127)
-            uint32_t mn0 = from_next_lane(m0), mn1 = from_next_lane(m1);
-            uint32_t pv0 = from_prev_lane(m0) >> 31, pv1 = from_prev_lane(m1) >> 31;
-            if (lane == 63) {
-                mn0 = m1_first;
-                mn1 = mh;
-            }
-            if (lane == 0) {
-                pv0 = prev_blk;
-                pv1 = m0_last >> 31;
-            }
-            mp[lane] = (uint64_t)((m0 & 0xFFFFu) | (mn0 << 16)) | ((uint64_t)((m0 >> 16) | (mn0 & 0xFFFF0000u)) << 32);
-            mp[64 + lane] = (uint64_t)((m1 & 0xFFFFu) | (mn1 << 16)) | ((uint64_t)((m1 >> 16) | (mn1 & 0xFFFF0000u)) << 32);
-            // token starts (a non-space byte after a space), both tiles' counts in one wave prefix sum
-            const uint32_t S0 = m0 >> 16, S1 = m1 >> 16;
-            uint32_t st0 = ~S0 & ((S0 << 1) | pv0) & 0xFFFFu, st1 = ~S1 & ((S1 << 1) | pv1) & 0xFFFFu;
-            if (l16 >= tend) st0 = 0;
-            if (1024u + l16 >= tend) st1 = 0;
-            const uint32_t c0 = __builtin_popcount(st0), c1 = __builtin_popcount(st1);
-            const uint32_t incl = wave_incl_scan(c0 | (c1 << 16));
-            const uint32_t tot = lane_u32(incl, 63);
-            uint32_t pos0 = (incl & 0xFFFFu) - c0, pos1 = (tot & 0xFFFFu) + (incl >> 16) - c1;
-            if (abl & 64u) {  // timing only: no queue writes, no tokens
-                my_tokens += (st0 ^ st1) & 1u;
-                st0 = st1 = 0;
-            }
-            while (st0) {
-                const uint32_t kb = (uint32_t)__builtin_ctz(st0);
-                st0 &= st0 - 1u;
-                queue[pos0++] = (uint16_t)(l16 + kb);
-            }
-            while (st1) {
-                const uint32_t kb = (uint32_t)__builtin_ctz(st1);
-                st1 &= st1 - 1u;
-                queue[pos1++] = (uint16_t)(1024u + l16 + kb);
-            }
-            const uint32_t total = (abl & 68u) ? 0u : (tot & 0xFFFFu) + (tot >> 16);
-            MRG_PT(2);
-            uint32_t nslow = 0;
-            const bool may_claim =
-                __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
-                (uint32_t)CAP;
-            my_tokens += (abl & 4u) ? c0 + c1 : 0u;
-            wave_sync_lds();
-            // FOUR tokens per lane per round (entries q, q + 64, q + 128, q + 192); the queue, the masks
-            // and the window are read-only now
-            for (uint32_t base = 0; base < total; base += 256) {
-                bool fs[4], sl[4];
-                uint32_t sv[4], gp4[4];
-                uint64_t a0[4], a1[4];
-                uint32_t rq[4];
-#pragma unroll
-                for (int t = 0; t < 4; ++t)
-                    rq[t] = queue[min(base + (uint32_t)lane + 64u * t, (uint32_t)QCAP - 1u)];
-                bool anyg = false;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    gp4[t] = extract(base + (uint32_t)lane + 64u * t, rq[t], total, fs[t], sl[t], sv[t], a0[t], a1[t]);
-                    anyg = anyg || gp4[t] != 0u;
-                }
-                if (__any(anyg)) {
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) squeeze(gp4[t], a0[t], a1[t]);
-                }
-                // slow tokens (past the 2-segment window, or > 16 raw key bytes) are deferred: their
-                // starts go to the consumed front of the queue
-                uint64_t ms[4];
-                bool anys = false;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    ms[t] = __ballot(sl[t]);
-                    anys = anys || ms[t] != 0ull;
-                }
-                if (anys) {
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(ms[t] >> 32),
-                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)ms[t], 0u));
-                        if (sl[t]) queue[nslow + rk] = (uint16_t)sv[t];
-                        nslow += (uint32_t)__builtin_popcountll(ms[t]);
-                    }
-                }
-#pragma unroll
-                for (int t = 0; t < 4; ++t) my_tokens += fs[t] ? 1u : 0u;
-                emit_fastN<4>(A, abl, hbits, table, tails, pool, pool16, fs, a0, a1, docid, may_claim);
-            }
-            // deferred slow tokens: the exact per-codepoint walker, one token per lane (forward
-            // reads only: the staged bytes are [Ab, whi))
-            MRG_PT(3);
-            if (nslow) {
-                wave_sync_lds();
-                auto rd = [&](uint64_t a) -> uint32_t {
-                    if (a >= Ab && a < whi) return (uint32_t)win[a - wbase];
-                    return (uint32_t)gp(A.in)[a];
-                };
-                for (uint32_t base = 0; base < nslow; base += 64) {
-                    const uint32_t q = base + (uint32_t)lane;
-                    bool have = false;
-                    uint64_t tk0 = 0, tk1 = 0, a = 0;
-                    uint32_t tlen = 0, traw = 0;
-                    if (q < nslow) {
-                        a = Ab + queue[q];
-                        uint64_t e2;
-                        if (walk_token(rd, a, doc_hi, A.counters, tk0, tk1, tlen, e2) && tlen > 0) {
-                            have = true;
-                            traw = (uint32_t)(e2 - a);
-                        }
-                    }
-                    my_tokens += have ? 1u : 0u;
-                    emit(A, table, tails, have, tk0, tk1, tlen, a, traw, docid);
-                }
-            }
-        }
-#else
 #pragma unroll
         for (uint32_t j = 0; j < NSUB; ++j) {
             const uint64_t At = Ab + (uint64_t)j * TILE;
             if (At >= doc_hi) break;
             const bool last = j == NSUB - 1;
-            const uint4 x = j == 0 ? X.v0 : X.v1;
-            const uint4 xh = j == 0 ? X.v1 : X.e;  // halo source
             const uint32_t mlut = j == 0 ? m0 : m1;
             const uint32_t mprev = m0;
             const uint64_t t1 = umin64(At + (uint64_t)TILE, doc_hi);
             const uint64_t whi = umin64(t1 + (uint64_t)HALO, doc_hi);
-            const uint64_t wbase = At - (uint64_t)BEHIND;
-
-            // stage the tile and its 64-byte halo (the previous tile's readers are done: program order)
-            wave_sync_lds();
-            reinterpret_cast<uint4 *>(win)[1 + lane] = x;
-            if (!last ? lane < 4 : (lane >= 1 && lane < 5))
-                reinterpret_cast<uint4 *>(win)[65 + (!last ? lane : lane - 1)] = xh;
+            const uint64_t wbase = Ab - (uint64_t)BEHIND;  // the block's window (staged above)
+            const uint32_t tb = j * (uint32_t)TILE;
             // masks: this lane's segment and the next one (lane 63: the first halo segment)
             const uint32_t m = mlut;
             uint32_t mn = from_next_lane(m);
@@ -1231,8 +1191,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 // bounds), so the two chains share every LDS wait
                 const uint32_t qa = base + (uint32_t)lane, qb = qa + 64u;
                 const uint32_t ra = queue[min(qa, (uint32_t)QCAP - 1u)], rb = queue[min(qb, (uint32_t)QCAP - 1u)];
-                uint32_t ga = extract(qa, ra, total, fa, sa, sA, a0, a1);
-                uint32_t gb = extract(qb, rb, total, fb, sb, sB, b0, b1);
+                uint32_t ga = extract(tb, qa, ra, total, fa, sa, sA, a0, a1);
+                uint32_t gb = extract(tb, qb, rb, total, fb, sb, sB, b0, b1);
                 if (__any((ga | gb) != 0u)) {
                     squeeze(ga, a0, a1);
                     squeeze(gb, b0, b1);
@@ -1254,8 +1214,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 const uint64_t kk0[2] = {a0, b0}, kk1[2] = {a1, b1};
                 emit_fastN<2>(A, abl, hbits, table, tails, pool, pool16, hv, kk0, kk1, docid, may_claim);
             }
-            // deferred slow tokens: the exact per-codepoint walker, one token per lane (forward
-            // reads only: the staged bytes are [At, whi))
+            // deferred slow tokens, one per lane: through the tile's masks, or (a token running past
+            // the first halo segment) the exact per-codepoint walker (forward reads only: the staged
+            // bytes are [At, whi))
             MRG_PT(3);
             if (nslow) {
                 wave_sync_lds();
@@ -1269,11 +1230,16 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                     uint64_t tk0 = 0, tk1 = 0, a = 0;
                     uint32_t tlen = 0, traw = 0;
                     if (q < nslow) {
-                        a = At + queue[q];
-                        uint64_t e2;
-                        if (walk_token(rd, a, doc_hi, A.counters, tk0, tk1, tlen, e2) && tlen > 0) {
-                            have = true;
-                            traw = (uint32_t)(e2 - a);
+                        const uint32_t s = queue[q];
+                        a = At + s;
+                        if (!(abl & 128u) && mask_walk(tb, s, 64u, tk0, tk1, tlen, traw)) {
+                            have = tlen > 0;
+                        } else {
+                            uint64_t e2;
+                            if (walk_token(rd, a, doc_hi, A.counters, tk0, tk1, tlen, e2) && tlen > 0) {
+                                have = true;
+                                traw = (uint32_t)(e2 - a);
+                            }
                         }
                     }
                     my_tokens += have ? 1u : 0u;
@@ -1281,7 +1247,6 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 }
             }
         }
-#endif
         MRG_PT(4);
     };
 

@@ -91,7 +91,8 @@ struct MapArgs {
                                  // become tail records), 4 = no per-token work after the queue,
                                  // 8 = every block loads its document's first block (L2-resident),
                                  // 16 = no LDS count add on table hits, 32 = classification
-                                 // only, 64 = no queue writes (and no tokens)
+                                 // only, 64 = no queue writes (and no tokens), 128 = every slow
+                                 // token through the codepoint walker (results exact: an A/B knob)
     unsigned long long *prof;    // perf diagnostics (env MRG_PROF): per-phase wave clocks, [7]; else null
 };
 
