@@ -869,8 +869,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // of every segment of the tile, exact for UTF-8 too (pair k = segments k and k + 1, so the last
     // pair's high halves are the first halo segment), and the window holds its bytes -- the token's
     // end and key need no codepoint decoding: the key is the W bytes before the first S byte.  s = the
-    // token's tile offset, tb the tile's block offset, nseg = the tile's segments.  False when the token runs past the first halo
-    // segment (then the codepoint walker).
+    // token's tile offset, tb the tile's block offset, nseg = the tile's segments.  False when the
+    // token runs past the first halo segment (then the codepoint walker).
     auto mask_walk = [&](uint32_t tb, uint32_t s, uint32_t nseg, uint64_t &tk0, uint64_t &tk1, uint32_t &tlen,
                          uint32_t &traw) -> bool {
         tk0 = 0;
@@ -885,16 +885,34 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const uint32_t S = ((((uint32_t)(mw >> 32) >> sh) & 0xFFFFu) >> i) << i;
             const uint32_t e = S ? (uint32_t)__builtin_ctz(S) : 16u;
             W &= (1u << e) - 1u;
-            if (W && tlen < 16u) {  // key bytes (only the first 16 are packed)
-                const uint32_t o = ((uint32_t)BEHIND + tb) / 4u + 4u * seg;
-                const uint32_t d0 = win32[o], d1 = win32[o + 1], d2 = win32[o + 2], d3 = win32[o + 3];
-                while (W && tlen < 16u) {
-                    const uint32_t b = (uint32_t)__builtin_ctz(W);
-                    W &= W - 1u;
-                    const uint32_t d = (b & 8u) ? ((b & 4u) ? d3 : d2) : ((b & 4u) ? d1 : d0);
-                    mrg_key_append(tk0, tk1, tlen, __builtin_amdgcn_ubfe(d, 8u * (b & 3u), 8));
-                    ++tlen;
+            // key bytes (only the first 16 are packed): each run of W bytes as one selector load (the
+            // fast path's), shifted behind the bytes so far
+            while (W && tlen < 16u) {
+                const uint32_t b = (uint32_t)__builtin_ctz(W);
+                const uint32_t r = (uint32_t)__builtin_ctz(~(W >> b));  // run length (<= 16 - b)
+                W &= ~(((1u << r) - 1u) << b);
+                const uint32_t off = (uint32_t)BEHIND + tb + 16u * seg + b;
+                const uint32_t dw = off >> 2, ra = off & 3u;
+                const uint32_t d0 = win32[dw], d1 = win32[dw + 1], d2 = win32[dw + 2], d3 = win32[dw + 3],
+                               d4 = win32[dw + 4];
+                const u32x4 sl = *reinterpret_cast<const u32x4 *>(s_sel[r * 17u + 16u]);
+                const uint32_t a0 = __builtin_amdgcn_alignbyte(d1, d0, ra), a1 = __builtin_amdgcn_alignbyte(d2, d1, ra),
+                               a2 = __builtin_amdgcn_alignbyte(d3, d2, ra), a3 = __builtin_amdgcn_alignbyte(d4, d3, ra),
+                               a4 = __builtin_amdgcn_alignbyte(0u, d4, ra);
+                const uint64_t v0 = ((uint64_t)__builtin_amdgcn_perm(a1, a0, sl.x) << 32) | __builtin_amdgcn_perm(a2, a1, sl.y);
+                const uint64_t v1 = ((uint64_t)__builtin_amdgcn_perm(a3, a2, sl.z) << 32) | __builtin_amdgcn_perm(a4, a3, sl.w);
+                // (v0:v1) >> 8 * tlen
+                const uint32_t ks = 8u * tlen;
+                if (ks == 0u) {
+                    tk0 |= v0;
+                    tk1 |= v1;
+                } else if (ks < 64u) {
+                    tk0 |= v0 >> ks;
+                    tk1 |= (v1 >> ks) | (v0 << (64u - ks));
+                } else {
+                    tk1 |= v0 >> (ks - 64u);
                 }
+                tlen += r;
             }
             tlen += (uint32_t)__builtin_popcount(W);
             if (S) {
@@ -980,8 +998,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             // for its busiest lane, once per segment kind).  The owners read their leads' lengths and
             // classes back in order; a codepoint's last bytes may lie in the next segment (DPP).  Every
             // non-ASCII byte must be covered by a decoded codepoint, else the block holds invalid UTF-8
-            // and is deferred.  Two chunks (tile 0 with the codepoint holding the byte before the block,
-            // tile 1 with the first halo segment) keep the queue at <= 520 entries.
+            // and is deferred.
             const int64_t dlo = (int64_t)(doc_lo - Ab);  // two's complement (see lo below)
             // the document in block offsets: lo in [-16, 16), hi in (0, 2112].  (A select on
             // doc_lo > Ab lost its first case in the compiled code: keep a clamped signed difference.)
@@ -1055,13 +1072,24 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                     S |= cl == MRG_CLS_S ? span : 0u;
                 }
             };
-            // chunk 0: the codepoint before the block, tile 0
+            // chunk 0: the codepoint before the block, tile 0; chunk 1: tile 1, the first halo segment.
+            // Both in one decode pass when the queue holds them (sparse non-ASCII text), else one after
+            // the other (the queue is reused once chunk 0 is read)
+            const uint32_t n0 = tot & 0xFFFFu, n1 = tot >> 16;
+            const bool split = n0 + n1 > (uint32_t)QCAP;
+            const uint32_t b1 = split ? 0u : n0;  // chunk 1's first slot
+            auto put1 = [&]() {
+                uint32_t k = b1 + e1;
+                for (uint32_t m = ld1; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + 1024u + l16 + __builtin_ctz(m));
+                for (uint32_t m = ldh; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + BLK + __builtin_ctz(m));
+            };
             {
                 uint32_t k = e0;
                 if (hasb) queue[k++] = (uint16_t)(BEHIND + pbp);
                 for (uint32_t m = ld0; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + l16 + __builtin_ctz(m));
             }
-            decode(tot & 0xFFFFu);
+            if (!split) put1();
+            decode(split ? n0 : n0 + n1);
             uint32_t W0, S0, C0, bsp = 0, pb_l = prev_blk;
             if (hasb) {  // its bytes from 0 on spill into tile 0's first segment; byte -1 gives prev_blk
                 const uint32_t r = queue[e0], n = r & 7u, cl = r >> 3;
@@ -1075,17 +1103,14 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 }
             }
             own(ld0, e0 + hasb, W0, S0, C0);
-            // chunk 1: tile 1, the first halo segment (the queue is reused: chunk 0 is read)
-            wave_sync_lds();
-            {
-                uint32_t k = e1;
-                for (uint32_t m = ld1; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + 1024u + l16 + __builtin_ctz(m));
-                for (uint32_t m = ldh; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + BLK + __builtin_ctz(m));
+            if (split) {
+                wave_sync_lds();
+                put1();
+                decode(n1);
             }
-            decode(tot >> 16);
             uint32_t W1, S1, C1, Wh, Sh, Ch;
-            own(ld1, e1, W1, S1, C1);
-            own(ldh, e1 + (uint32_t)__builtin_popcount(ld1), Wh, Sh, Ch);
+            own(ld1, b1 + e1, W1, S1, C1);
+            own(ldh, b1 + e1 + (uint32_t)__builtin_popcount(ld1), Wh, Sh, Ch);
             // spills (C | W << 4 | S << 8 of bits 16..18) into the next segment: lane l+1, tile 1's lane
             // 0 after tile 0's lane 63, the halo segment after tile 1's lane 63 (same lane)
             auto pack = [](uint32_t W, uint32_t S, uint32_t C) { return (C >> 16) | ((W >> 16) << 4) | ((S >> 16) << 8); };

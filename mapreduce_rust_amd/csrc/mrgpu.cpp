@@ -575,8 +575,12 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         c->spec_agg = !idx;
         c->spec_c32 = c32;  // the width this job allowed (not the one a reused launch happened to use)
         c->st.agg_path = 1;
-        {  // the next job's workgroups per bucket: enough sub-ranges for this job's key count
-            const uint64_t per = (uint64_t)MRG_NBUCKET * 4096u;
+        {  // the next job's workgroups per bucket: enough sub-ranges for this job's key count, each
+           // sub-range's table at most 5/6 full.  Each sub-range is one more pass over the bucket's
+           // tail stream: zipf_u (2.9 M keys) aggregates in 6.9 ms at 1 (2 M records overflow to the
+           // HBM table), 3.6 ms at 2 (81 % full, no overflow), 4.2 ms at 3 (profiles/r04/v34_*)
+            const uint64_t slots = idx ? 4096u : (c32 ? 6912u : 6112u);  // k_keys.hip ba_cap
+            const uint64_t per = (uint64_t)MRG_NBUCKET * (slots * 5u / 6u);
             c->agg_nsub = (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, (c->h_cnt[CNT_KEYS] + per - 1) / per));
         }
         break;
