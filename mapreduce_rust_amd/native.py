@@ -14,7 +14,7 @@ APP_INDEXER = 1
 FLAG_NO_COMPAT_DROP_LAST = 0x1
 FLAG_FINAL_TXT = 0x2
 XREC_BYTES = 24  # include/mrgpu.h MRG_XREC_BYTES (ABI 3)
-ABI_VERSION = 3
+ABI_VERSION = 4  # include/mrgpu.h MRG_ABI_VERSION
 
 OK, EINVAL, EUTF8, EHIP, ENOMEM, EIO, ECOMM = 0, -1, -2, -3, -4, -5, -6
 _CODES = {EINVAL: "EINVAL", EUTF8: "EUTF8", EHIP: "EHIP", ENOMEM: "ENOMEM", EIO: "EIO", ECOMM: "ECOMM"}

@@ -50,7 +50,7 @@ def test_record_layout_constant():
     src = open(os.path.join(ROOT, "include", "mrgpu.h")).read()
     assert "#define MRG_XREC_BYTES 24" in src and "#define MRG_ABI_VERSION 4" in src
     from mapreduce_rust_amd import native, shuffle
-    assert native.XREC_BYTES == shuffle.XREC == 24 and native.ABI_VERSION == 3
+    assert native.XREC_BYTES == shuffle.XREC == 24 and native.ABI_VERSION == 4
     assert b"abi 4" in native.load().mrg_version()
     rs = open(os.path.join(ROOT, "mrgpu-sys", "src", "lib.rs")).read()
     assert "pub const MRG_XREC_BYTES: usize = 24;" in rs and "pub const MRG_ABI_VERSION: u32 = 4;" in rs
