@@ -41,8 +41,8 @@ namespace {
 
 // Block rounds (r04, MRG_MAP_BR=1 in commit 5e363df, since removed): both tiles of a block tokenized
 // by rounds of four tokens per lane with 12 waves per workgroup -- slower (157 VGPRs, 3 waves per
-// SIMD).  The block's bytes are staged together (one window of the 2 KiB
-// block, the 16 bytes before it and the halo), then its tiles are tokenized one by one.
+// SIMD).  Tiles are staged one at a time (a whole-block window needs the 16
+// KiB that 16-byte table slots freed, and those slots cost ASCII text 3.5 %: section 11.1).
 constexpr int NW = MRG_MAP_WAVES;
 constexpr int WG = 64 * NW;
 constexpr int SEG = MRG_MAP_SEG;
@@ -52,7 +52,7 @@ constexpr int BEHIND = MRG_MAP_BEHIND;
 constexpr int NSUB = MRG_MAP_NSUB;               // 1 KiB tiles per block
 constexpr int BLK = NSUB * TILE;                 // bytes per wave iteration
 // staged window + slack for the 5-dword key reads (a key starts within 31 bytes of a token start)
-constexpr int WIN = BEHIND + BLK + HALO + 48;
+constexpr int WIN = BEHIND + TILE + HALO + 48;
 constexpr int QCAP = TILE / 2 + 16;  // a start needs a space before it; <= 520 codepoint leads
 constexpr int NMP = 64;         // mask pairs per wave (one per segment of the tile)
 static_assert(TILE == 64 * SEG, "one segment per lane");
@@ -213,26 +213,12 @@ struct alignas(16) KeyPair {
     uint64_t a, b;
 };
 
-// A combine-table slot (r04): a key of at most 12 bytes -- k0 and the high word of k1 (its low word
-// is 0 for such keys) -- and its count: 16 bytes, one ds_read_b128 per way, 64 KiB for 4096 slots
-// (was 16-byte keys + a count array, 80 KiB).  Keys of 13..16 bytes never enter the table (the
-// 16-byte tail regions take them).
-#define MRG_EMPTY_HI 0xFFFFFFFFu  // high word of k1 while a claim is in progress (0xFF bytes: never UTF-8)
-struct alignas(16) Slot {
-    uint64_t a;    // k0 (MRG_EMPTY_K0: empty)
-    uint32_t b;    // high word of k1
-    uint32_t cnt;
-};
-__device__ __forceinline__ bool slot_eq(const Slot &k, uint64_t a, uint64_t b) {
-    return ((k.a ^ a) | (uint64_t)(k.b ^ (uint32_t)(b >> 32)) | (b & 0xFFFFFFFFull)) == 0ull;
-}
-
 // Workgroup LDS combine table: 2-way sets -- slots s and s + NS of set s = low
 // hash bits (way-major: way 0 of the 2048 sets, then way 1, so a wave's 16-byte reads of one way
 // spread over all 64 banks instead of half of them; A/B -0.5 % map).  A probe reads both keys at
 // once (one LDS round trip: no tag step) and adds 1 to the
 // matching slot's count.  A new key claims an empty way by a 64-bit CAS on k0 (EMPTY -> k0), then
-// writes k1's high word (and doc) and adds its first count; slots only ever go EMPTY -> (k0, EMPTY) -> (k0, k1),
+// writes k1 (and doc) and adds its first count; slots only ever go EMPTY -> (k0, EMPTY) -> (k0, k1),
 // so a slot read equal to the full key is that key's slot for good.  A reader that sees a half
 // written slot, or a claimer that loses its CAS to the same k0, just misses -- harmless: misses go
 // to the tail and every slot is flushed and summed exactly; at worst a key occupies both ways.
@@ -259,8 +245,8 @@ struct LdsTable {
     static constexpr uint32_t NS = CAP / 2;
     // the indexer's table has a doc word per slot: its bitmap stays at 32 Kibit to fit the LDS
     static constexpr uint32_t DW = (IDX && MRG_MAP_DOOR_WORDS > 1024) ? 1024u : (uint32_t)MRG_MAP_DOOR_WORDS;
-    Slot *slot;
-    unsigned int *doc;
+    KeyPair *key;
+    unsigned int *cnt, *doc;
     unsigned int *door;
     unsigned int *fill;  // slots claimed so far (never decreases: a claimed slot keeps its key)
 
@@ -285,6 +271,10 @@ struct LdsTable {
         return (atomicOr(w, hi) & hi) != 0u;
     }
 
+    __device__ __forceinline__ bool matches(uint32_t s, uint64_t a, uint64_t b, uint32_t d) const {
+        const KeyPair k = key[s];  // one 16-byte LDS read
+        return ((k.a ^ a) | (k.b ^ b)) == 0 && (!IDX || doc[s] == d);
+    }
 
     // claim an empty way of set s0 (ways seen empty: e0, e1); true if the key got a slot and its count
     __device__ __forceinline__ bool claim(uint32_t s0, bool e0, bool e1, uint64_t a, uint64_t b, uint32_t d,
@@ -293,11 +283,11 @@ struct LdsTable {
         for (uint32_t w = 0; w < 2; ++w) {
             if (!(w ? e1 : e0)) continue;
             const uint32_t s = s0 + w * NS;  // way w of set s0: way-major layout
-            const unsigned long long old = atomicCAS(&slot[s].a, (unsigned long long)MRG_EMPTY_K0, (unsigned long long)a);
+            const unsigned long long old = atomicCAS(&key[s].a, (unsigned long long)MRG_EMPTY_K0, (unsigned long long)a);
             if (old == MRG_EMPTY_K0) {
-                slot[s].b = (uint32_t)(b >> 32);
+                key[s].b = b;
                 if (IDX) doc[s] = d;
-                atomicAdd(&slot[s].cnt, 1u);
+                atomicAdd(&cnt[s], 1u);
                 atomicAdd(fill, 1u);
                 return true;
             }
@@ -306,16 +296,15 @@ struct LdsTable {
         return false;
     }
 
-    // one probe per lane (slow path: one token per lane); keys of more than 12 bytes always miss
+    // one probe per lane (slow path: one token per lane)
     __device__ __forceinline__ bool insert_wave(bool act, uint64_t a, uint64_t b, uint32_t d, uint32_t h,
                                                 uint32_t abl = 0) {
-        act = act && (uint32_t)b == 0u;
         const uint32_t s0 = act ? (h & (NS - 1)) : 0u;
-        const Slot k0 = slot[s0], k1 = slot[s0 + NS];
-        const bool m0 = act & slot_eq(k0, a, b) & (!IDX || doc[s0] == d);
-        const bool m1 = act & !m0 & slot_eq(k1, a, b) & (!IDX || doc[s0 + NS] == d);
+        const KeyPair k0 = key[s0], k1 = key[s0 + NS];
+        const bool m0 = act & (((k0.a ^ a) | (k0.b ^ b)) == 0) & (!IDX || doc[s0] == d);
+        const bool m1 = act & !m0 & (((k1.a ^ a) | (k1.b ^ b)) == 0) & (!IDX || doc[s0 + NS] == d);
         bool hit = m0 | m1;
-        if (hit && !(abl & 16u)) atomicAdd(&slot[m0 ? s0 : s0 + NS].cnt, 1u);
+        if (hit && !(abl & 16u)) atomicAdd(&cnt[m0 ? s0 : s0 + NS], 1u);
         const bool e0 = k0.a == MRG_EMPTY_K0, e1 = k1.a == MRG_EMPTY_K0;
         const bool need = act && !hit && (e0 || e1);
         if (__any(need)) {
@@ -399,13 +388,12 @@ __device__ __forceinline__ void emit_fastN(const MapArgs &A, uint32_t abl, uint3
     const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
     uint32_t h[N], s[N], b[N];
     bool act[N], w16[N], hit[N], m0[N];
-    Slot kw0[N], kw1[N];
+    KeyPair kw0[N], kw1[N];
     uint64_t end[N];
 #pragma unroll
     for (int t = 0; t < N; ++t) {
         h[t] = key_hash(k0[t], k1[t], dkey, hbits);
-        // keys of more than 12 bytes (k1 low word non-zero) have no table slot: straight to the tail
-        act[t] = has[t] && !(abl & 2u) && (uint32_t)k1[t] == 0u;
+        act[t] = has[t] && !(abl & 2u);
         s[t] = act[t] ? (h[t] & (NS - 1)) : 0u;
         b[t] = bucket_of(h[t]);
         w16[t] = !IDX && (uint32_t)k1[t] != 0u;  // wc keys of 13..16 bytes: the 16-byte regions
@@ -413,20 +401,21 @@ __device__ __forceinline__ void emit_fastN(const MapArgs &A, uint32_t abl, uint3
     // both ways of every set: 2N 16-byte reads in flight together, with the region ends
 #pragma unroll
     for (int t = 0; t < N; ++t) {
-        kw0[t] = T.slot[s[t]];
-        kw1[t] = T.slot[s[t] + NS];
+        kw0[t] = T.key[s[t]];
+        kw1[t] = T.key[s[t] + NS];
         end[t] = (w16[t] ? R.end16 : R.end)[b[t]];
     }
 #pragma unroll
     for (int t = 0; t < N; ++t) {
-        m0[t] = act[t] & slot_eq(kw0[t], k0[t], k1[t]) & (!IDX || T.doc[s[t]] == dkey);
-        const bool m1 = act[t] & !m0[t] & slot_eq(kw1[t], k0[t], k1[t]) & (!IDX || T.doc[s[t] + NS] == dkey);
+        m0[t] = act[t] & (((kw0[t].a ^ k0[t]) | (kw0[t].b ^ k1[t])) == 0) & (!IDX || T.doc[s[t]] == dkey);
+        const bool m1 = act[t] & !m0[t] & (((kw1[t].a ^ k0[t]) | (kw1[t].b ^ k1[t])) == 0) &
+                        (!IDX || T.doc[s[t] + NS] == dkey);
         hit[t] = m0[t] | m1;
     }
     if (!(abl & 16u)) {
 #pragma unroll
         for (int t = 0; t < N; ++t)
-            if (hit[t]) atomicAdd(&T.slot[m0[t] ? s[t] : s[t] + NS].cnt, 1u);
+            if (hit[t]) atomicAdd(&T.cnt[m0[t] ? s[t] : s[t] + NS], 1u);
     }
     // empty ways exist only until the table has filled (wave-uniform: a stale count only means
     // an unneeded test)
@@ -637,7 +626,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // v_perm selectors per (key length, 1-byte gap position; 16 = none) over the r-aligned window
     __shared__ __attribute__((aligned(16))) uint32_t s_sel[17 * 17][4];
     // workgroup: combine table + tail-region cursors
-    __shared__ Slot s_slot[CAP];
+    __shared__ KeyPair s_key[CAP];
+    __shared__ unsigned int s_cnt[CAP];
     __shared__ __attribute__((aligned(16))) unsigned int s_doc[IDX ? CAP : 1];
     __shared__ unsigned long long s_tcur[MRG_NBUCKET];  // next pool record of (bucket, this WG)
     __shared__ unsigned long long s_tend[MRG_NBUCKET];  // end of that region
@@ -660,7 +650,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // index, document bounds) is wave-uniform and keeps it in SGPRs
     const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int i = tid; i < CAP; i += WG) {
-        s_slot[i] = Slot{MRG_EMPTY_K0, MRG_EMPTY_HI, 0u};
+        s_key[i] = KeyPair{MRG_EMPTY_K0, MRG_EMPTY_K1};
+        s_cnt[i] = 0;
         if (IDX) s_doc[i] = MRG_EMPTY_DOC;
     }
     if (MRG_MAP_DOOR)
@@ -707,7 +698,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const uint32_t zm = zmask(L, j), gm = zmask(g, j);
         s_sel[L * 17u + g][j] = ((0x00010203u + (gm & 0x01010101u)) & ~zm) | (0x0C0C0C0Cu & zm);
     }
-    LdsTable<CAP, IDX> table{s_slot, s_doc, s_door, &s_fill};
+    LdsTable<CAP, IDX> table{s_key, s_cnt, s_doc, s_door, &s_fill};
     const TailRegions tails{s_tcur, s_tend, s_tcur16, s_tend16};
     uint32_t my_tokens = 0;
     // uniform job parameters used in the hot loop, read once
@@ -799,7 +790,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // length, \w span and deleted bytes come from one 8-byte mask-pair read, its key bytes from the
     // window.  fast: a key of <= 16 bytes ending inside the 2-segment window; slow: the rest (the
     // exact walker).  Returns the deleted-byte runs still to squeeze out (more than one).
-    auto extract = [&](uint32_t tb, uint32_t q, uint32_t sraw, uint32_t total, bool &fast, bool &slow, uint32_t &s,
+    auto extract = [&](uint32_t q, uint32_t sraw, uint32_t total, bool &fast, bool &slow, uint32_t &s,
                        uint64_t &tk0, uint64_t &tk1) -> uint32_t {
         const bool act = q < total;
         s = act ? sraw : 0u;
@@ -829,7 +820,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         // the 17 window bytes from the key's first byte as five dwords: one unaligned 16-byte
         // LDS read and one 4-byte read (gfx950 runs in unaligned access mode: no dword
         // alignment, no v_alignbyte), then one selector word per output word
-        const uint32_t off = (uint32_t)BEHIND + tb + s + first;  // tb = the tile's block offset
+        const uint32_t off = (uint32_t)BEHIND + s + first;
         const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
         const uint32_t dw = off >> 2, r = off & 3u;
         const uint32_t d0 = win32[dw], d1 = win32[dw + 1], d2 = win32[dw + 2], d3 = win32[dw + 3],
@@ -869,9 +860,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // of every segment of the tile, exact for UTF-8 too (pair k = segments k and k + 1, so the last
     // pair's high halves are the first halo segment), and the window holds its bytes -- the token's
     // end and key need no codepoint decoding: the key is the W bytes before the first S byte.  s = the
-    // token's tile offset, tb the tile's block offset, nseg = the tile's segments.  False when the
-    // token runs past the first halo segment (then the codepoint walker).
-    auto mask_walk = [&](uint32_t tb, uint32_t s, uint32_t nseg, uint64_t &tk0, uint64_t &tk1, uint32_t &tlen,
+    // token's tile offset, nseg = the tile's segments.  False when the token runs past the first halo
+    // segment (then the codepoint walker).
+    auto mask_walk = [&](uint32_t s, uint32_t nseg, uint64_t &tk0, uint64_t &tk1, uint32_t &tlen,
                          uint32_t &traw) -> bool {
         tk0 = 0;
         tk1 = 0;
@@ -891,7 +882,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 const uint32_t b = (uint32_t)__builtin_ctz(W);
                 const uint32_t r = (uint32_t)__builtin_ctz(~(W >> b));  // run length (<= 16 - b)
                 W &= ~(((1u << r) - 1u) << b);
-                const uint32_t off = (uint32_t)BEHIND + tb + 16u * seg + b;
+                const uint32_t off = (uint32_t)BEHIND + 16u * seg + b;
                 const uint32_t dw = off >> 2, ra = off & 3u;
                 const uint32_t d0 = win32[dw], d1 = win32[dw + 1], d2 = win32[dw + 2], d3 = win32[dw + 3],
                                d4 = win32[dw + 4];
@@ -980,12 +971,6 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         // after which both tiles are tokenized exactly like ASCII tiles -- every byte of a codepoint
         // carries its class, so the W / S masks mean the same.  Invalid UTF-8 defers the block's tiles
         // to generic_tile after the main loop (which reports the first bad byte).
-        // stage the block: the 16 bytes before it, both tiles, the 64-byte halo (the previous block's
-        // readers are done: program order)
-        wave_sync_lds();
-        reinterpret_cast<uint4 *>(win)[1 + lane] = X.v0;
-        reinterpret_cast<uint4 *>(win)[65 + lane] = X.v1;
-        if (lane < 5) reinterpret_cast<uint4 *>(win)[lane == 0 ? 0 : 128 + lane] = X.e;
         bool defer_blk = false;
         if (__any(n0 || n1 || (lane <= 1 && ne))) {
 #ifdef MRG_MAP_NO_UNI
@@ -1042,8 +1027,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const uint32_t incl = wave_incl_scan(c0 | (c1 << 16));
             const uint32_t tot = lane_u32(incl, 63);
             const uint32_t e0 = (incl & 0xFFFFu) - c0, e1 = (incl >> 16) - c1;  // first slots
-            // decode queue entries [0, n): block offset + 16 in, length | class << 3 out (0: invalid)
-            auto decode = [&](uint32_t n) {
+            // decode queue entries [0, n): window index in (the chunk's tile staged at block offset cb),
+            // length | class << 3 out (0: invalid)
+            auto decode = [&](uint32_t n, int cb) {
                 wave_sync_lds();
                 const uint32_t *w32 = reinterpret_cast<const uint32_t *>(win);
                 for (uint32_t base = 0; base < n; base += 64) {
@@ -1053,7 +1039,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                         const uint32_t v = __builtin_amdgcn_alignbyte(w32[(e >> 2) + 1u], w32[e >> 2], e & 3u);
                         auto rd = [&](uint64_t a) -> uint32_t { return (v >> (8u * (uint32_t)a)) & 0xFFu; };
                         uint32_t cp = 0, raw;
-                        const int ln = mrg_utf8_decode(rd, 0ull, (uint64_t)min(hi - ((int)e - BEHIND), 4), &cp, &raw);
+                        const int ln = mrg_utf8_decode(rd, 0ull, (uint64_t)min(hi - (cb + (int)e - BEHIND), 4), &cp, &raw);
                         queue[j] = (uint16_t)(ln > 0 ? (uint32_t)ln | (uni_class(uc, cp) << 3) : 0u);
                     }
                 }
@@ -1072,24 +1058,30 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                     S |= cl == MRG_CLS_S ? span : 0u;
                 }
             };
-            // chunk 0: the codepoint before the block, tile 0; chunk 1: tile 1, the first halo segment.
-            // Both in one decode pass when the queue holds them (sparse non-ASCII text), else one after
-            // the other (the queue is reused once chunk 0 is read)
-            const uint32_t n0 = tot & 0xFFFFu, n1 = tot >> 16;
-            const bool split = n0 + n1 > (uint32_t)QCAP;
-            const uint32_t b1 = split ? 0u : n0;  // chunk 1's first slot
-            auto put1 = [&]() {
-                uint32_t k = b1 + e1;
-                for (uint32_t m = ld1; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + 1024u + l16 + __builtin_ctz(m));
-                for (uint32_t m = ldh; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + BLK + __builtin_ctz(m));
-            };
+            // chunk 1 (tile 1, the first halo segment), then chunk 0 (the codepoint holding the byte
+            // before the block, tile 0), each decoded from its tile's window; tile 0 stays staged
+            uint32_t W1, S1, C1, Wh, Sh, Ch;
+            wave_sync_lds();
+            reinterpret_cast<uint4 *>(win)[1 + lane] = X.v1;
+            if (lane >= 1 && lane < 5) reinterpret_cast<uint4 *>(win)[64 + lane] = X.e;  // the halo
+            {
+                uint32_t k = e1;
+                for (uint32_t m = ld1; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + l16 + __builtin_ctz(m));
+                for (uint32_t m = ldh; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + TILE + __builtin_ctz(m));
+            }
+            decode(tot >> 16, TILE);
+            own(ld1, e1, W1, S1, C1);
+            own(ldh, e1 + (uint32_t)__builtin_popcount(ld1), Wh, Sh, Ch);
+            wave_sync_lds();
+            reinterpret_cast<uint4 *>(win)[1 + lane] = X.v0;
+            if (lane < 4) reinterpret_cast<uint4 *>(win)[65 + lane] = X.v1;
+            if (lane == 0) reinterpret_cast<uint4 *>(win)[0] = X.e;  // the 16 bytes before the block
             {
                 uint32_t k = e0;
                 if (hasb) queue[k++] = (uint16_t)(BEHIND + pbp);
                 for (uint32_t m = ld0; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + l16 + __builtin_ctz(m));
             }
-            if (!split) put1();
-            decode(split ? n0 : n0 + n1);
+            decode(tot & 0xFFFFu, 0);
             uint32_t W0, S0, C0, bsp = 0, pb_l = prev_blk;
             if (hasb) {  // its bytes from 0 on spill into tile 0's first segment; byte -1 gives prev_blk
                 const uint32_t r = queue[e0], n = r & 7u, cl = r >> 3;
@@ -1103,14 +1095,6 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 }
             }
             own(ld0, e0 + hasb, W0, S0, C0);
-            if (split) {
-                wave_sync_lds();
-                put1();
-                decode(n1);
-            }
-            uint32_t W1, S1, C1, Wh, Sh, Ch;
-            own(ld1, b1 + e1, W1, S1, C1);
-            own(ldh, b1 + e1 + (uint32_t)__builtin_popcount(ld1), Wh, Sh, Ch);
             // spills (C | W << 4 | S << 8 of bits 16..18) into the next segment: lane l+1, tile 1's lane
             // 0 after tile 0's lane 63, the halo segment after tile 1's lane 63 (same lane)
             auto pack = [](uint32_t W, uint32_t S, uint32_t C) { return (C >> 16) | ((W >> 16) << 4) | ((S >> 16) << 8); };
@@ -1167,8 +1151,12 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const uint32_t mprev = m0;
             const uint64_t t1 = umin64(At + (uint64_t)TILE, doc_hi);
             const uint64_t whi = umin64(t1 + (uint64_t)HALO, doc_hi);
-            const uint64_t wbase = Ab - (uint64_t)BEHIND;  // the block's window (staged above)
-            const uint32_t tb = j * (uint32_t)TILE;
+            const uint64_t wbase = At - (uint64_t)BEHIND;
+            // stage the tile and its 64-byte halo (the previous tile's readers are done: program order)
+            wave_sync_lds();
+            reinterpret_cast<uint4 *>(win)[1 + lane] = j == 0 ? X.v0 : X.v1;
+            if (j == 0 ? lane < 4 : (lane >= 1 && lane < 5))
+                reinterpret_cast<uint4 *>(win)[65 + (j == 0 ? lane : lane - 1)] = j == 0 ? X.v1 : X.e;
             // masks: this lane's segment and the next one (lane 63: the first halo segment)
             const uint32_t m = mlut;
             uint32_t mn = from_next_lane(m);
@@ -1216,8 +1204,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 // bounds), so the two chains share every LDS wait
                 const uint32_t qa = base + (uint32_t)lane, qb = qa + 64u;
                 const uint32_t ra = queue[min(qa, (uint32_t)QCAP - 1u)], rb = queue[min(qb, (uint32_t)QCAP - 1u)];
-                uint32_t ga = extract(tb, qa, ra, total, fa, sa, sA, a0, a1);
-                uint32_t gb = extract(tb, qb, rb, total, fb, sb, sB, b0, b1);
+                uint32_t ga = extract(qa, ra, total, fa, sa, sA, a0, a1);
+                uint32_t gb = extract(qb, rb, total, fb, sb, sB, b0, b1);
                 if (__any((ga | gb) != 0u)) {
                     squeeze(ga, a0, a1);
                     squeeze(gb, b0, b1);
@@ -1257,7 +1245,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                     if (q < nslow) {
                         const uint32_t s = queue[q];
                         a = At + s;
-                        if (!(abl & 128u) && mask_walk(tb, s, 64u, tk0, tk1, tlen, traw)) {
+                        if (!(abl & 128u) && mask_walk(s, 64u, tk0, tk1, tlen, traw)) {
                             have = tlen > 0;
                         } else {
                             uint64_t e2;
@@ -1359,9 +1347,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     for (int b = tid; b <= MRG_NBUCKET; b += WG) s_hist[b] = 0;
     __syncthreads();
     for (int i = tid; i < CAP; i += WG) {
-        const Slot k = s_slot[i];
+        const KeyPair k = s_key[i];
         if (k.a == MRG_EMPTY_K0) continue;
-        const uint32_t b = bucket_of(key_hash(k.a, (uint64_t)k.b << 32, IDX ? s_doc[i] : MRG_EMPTY_DOC, A.hash_bits));
+        const uint32_t b = bucket_of(key_hash(k.a, k.b, IDX ? s_doc[i] : MRG_EMPTY_DOC, A.hash_bits));
         s_rank[i] = (uint16_t)atomicAdd(&s_hist[b], 1u);
     }
     __syncthreads();
@@ -1380,15 +1368,14 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     for (int b = tid; b <= MRG_NBUCKET; b += WG) foff[b] = s_hist[b];
     const uint64_t reg = (uint64_t)blockIdx.x * CAP;
     for (int i = tid; i < CAP; i += WG) {
-        const Slot k = s_slot[i];
+        const KeyPair k = s_key[i];
         if (k.a == MRG_EMPTY_K0) continue;
         const uint32_t d = IDX ? s_doc[i] : MRG_EMPTY_DOC;
-        const uint64_t k1 = (uint64_t)k.b << 32;
-        const uint32_t b = bucket_of(key_hash(k.a, k1, d, A.hash_bits));
+        const uint32_t b = bucket_of(key_hash(k.a, k.b, d, A.hash_bits));
         const uint64_t pos2 = reg + s_hist[b] + s_rank[i];
         gp(A.fk0)[pos2] = k.a;
-        gp(A.fk1)[pos2] = k1;
-        gp(A.fcnt)[pos2] = k.cnt;
+        gp(A.fk1)[pos2] = k.b;
+        gp(A.fcnt)[pos2] = s_cnt[i];
         if (IDX) gp(A.fdoc)[pos2] = d;
     }
     // token and tail totals: waves -> LDS -> one device atomic per workgroup and counter (a wave
