@@ -22,7 +22,10 @@ D2H of the output is measured after the timed loop and reported beside `value`).
 `value` = input bytes of all ranks per step / the MEDIAN step time (each step's time is the max over
 ranks); `ms_per_step` is that median; the mean over the bracketed K steps is reported as well.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 via torch.distributed.run.
+Launch: python bench.py [--gpus N --steps K --warmup W].  N > 1: under torch.distributed.run (one rank
+per GPU), or without a launcher, when bench.py starts the N ranks itself before touching the GPU; it
+exits non-zero if fewer than N GPUs are visible, and the line carries `rccl_nranks` (ncclCommCount of
+the library's communicator) beside `n_gpus`.
 """
 import argparse
 import gzip
@@ -372,13 +375,55 @@ def c2_latency(ctx, dev):
     return res
 
 
+def launch_plan(gpus, backend, env, n_devices):
+    """How this process runs `--gpus N` (decided before anything touches the GPU):
+    "single" -- N = 1, no launcher: this process is the only rank;
+    "spawn"  -- N > 1, no launcher (WORLD_SIZE unset): start N rank processes through
+                torch.distributed.run on this node and exit with their status;
+    "rank"   -- started by a launcher as one of WORLD_SIZE ranks.
+    Raises SystemExit when N does not match the launcher's WORLD_SIZE, or when the RCCL path would
+    put two ranks on one GPU (fewer visible devices than ranks on the node): a multi-GPU bench never
+    falls back to measuring fewer GPUs than it reports."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    if gpus < 1:
+        raise SystemExit(f"--gpus {gpus}: need at least 1")
+    if world > 1 or ("WORLD_SIZE" in env and gpus > 1):
+        if gpus != world:
+            raise SystemExit(f"--gpus {gpus} but WORLD_SIZE {world}")
+        local_world = int(env.get("LOCAL_WORLD_SIZE", str(world)))
+        if backend == "nccl" and n_devices < local_world:
+            raise SystemExit(f"{local_world} ranks on this node but only {n_devices} GPU(s) visible: "
+                             "the RCCL path needs one GPU per rank")
+        return "rank"
+    if gpus == 1:
+        return "single"
+    if backend == "nccl" and n_devices < gpus:
+        raise SystemExit(f"--gpus {gpus} but only {n_devices} GPU(s) visible")
+    return "spawn"
+
+
+def spawn_ranks(gpus, argv):
+    """N rank processes on this node (torch.distributed.run, rendezvous on 127.0.0.1), started from a
+    parent that has not touched the GPU; returns their exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    log(f"--gpus {gpus} without a launcher: starting {gpus} ranks ({' '.join(cmd[1:6])} ...)")
+    return subprocess.call(cmd)
+
+
 def main():
     a = parse()
+    plan = launch_plan(a.gpus, a.backend, os.environ, torch.cuda.device_count())
+    if plan == "spawn":
+        raise SystemExit(spawn_ranks(a.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
     if a.quick:
         a.no_e2e = a.no_cpu_baseline = a.no_zipf_u = a.no_c5 = a.no_c2 = True
     gpu = local % max(1, torch.cuda.device_count())  # = local on a node with one GPU per rank
@@ -474,11 +519,18 @@ def main():
         wl = ("C4: wc, Zipf(%.2f) %s text sharded over %d GPUs, %s shuffle"
               % (a.zipf_s, "ASCII" if a.workload == "zipf" else "Gutenberg-like Unicode", world,
                  "RCCL" if a.backend == "nccl" else "gloo (host-staged rehearsal)"))
+    # ranks of the library's RCCL communicator as RCCL counts them (ncclCommCount): at N > 1 it must
+    # equal n_gpus; null when no communicator exists (N = 1, or the gloo rehearsal)
+    rccl_nranks = comm.count() if comm is not None else None
+    if world > 1 and a.backend == "nccl" and rccl_nranks != world:
+        raise SystemExit(f"RCCL communicator has {rccl_nranks} ranks, WORLD_SIZE is {world}")
     line = {
         "metric": "word-count input GB/s (whole node) at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 3),
         "unit": "GB/s",
         "n_gpus": world,
+        "rccl_nranks": rccl_nranks,
+        "devices_visible": torch.cuda.device_count(),
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(m * 1e3, 3),

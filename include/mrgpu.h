@@ -93,8 +93,8 @@ typedef struct {
     uint64_t map_spill;        /* map records that overflowed their tail region into a bucket's shared
                                   overflow list (last map launch) */
     uint64_t nonascii_tiles;   /* 1 KiB tiles that took the non-ASCII tokenizer (last map launch) */
-    uint64_t tail_records_16;  /* map records stored as 16-byte tail records (keys of 13..16 bytes; the
-                                  others are 12-byte records) */
+    uint64_t tail_records_16;  /* wc: map records stored as 16-byte tail records (keys of 13..16 bytes; the
+                                  others are 12-byte records); 0 for the indexer (all 24-byte records) */
     uint32_t spec_agg;         /* the aggregation queued behind the map: 0 none, 1 used, 2 dropped */
     uint32_t agg_path;         /* aggregation taken: 0 none, 1 bucket tables, 2 wide (sort-based) */
 } mrg_stats;
@@ -173,6 +173,13 @@ int mrg_comm_destroy(mrg_comm *comm);
  * owns (the others come out empty).  Every rank must reach this call: a rank whose map failed must
  * still tell the others (the host's concern; mrg_run_job does it). */
 int mrg_job_shuffle(mrg_ctx *ctx, mrg_comm *comm);
+/* Ranks of the communicator as RCCL counts them (ncclCommCount): the bench reports it beside n_gpus. */
+int mrg_comm_count(const mrg_comm *comm, int *n_ranks);
+
+/* ---- diagnostics ---- */
+/* The context's device buffer pool: blocks handed out and not yet returned (between calls this is
+ * the job state the context keeps), and all bytes it holds (handed out + cached).  Either may be NULL. */
+int mrg_pool_stats(mrg_ctx *ctx, uint64_t *outstanding, uint64_t *held_bytes);
 
 /* ---- plugin-surface equivalents, host buffers (one map task / one reduce task) ---- */
 

@@ -25,8 +25,10 @@
 //      table gives the big-endian packed key (k0, k1); further interior deletions are squeezed out
 //      by 128-bit shifts; tokens that run past the 2-segment window or the staged halo are deferred
 //      to the exact per-codepoint walker.
-// Non-ASCII tiles are listed by the main loop and walked afterwards by all 16 waves (UTF-8 decode +
-// two-level class table per lane).
+// Blocks with a non-ASCII byte take the same path with UTF-8-exact byte classes (codepoint leads
+// compacted into the wave's queue and decoded one per lane, see the block step); only blocks holding
+// invalid UTF-8 are listed by the main loop and walked afterwards by all 16 waves with the exact
+// per-codepoint walker, which reports the first bad byte.
 // Keys of <= 16 bytes go to the workgroup's LDS hash table (exact: the packed key IS the identity):
 // 4096 slots in 2-way sets, claimed only on a key's second sighting (a two-position Bloom
 // doorkeeper).  A miss is appended to one of 256 hash buckets in HBM, into the region this workgroup
@@ -1027,6 +1029,13 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const uint32_t incl = wave_incl_scan(c0 | (c1 << 16));
             const uint32_t tot = lane_u32(incl, 63);
             const uint32_t e0 = (incl & 0xFFFFu) - c0, e1 = (incl >> 16) - c1;  // first slots
+            // Valid UTF-8 has at most 520 leads per chunk (every lead is followed by a continuation
+            // byte), so the queue holds them; more leads (binary data: 1 KiB of 0xFF or 0xC3 0xC3 ...)
+            // can only be invalid -- the block is deferred to the exact walker, which reports the
+            // first bad byte, without writing past the wave's queue (tot is wave-uniform)
+            if ((tot & 0xFFFFu) > (uint32_t)QCAP || (tot >> 16) > (uint32_t)QCAP) {
+                defer_blk = true;
+            } else {
             // decode queue entries [0, n): window index in (the chunk's tile staged at block offset cb),
             // length | class << 3 out (0: invalid)
             auto decode = [&](uint32_t n, int cb) {
@@ -1120,6 +1129,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             prev_blk = lane_u32(pb_l, 0);
             defer_blk = __any(bad);
             if (!defer_blk && lane == 0) atomicAdd(&s_nuni, Ab + (uint64_t)TILE < doc_hi ? 2u : 1u);
+            }
 #endif
         }
         MRG_PT(1);

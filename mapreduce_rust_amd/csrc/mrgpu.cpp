@@ -139,6 +139,13 @@ class Pool : public DevPool {
         }
         free_.clear();
     }
+    // blocks handed out and not returned; bytes held by the pool (handed out or cached)
+    uint64_t outstanding() const { return size_.size() - free_.size(); }
+    uint64_t held_bytes() const {
+        uint64_t b = 0;
+        for (auto &kv : size_) b += kv.second;
+        return b;
+    }
     ~Pool() override {
         (void)hipDeviceSynchronize();
         for (auto &kv : size_) (void)hipFree(kv.first);
@@ -1168,7 +1175,7 @@ void job_map(mrg_ctx *c) {
     c->st.long_tokens = c->h_cnt[CNT_LONG];
     c->st.map_records = c->h_cnt[CNT_REC];
     c->st.nonascii_tiles = c->h_cnt[CNT_NONASCII];
-    c->st.tail_records_16 = is_idx(c) ? c->h_cnt[CNT_REC] : c->h_cnt[CNT_REC16];  // the indexer's are 24 B
+    c->st.tail_records_16 = is_idx(c) ? 0 : c->h_cnt[CNT_REC16];  // the indexer's are all 24-byte records
     const uint64_t errpos = c->h_cnt[CNT_ERRPOS];
     auto release_map = [&]() {
         agg_put(c, spec);
@@ -1577,12 +1584,15 @@ struct CommLock {
     explicit CommLock(mrg_comm *m) : lk(m->mu) { check_not_aborted(m); }
 };
 
-// Abort from any thread (mrg_run_job's watchdog), serialised with the rank threads' enqueues.  An
-// enqueue can itself block inside RCCL (a first send/recv to a peer sets up the connection and waits
-// for that peer): a lock still held after 2 s belongs to such a blocked call, which is exactly what
-// ncclCommAbort exists to release, so the abort then goes ahead without the lock.
-void comm_abort(mrg_comm *m) {
-    std::unique_lock<std::timed_mutex> lk(m->mu, std::chrono::milliseconds(2000));
+// Abort from any thread (mrg_run_job's watchdog), serialised with the rank threads' enqueues until
+// `deadline`.  An enqueue can itself block inside RCCL (a first send/recv to a peer sets up the
+// connection and waits for that peer): a lock still held at the deadline belongs to such a blocked
+// call, and the abort then goes ahead without the lock -- the accepted exception to the lock's rule,
+// since releasing a blocked call is exactly what ncclCommAbort exists for.  The watchdog aborts all
+// ranks in parallel against one deadline (a job with G hung ranks waits once, not G times).
+void comm_abort(mrg_comm *m, std::chrono::steady_clock::time_point deadline) {
+    std::unique_lock<std::timed_mutex> lk(m->mu, std::defer_lock);
+    (void)lk.try_lock_until(deadline);
     if (m->comm && !m->aborted.exchange(true)) (void)ncclCommAbort(m->comm);
 }
 
@@ -1610,6 +1620,51 @@ int agree(mrg_ctx *c, mrg_comm *m, int flag) {
 // counts message carries it (the first collective), and one status all-reduce precedes the data
 // transfer; every rank then raises together (the failing rank its own error, the others MRG_ECOMM).
 // An RCCL error aborts the communicator.
+// Pool buffers of one exchange, returned to the pool on every exit (a failed collective or a watchdog
+// abort throws past the success path).
+struct PoolLease {
+    Pool &p;
+    uint8_t *b[4] = {nullptr, nullptr, nullptr, nullptr};
+    explicit PoolLease(Pool &pool) : p(pool) {}
+    PoolLease(const PoolLease &) = delete;
+    PoolLease &operator=(const PoolLease &) = delete;
+    uint8_t *get(int i, uint64_t bytes) { return b[i] = pget<uint8_t>(p, bytes); }
+    void put(int i) {
+        p.put(b[i]);
+        b[i] = nullptr;
+    }
+    ~PoolLease() {
+        for (int i = 0; i < 4; ++i) p.put(b[i]);
+    }
+};
+
+// A pair of timing events, destroyed on every exit.
+struct EventPair {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    EventPair() {
+        HIPCHK(hipEventCreate(&e0));
+        if (hipEventCreate(&e1) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipEventDestroy(e0);
+            raise(MRG_EHIP, "hipEventCreate failed");
+        }
+    }
+    EventPair(const EventPair &) = delete;
+    EventPair &operator=(const EventPair &) = delete;
+    ~EventPair() {
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+};
+
+// An RCCL call inside the send/recv group: on failure the group is closed first (the calling thread's
+// group depth stays balanced for its next RCCL call), then the communicator is aborted.
+void group_or_abort(mrg_comm *m, ncclResult_t r, const char *what) {
+    if (r == ncclSuccess) return;
+    (void)ncclGroupEnd();
+    nccl_or_abort(m, r, what);
+}
+
 void job_shuffle(mrg_ctx *c, mrg_comm *m) {
     if (!c || !m || !m->comm) raise(MRG_EINVAL, "null context or communicator");
     if (m->device != c->device) raise(MRG_EINVAL, "communicator is on device %d, context on %d", m->device, c->device);
@@ -1619,11 +1674,8 @@ void job_shuffle(mrg_ctx *c, mrg_comm *m) {
     const uint32_t G = (uint32_t)m->n;
     const uint32_t me = (uint32_t)m->rank;
     const uint64_t X = MRG_XREC_BYTES;
-    uint8_t *srec = nullptr, *sheap = nullptr, *rrec = nullptr, *rheap = nullptr;
-    auto release = [&]() {
-        p.put(srec); p.put(sheap); p.put(rrec); p.put(rheap);
-        srec = sheap = rrec = rheap = nullptr;
-    };
+    enum { SREC, SHEAP, RREC, RHEAP };
+    PoolLease buf(p);  // send records / heap, receive records / heap: returned on every exit
     MrgError mine{MRG_OK, ""};
     // ---- local: export sizes and pack (the pack runs on the stream, no host wait)
     std::vector<uint64_t> sc(3ull * G, 0), rc(3ull * G, 0);  // per peer: records, heap bytes, status
@@ -1639,13 +1691,14 @@ void job_shuffle(mrg_ctx *c, mrg_comm *m) {
             sro[o + 1] = sro[o] + sc[3 * o];
             sho[o + 1] = sho[o] + sc[3 * o + 1];
         }
-        srec = pget<uint8_t>(p, sro[G] * X + 16);
-        sheap = pget<uint8_t>(p, sho[G] + 16);
-        export_pack(c, srec, sheap, false);
+        buf.get(SREC, sro[G] * X + 16);
+        buf.get(SHEAP, sho[G] + 16);
+        export_pack(c, buf.b[SREC], buf.b[SHEAP], false);
     } catch (const MrgError &e) {
         mine = e;
         std::fill(sc.begin(), sc.end(), 0);
     }
+    uint8_t *const srec = buf.b[SREC], *const sheap = buf.b[SHEAP];
     for (uint32_t o = 0; o < G; ++o) sc[3 * o + 2] = mine.code ? 1u : 0u;
     // ---- collective 1: the counts all-to-all (with every rank's status)
     HIPCHK(hipMemcpyAsync(m->d_counts, sc.data(), 24ull * G, hipMemcpyHostToDevice, s));
@@ -1659,11 +1712,8 @@ void job_shuffle(mrg_ctx *c, mrg_comm *m) {
     int failed_peer = -1;
     for (uint32_t o = 0; o < G; ++o)
         if (rc[3 * o + 2] && failed_peer < 0) failed_peer = (int)o;
-    if (mine.code || failed_peer >= 0) {
-        release();
-        if (mine.code) throw mine;
-        raise(MRG_ECOMM, "rank %d of the exchange failed before sending", failed_peer);
-    }
+    if (mine.code) throw mine;
+    if (failed_peer >= 0) raise(MRG_ECOMM, "rank %d of the exchange failed before sending", failed_peer);
     // ---- local: receive buffers
     std::vector<uint64_t> rro(G + 1, 0), rho(G + 1, 0), seg_rec(G), seg_heap(G);
     for (uint32_t o = 0; o < G; ++o) {
@@ -1674,54 +1724,56 @@ void job_shuffle(mrg_ctx *c, mrg_comm *m) {
     }
     try {
         test_fail("recv", (int)me);
-        rrec = pget<uint8_t>(p, rro[G] * X + 16);
-        rheap = pget<uint8_t>(p, rho[G] + 16);
+        buf.get(RREC, rro[G] * X + 16);
+        buf.get(RHEAP, rho[G] + 16);
     } catch (const MrgError &e) {
         mine = e;
     }
     // ---- collective 2: everyone ready to transfer?
     if (agree(c, m, mine.code ? 1 : 0)) {
-        release();
         if (mine.code) throw mine;
         raise(MRG_ECOMM, "another rank of the exchange could not allocate its receive buffers");
     }
+    uint8_t *const rrec = buf.b[RREC], *const rheap = buf.b[RHEAP];
     // ---- collective 3: own slice by a device copy; peers by one send/recv group (each peer pair has
     // its own xGMI link)
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    HIPCHK(hipEventRecord(e0, s));
+    EventPair ev;
+    HIPCHK(hipEventRecord(ev.e0, s));
     if (sc[3 * me]) HIPCHK(hipMemcpyAsync(rrec + rro[me] * X, srec + sro[me] * X, sc[3 * me] * X, hipMemcpyDeviceToDevice, s));
     if (sc[3 * me + 1]) HIPCHK(hipMemcpyAsync(rheap + rho[me], sheap + sho[me], sc[3 * me + 1], hipMemcpyDeviceToDevice, s));
     uint64_t sent = 0, recv = 0;
     {
         CommLock lk(m);
         nccl_or_abort(m, ncclGroupStart(), "ncclGroupStart");
+        // test knob: an RCCL failure inside the group, after the events and all four buffers exist
+        if (getenv("MRG_TEST_FAIL")) {
+            try {
+                test_fail("sendrecv", (int)me);
+            } catch (const MrgError &) {
+                group_or_abort(m, ncclInternalError, "ncclSend (MRG_TEST_FAIL=sendrecv)");
+            }
+        }
         for (uint32_t o = 0; o < G; ++o) {
             if (o == me) continue;
-            if (sc[3 * o]) nccl_or_abort(m, ncclSend(srec + sro[o] * X, sc[3 * o] * X, ncclUint8, (int)o, m->comm, s), "ncclSend");
-            if (sc[3 * o + 1]) nccl_or_abort(m, ncclSend(sheap + sho[o], sc[3 * o + 1], ncclUint8, (int)o, m->comm, s), "ncclSend");
-            if (rc[3 * o]) nccl_or_abort(m, ncclRecv(rrec + rro[o] * X, rc[3 * o] * X, ncclUint8, (int)o, m->comm, s), "ncclRecv");
-            if (rc[3 * o + 1]) nccl_or_abort(m, ncclRecv(rheap + rho[o], rc[3 * o + 1], ncclUint8, (int)o, m->comm, s), "ncclRecv");
+            if (sc[3 * o]) group_or_abort(m, ncclSend(srec + sro[o] * X, sc[3 * o] * X, ncclUint8, (int)o, m->comm, s), "ncclSend");
+            if (sc[3 * o + 1]) group_or_abort(m, ncclSend(sheap + sho[o], sc[3 * o + 1], ncclUint8, (int)o, m->comm, s), "ncclSend");
+            if (rc[3 * o]) group_or_abort(m, ncclRecv(rrec + rro[o] * X, rc[3 * o] * X, ncclUint8, (int)o, m->comm, s), "ncclRecv");
+            if (rc[3 * o + 1]) group_or_abort(m, ncclRecv(rheap + rho[o], rc[3 * o + 1], ncclUint8, (int)o, m->comm, s), "ncclRecv");
             sent += sc[3 * o] * X + sc[3 * o + 1];
             recv += rc[3 * o] * X + rc[3 * o + 1];
         }
         nccl_or_abort(m, ncclGroupEnd(), "ncclGroupEnd");
     }
-    HIPCHK(hipEventRecord(e1, s));
-    HIPCHK(hipEventSynchronize(e1));
+    HIPCHK(hipEventRecord(ev.e1, s));
+    HIPCHK(hipEventSynchronize(ev.e1));
     check_not_aborted(m);  // a watchdog abort ends a transfer early: its buffers are not to be used
-    p.put(srec);
-    p.put(sheap);
-    srec = sheap = nullptr;
+    buf.put(SREC);
+    buf.put(SHEAP);
     // ---- local: re-aggregate what arrived (no collective after this point)
     const mrg_stats keep = c->st;
     job_import(c, rrec, rro[G], rheap, rho[G], seg_rec.data(), seg_heap.data(), G);  // ends with a host wait
     float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    release();
+    HIPCHK(hipEventElapsedTime(&ms, ev.e0, ev.e1));
     // the import's aggregation time is the reduce side's; the map-side stats stay those of the map
     const double agg_import = c->st.ms_aggregate;
     c->st = keep;
@@ -2232,6 +2284,25 @@ int mrg_job_shuffle(mrg_ctx *c, mrg_comm *m) {
     return guard([&] { job_shuffle(c, m); });
 }
 
+int mrg_comm_count(const mrg_comm *m, int *n_ranks) {
+    return guard([&] {
+        if (!m || !n_ranks) raise(MRG_EINVAL, "null argument");
+        if (!m->comm || m->aborted.load()) raise(MRG_ECOMM, "the communicator was aborted");
+        int n = 0;
+        const ncclResult_t r = ncclCommCount(m->comm, &n);
+        if (r != ncclSuccess) raise(MRG_ECOMM, "ncclCommCount: %s", ncclGetErrorString(r));
+        *n_ranks = n;
+    });
+}
+
+int mrg_pool_stats(mrg_ctx *c, uint64_t *outstanding, uint64_t *held_bytes) {
+    return guard([&] {
+        if (!c) raise(MRG_EINVAL, "null context");
+        if (outstanding) *outstanding = c->pool.outstanding();
+        if (held_bytes) *held_bytes = c->pool.held_bytes();
+    });
+}
+
 }  // extern "C"
 
 namespace {
@@ -2423,8 +2494,13 @@ void run_ranks(std::vector<RankState> &rs, bool watch, F &&fn, std::vector<int> 
             if (first_fail == Clock::time_point{}) first_fail = Clock::now();
             if (ms_since(first_fail) < (double)grace_ms) continue;
             aborted = true;
+            lk.unlock();  // the rank threads report in while their communicators are aborted
+            const auto deadline = Clock::now() + std::chrono::milliseconds(2000);
+            std::vector<std::thread> ab;
             for (auto &r : rs)
-                if (r.m) comm_abort(r.m);
+                if (r.m) ab.emplace_back([m = r.m, deadline] { comm_abort(m, deadline); });
+            for (auto &t : ab) t.join();
+            lk.lock();
         }
     }
     for (auto &t : th) t.join();

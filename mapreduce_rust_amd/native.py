@@ -115,6 +115,8 @@ _SIGS = {
     "mrg_comm_init": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.POINTER(_vp)]),
     "mrg_comm_destroy": (C.c_int, [_vp]),
     "mrg_job_shuffle": (C.c_int, [_vp, _vp]),
+    "mrg_comm_count": (C.c_int, [_vp, C.POINTER(C.c_int)]),
+    "mrg_pool_stats": (C.c_int, [_vp, _u64p, _u64p]),
     "mrg_free": (None, [_vp]),
     "mrg_gen_zipf": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_double]),
     "mrg_gen_unique": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64]),
@@ -209,6 +211,12 @@ class Context:
 
     def set_stream(self, stream_ptr):
         _check(load().mrg_set_stream(self.h, stream_ptr))
+
+    def pool_stats(self):
+        """mrg_pool_stats: (device blocks handed out and not returned, bytes the pool holds)."""
+        n, b = C.c_uint64(), C.c_uint64()
+        _check(load().mrg_pool_stats(self.h, C.byref(n), C.byref(b)))
+        return n.value, b.value
 
     def set_timing(self, on=True):
         _check(load().mrg_set_timing(self.h, 1 if on else 0))
@@ -384,6 +392,12 @@ class Comm:
         self.h = h
         self.n_ranks = n_ranks
         self.rank = rank
+
+    def count(self):
+        """mrg_comm_count: ranks of the RCCL communicator (ncclCommCount)."""
+        n = C.c_int()
+        _check(load().mrg_comm_count(self.h, C.byref(n)))
+        return n.value
 
     def close(self):
         if self.h:

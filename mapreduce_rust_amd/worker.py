@@ -43,6 +43,10 @@ def read_rec(path):
         if fmt != REC_FORMAT or xb != native.XREC_BYTES:
             raise RecFileError(f"{path}: record format {fmt} ({xb}-byte records), expected {REC_FORMAT} "
                                f"({native.XREC_BYTES}-byte records)")
+        # sizes from the header are checked against the file before anything is read (a corrupt
+        # header must not make the reader allocate n * xb bytes)
+        if _REC_HDR.size + n * xb + hb != os.fstat(f.fileno()).st_size:
+            raise RecFileError(f"{path}: size does not match its header ({n} records, {hb} heap bytes)")
         rec = f.read(n * xb)
         heap = f.read(hb)
         if len(rec) != n * xb or len(heap) != hb or f.read(1):

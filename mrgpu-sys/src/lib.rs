@@ -113,6 +113,9 @@ extern "C" {
                          out: *mut *mut mrg_comm) -> c_int;
     pub fn mrg_comm_destroy(comm: *mut mrg_comm) -> c_int;
     pub fn mrg_job_shuffle(ctx: *mut mrg_ctx, comm: *mut mrg_comm) -> c_int;
+    pub fn mrg_comm_count(comm: *const mrg_comm, n_ranks: *mut c_int) -> c_int;
+
+    pub fn mrg_pool_stats(ctx: *mut mrg_ctx, outstanding: *mut u64, held_bytes: *mut u64) -> c_int;
 
     pub fn mrg_map(ctx: *mut mrg_ctx, app: c_int, h_bytes: *const u8, n: usize, doc: *const c_char, doc_id: u32,
                    n_reduce: u32, flags: u32, out: *mut *mut mrg_parts) -> c_int;

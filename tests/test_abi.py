@@ -129,6 +129,10 @@ def test_rec_file_header_checks(tmp_path):
             f.write(data[:cut])
         with pytest.raises(W.RecFileError):
             W.read_rec(p)
+    with open(p, "wb") as f:                                   # a corrupt count: refused before any read
+        f.write(struct.pack("<8sIIQQ", W.REC_MAGIC, W.REC_FORMAT, X, 1 << 60, 0) + rec)
+    with pytest.raises(W.RecFileError, match="does not match"):
+        W.read_rec(p)
     with open(p, "wb") as f:
         f.write(data + b"x")
     with pytest.raises(W.RecFileError, match="does not match"):

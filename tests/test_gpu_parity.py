@@ -89,6 +89,26 @@ def test_invalid_utf8_is_an_error(ctx):
         assert ei.value.code == -2
 
 
+def test_dense_invalid_bytes_then_reuse(ctx):
+    """Binary-like documents (KiBs of 0xFF, of 0xC3 leads without continuations, of 0xE2 0x80 pairs)
+    between valid ones: every codepoint-lead byte counts as a lead, so a 1 KiB tile can hold up to 1 KiB
+    of them -- more than the UTF-8 class path's queue takes (k_map.hip QCAP).  The job must fail with
+    MRG_EUTF8 (the reference's read_to_string panic, worker.rs:75), and the same context must then run a
+    valid job exactly (no LDS or tail-cursor corruption left behind)."""
+    import oracle_lib as O
+    import mapreduce_rust_amd as M
+    from gpu_util import run_wc
+    good = [b"fine text " * 300, "café naïve ’tis ".encode() * 200]
+    for junk in [b"\xff" * 3000, b"\xc3" * 4096, b"\xe2\x80" * 2500, b"\xf0" * 2100 + b"abc",
+                 b"ok " * 700 + b"\xc3" * 2048 + b" ok"]:
+        for R in (1, 10):
+            with pytest.raises(M.MrgError) as ei:
+                run_wc(ctx, [good[0], junk, good[1]], R)
+            assert ei.value.code == -2
+        docs = good + [b"after the error " * 500]
+        assert run_wc(ctx, docs, 10) == O.wc(docs, 10, O.FAST)
+
+
 def _rand_text(rng, n_tokens, alphabet, seps, max_len=30):
     out = []
     for _ in range(n_tokens):

@@ -300,6 +300,40 @@ def test_library_shuffle_single_rank(ctx, corpus):
         comm.close()
 
 
+def test_shuffle_failure_inside_group_releases_buffers(ctx, corpus):
+    """An RCCL failure inside the exchange's send/recv group (MRG_TEST_FAIL=sendrecv: raised after the
+    timing events and all four exchange buffers exist) aborts the communicator and fails the call with
+    MRG_ECOMM; the context's pool gets every exchange buffer back (mrg_pool_stats' outstanding count is
+    the pre-exchange one) and the same context then runs a normal job to the golden output."""
+    import mapreduce_rust_amd as M
+    from gpu_util import to_device
+    comm = M.Comm(ctx, M.comm_id(), 1, 0)
+    try:
+        assert comm.count() == 1
+        t, off = to_device(corpus)
+        ctx.job_begin(M.APP_WC, 10)
+        ctx.set_input(t.data_ptr(), off)
+        ctx.map()
+        before = ctx.pool_stats()[0]
+        os.environ["MRG_TEST_FAIL"] = "sendrecv"
+        try:
+            with pytest.raises(M.MrgError) as ei:
+                ctx.shuffle(comm)
+        finally:
+            os.environ.pop("MRG_TEST_FAIL", None)
+        assert ei.value.code == -6 and "sendrecv" in str(ei.value), ei.value
+        assert ctx.pool_stats()[0] == before
+        with pytest.raises(M.MrgError):        # the communicator stays aborted
+            comm.count()
+        ctx.job_begin(M.APP_WC, 10)
+        ctx.set_input(t.data_ptr(), off)
+        ctx.map()
+        ctx.reduce()
+        assert [sha(o) for o in ctx.outputs()] == [GOLDEN["wc"]["10"][f"mr-{r}.txt"] for r in range(10)]
+    finally:
+        comm.close()
+
+
 def _data_dir(tmp_path, corpus, extra=None):
     d = tmp_path / "data"
     d.mkdir()
