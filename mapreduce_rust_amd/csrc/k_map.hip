@@ -55,7 +55,7 @@ constexpr int NSUB = MRG_MAP_NSUB;               // 1 KiB tiles per block
 constexpr int BLK = NSUB * TILE;                 // bytes per wave iteration
 // staged window + slack for the 5-dword key reads (a key starts within 31 bytes of a token start)
 constexpr int WIN = BEHIND + TILE + HALO + 48;
-constexpr int QCAP = TILE / 2 + 16;  // a start needs a space before it; <= 520 codepoint leads
+constexpr int QCAP = TILE / 2 + 16;  // token starts of a tile (a start needs a space before it)
 constexpr int NMP = 64;         // mask pairs per wave (one per segment of the tile)
 static_assert(TILE == 64 * SEG, "one segment per lane");
 static_assert(WIN % 16 == 0, "16-byte window rows");
@@ -110,17 +110,6 @@ template <class T>
 __device__ __forceinline__ T g_add(T *p, T v) {
     return __hip_atomic_fetch_add(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// wave-aggregated append on a global counter (one atomic per wave): this lane's slot if pred
-__device__ __forceinline__ uint64_t g_wave_append(unsigned long long *counter, bool pred) {
-    const uint64_t mask = __ballot(pred);
-    if (!mask) return 0;
-    const int leader = __ffsll((long long)mask) - 1;
-    unsigned long long base = 0;
-    if ((int)__lane_id() == leader) base = g_add(counter, (unsigned long long)__popcll(mask));
-    base = __shfl(base, leader);
-    return base + (uint64_t)__popcll(mask & mrg_lanemask_lt());
-}
-
 // 64-bit min/max as plain compares (HIP's overload set can resolve max(u64, u64) to the double
 // version: a VALU f64 round trip per call)
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
@@ -357,6 +346,7 @@ struct TailRegions {
     const unsigned long long *end;
     unsigned long long *cur16;  // wc keys of 13..16 bytes: their own regions of 16-byte records
     const unsigned long long *end16;
+    unsigned int *lcnt;         // long-token records of this workgroup so far (its region's cursor)
 };
 typedef uint32_t u32x3a __attribute__((ext_vector_type(3), aligned(4)));  // one 12-byte tail record
 
@@ -513,12 +503,30 @@ __device__ __forceinline__ void emit(const MapArgs &A, LdsTable<CAP, IDX> &table
             }
         }
     }
+    // long tokens: the workgroup's own region through an LDS cursor (one LDS atomic per wave).  Until
+    // r04 every such wave took its slots from ONE device-wide counter: a returning atomic on a single
+    // address serialises chip-wide (~90 per microsecond), which bounded k_map on Gutenberg-like text,
+    // where em-dash-joined words make ~1.2 M long tokens per 10 GiB, at ~14 ms.
     if (__any(is_long)) {
-        const uint64_t li = g_wave_append(&A.counters[CNT_LONG], is_long);
-        if (is_long && li < A.lcap) {
-            gp(A.lstart)[li] = tstart;
-            gp(A.llen)[li] = traw;
-            gp(A.ldoc)[li] = docid;
+        const uint64_t mask = __ballot(is_long);
+        const int leader = __ffsll((long long)mask) - 1;
+        uint32_t base = 0;
+        if ((int)__lane_id() == leader) base = atomicAdd(R.lcnt, (unsigned int)__popcll(mask));
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+        const uint32_t k = base + (uint32_t)__popcll(mask & mrg_lanemask_lt());
+        if (is_long) {
+            uint64_t li = ~0ull;
+            if (k < A.lper) {
+                li = (uint64_t)blockIdx.x * A.lper + k;
+            } else {  // region full (rare): the shared list
+                const uint64_t j = g_add(&A.counters[CNT_LONGX], 1ull);
+                if (j < A.lovf) li = (uint64_t)gridDim.x * A.lper + j;
+            }
+            if (li != ~0ull) {
+                gp(A.lstart)[li] = tstart;
+                gp(A.llen)[li] = traw;
+                gp(A.ldoc)[li] = docid;
+            }
         }
     }
 }
@@ -644,6 +652,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ uint8_t s_uc[9 * 64];
     __shared__ uint32_t s_tot[3];                        // workgroup totals: tokens, tail records, 16-byte ones
     __shared__ unsigned int s_fill;                      // table slots claimed
+    __shared__ unsigned int s_lcnt;                      // long-token records (region cursor)
     __shared__ unsigned int s_door[MRG_MAP_DOOR ? LdsTable<CAP, IDX>::DW : 1];  // admission bitmap
     static_assert(sizeof(s_q) >= CAP * sizeof(uint16_t), "flush ranks reuse the queues");
 
@@ -678,6 +687,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         s_tot[1] = 0;
         s_tot[2] = 0;
         s_fill = 0;
+        s_lcnt = 0;
     }
     if (tid < 9 * 64) {
         const uint32_t blk = tid < 512 ? (uint32_t)tid >> 6 : 0x20u;
@@ -701,7 +711,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         s_sel[L * 17u + g][j] = ((0x00010203u + (gm & 0x01010101u)) & ~zm) | (0x0C0C0C0Cu & zm);
     }
     LdsTable<CAP, IDX> table{s_key, s_cnt, s_doc, s_door, &s_fill};
-    const TailRegions tails{s_tcur, s_tend, s_tcur16, s_tend16};
+    const TailRegions tails{s_tcur, s_tend, s_tcur16, s_tend16, &s_lcnt};
     uint32_t my_tokens = 0;
     // uniform job parameters used in the hot loop, read once
     // ablation knobs (MRG_ABLATE, timing only) exist in -DMRG_MAP_ABLATION builds; in the product
@@ -978,14 +988,17 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
 #ifdef MRG_MAP_NO_UNI
             defer_blk = true;  // A/B builds only: every such block to the exact walker, as in r03
 #else
-            // UTF-8-exact classes by codepoint compaction: every lane lists the codepoint leads (bytes
-            // >= 0xC0 inside the document) of its segments, a wave prefix sum packs them into the
-            // queue, and each lane decodes ONE codepoint per round from the staged window -- one round
-            // for up to 64 codepoints (a per-lane walk over its segment's codepoints made the wave wait
-            // for its busiest lane, once per segment kind).  The owners read their leads' lengths and
-            // classes back in order; a codepoint's last bytes may lie in the next segment (DPP).  Every
-            // non-ASCII byte must be covered by a decoded codepoint, else the block holds invalid UTF-8
-            // and is deferred.
+            // UTF-8-exact classes in registers (r05): every lane decodes the codepoints whose leads lie
+            // in its own segments, straight from the segment's four dwords and the next segment's first
+            // (DPP) -- no LDS window, no queue, no compaction.  One loop over the lane's leads, both
+            // segments per trip (the trip count is the busiest lane's lead count: about 2 per block on
+            // English text, whose non-ASCII codepoints are sparse).  A lead's bytes are checked by the
+            // decode (continuation bytes, overlongs, surrogates, range); a codepoint's last bytes may lie in
+            // the next segment (spilled by DPP).  Every non-ASCII byte must be covered by a decoded
+            // codepoint, else the block holds invalid UTF-8 and is deferred.  (r04 compacted the leads
+            // into the wave's queue and decoded one per lane from the staged window: two stagings,
+            // two queue fills and two divergent read-backs per block, and a queue that invalid input
+            // with more than 528 leads per tile could overflow.)
             const int64_t dlo = (int64_t)(doc_lo - Ab);  // two's complement (see lo below)
             // the document in block offsets: lo in [-16, 16), hi in (0, 2112].  (A select on
             // doc_lo > Ab lost its first case in the compiled code: keep a clamped signed difference.)
@@ -1023,90 +1036,77 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 if (bb < 0xC0u || pbp < lo) bad = true;
                 else has_b = true;
             }
-            const uint32_t hasb = (lane == 0 && has_b) ? 1u : 0u;
-            const uint32_t c0 = (uint32_t)__builtin_popcount(ld0) + hasb;
-            const uint32_t c1 = (uint32_t)__builtin_popcount(ld1) + (uint32_t)__builtin_popcount(ldh);
-            const uint32_t incl = wave_incl_scan(c0 | (c1 << 16));
-            const uint32_t tot = lane_u32(incl, 63);
-            const uint32_t e0 = (incl & 0xFFFFu) - c0, e1 = (incl >> 16) - c1;  // first slots
-            // Valid UTF-8 has at most 520 leads per chunk (every lead is followed by a continuation
-            // byte), so the queue holds them; more leads (binary data: 1 KiB of 0xFF or 0xC3 0xC3 ...)
-            // can only be invalid -- the block is deferred to the exact walker, which reports the
-            // first bad byte, without writing past the wave's queue (tot is wave-uniform)
-            if ((tot & 0xFFFFu) > (uint32_t)QCAP || (tot >> 16) > (uint32_t)QCAP) {
-                defer_blk = true;
-            } else {
-            // decode queue entries [0, n): window index in (the chunk's tile staged at block offset cb),
-            // length | class << 3 out (0: invalid)
-            auto decode = [&](uint32_t n, int cb) {
-                wave_sync_lds();
-                const uint32_t *w32 = reinterpret_cast<const uint32_t *>(win);
-                for (uint32_t base = 0; base < n; base += 64) {
-                    const uint32_t j = base + (uint32_t)lane;
-                    if (j < n) {
-                        const uint32_t e = queue[j];
-                        const uint32_t v = __builtin_amdgcn_alignbyte(w32[(e >> 2) + 1u], w32[e >> 2], e & 3u);
-                        auto rd = [&](uint64_t a) -> uint32_t { return (v >> (8u * (uint32_t)a)) & 0xFFu; };
-                        uint32_t cp = 0, raw;
-                        const int ln = mrg_utf8_decode(rd, 0ull, (uint64_t)min(hi - (cb + (int)e - BEHIND), 4), &cp, &raw);
-                        queue[j] = (uint16_t)(ln > 0 ? (uint32_t)ln | (uni_class(uc, cp) << 3) : 0u);
+            // the 4 bytes after each segment: the next lane's first dword (lane 63: tile 1's first
+            // segment after tile 0, the first halo segment after tile 1); after the halo segment, lane
+            // 2's e (the halo's next 16 bytes)
+            const uint32_t v1_first = lane_u32(X.v1.x, 0), halo_next = lane_u32(X.e.x, 2);
+            uint32_t nA = from_next_lane(X.v0.x), nB = from_next_lane(X.v1.x);
+            if (lane == 63) {
+                nA = v1_first;
+                nB = xh.x;
+            }
+            // one codepoint whose lead is byte p of the 20-byte window d0..d4 starting at block offset so:
+            // W / S / covered-byte masks over the window (bits 16..19 spill into the next segment)
+            auto dec = [&](uint32_t p, uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t d4, int so,
+                           uint32_t &W, uint32_t &S, uint32_t &C) {
+                const uint32_t k = p >> 2;
+                const uint32_t a = (k & 2u) ? ((k & 1u) ? d3 : d2) : ((k & 1u) ? d1 : d0);
+                const uint32_t b = (k & 2u) ? ((k & 1u) ? d4 : d3) : ((k & 1u) ? d2 : d1);
+                const uint32_t w = __builtin_amdgcn_alignbyte(b, a, p & 3u);
+                auto rd = [&](uint64_t x) -> uint32_t { return (w >> (8u * (uint32_t)x)) & 0xFFu; };
+                uint32_t cp = 0, raw;
+                const int n = mrg_utf8_decode(rd, 0ull, (uint64_t)min(hi - (so + (int)p), 4), &cp, &raw);
+                bad |= n == 0;
+                const uint32_t span = ((1u << n) - 1u) << p;
+                const uint32_t cl = uni_class(uc, cp);
+                C |= span;
+                W |= cl == MRG_CLS_W ? span : 0u;
+                S |= cl == MRG_CLS_S ? span : 0u;
+            };
+            uint32_t W0 = 0, S0 = 0, C0 = 0, W1 = 0, S1 = 0, C1 = 0;
+            for (uint32_t mA = ld0, mB = ld1; __any((mA | mB) != 0u);) {
+                if (mA) {
+                    const uint32_t p = (uint32_t)__builtin_ctz(mA);
+                    mA &= mA - 1u;
+                    dec(p, X.v0.x, X.v0.y, X.v0.z, X.v0.w, nA, (int)l16, W0, S0, C0);
+                }
+                if (mB) {
+                    const uint32_t p = (uint32_t)__builtin_ctz(mB);
+                    mB &= mB - 1u;
+                    dec(p, X.v1.x, X.v1.y, X.v1.z, X.v1.w, nB, 1024 + (int)l16, W1, S1, C1);
+                }
+            }
+            // lane 0: the codepoint holding the byte before the block (window = the 16 bytes before it +
+            // the block's first 4, lead at 16 + pbp); lane 63: the first halo segment's leads
+            uint32_t WE = 0, SE = 0, CE = 0;
+            {
+                const bool l0 = lane == 0;
+                uint32_t mE = l0 ? (has_b ? 1u << (16 + pbp) : 0u) : ldh;
+                const uint4 xe = l0 ? X.e : xh;
+                const uint32_t ne = l0 ? X.v0.x : halo_next;
+                const int soe = l0 ? -16 : BLK;
+                while (__any(mE != 0u)) {
+                    if (mE) {
+                        const uint32_t p = (uint32_t)__builtin_ctz(mE);
+                        mE &= mE - 1u;
+                        dec(p, xe.x, xe.y, xe.z, xe.w, ne, soe, WE, SE, CE);
                     }
                 }
-                wave_sync_lds();
-            };
-            // the decoded codepoints of leads ld (first slot k) as W, S and covered-byte masks; bits 16..18
-            // are bytes of the next segment
-            auto own = [&](uint32_t ld, uint32_t k, uint32_t &W, uint32_t &S, uint32_t &C) {
-                W = S = C = 0u;
-                for (uint32_t m = ld; m; m &= m - 1u, ++k) {
-                    const uint32_t r = queue[k], n = r & 7u, cl = r >> 3;
-                    bad |= n == 0u;
-                    const uint32_t span = ((1u << n) - 1u) << __builtin_ctz(m);
-                    C |= span;
-                    W |= cl == MRG_CLS_W ? span : 0u;
-                    S |= cl == MRG_CLS_S ? span : 0u;
-                }
-            };
-            // chunk 1 (tile 1, the first halo segment), then chunk 0 (the codepoint holding the byte
-            // before the block, tile 0), each decoded from its tile's window; tile 0 stays staged
-            uint32_t W1, S1, C1, Wh, Sh, Ch;
-            wave_sync_lds();
-            reinterpret_cast<uint4 *>(win)[1 + lane] = X.v1;
-            if (lane >= 1 && lane < 5) reinterpret_cast<uint4 *>(win)[64 + lane] = X.e;  // the halo
-            {
-                uint32_t k = e1;
-                for (uint32_t m = ld1; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + l16 + __builtin_ctz(m));
-                for (uint32_t m = ldh; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + TILE + __builtin_ctz(m));
             }
-            decode(tot >> 16, TILE);
-            own(ld1, e1, W1, S1, C1);
-            own(ldh, e1 + (uint32_t)__builtin_popcount(ld1), Wh, Sh, Ch);
-            wave_sync_lds();
-            reinterpret_cast<uint4 *>(win)[1 + lane] = X.v0;
-            if (lane < 4) reinterpret_cast<uint4 *>(win)[65 + lane] = X.v1;
-            if (lane == 0) reinterpret_cast<uint4 *>(win)[0] = X.e;  // the 16 bytes before the block
-            {
-                uint32_t k = e0;
-                if (hasb) queue[k++] = (uint16_t)(BEHIND + pbp);
-                for (uint32_t m = ld0; m; m &= m - 1u) queue[k++] = (uint16_t)(BEHIND + l16 + __builtin_ctz(m));
-            }
-            decode(tot & 0xFFFFu, 0);
-            uint32_t W0, S0, C0, bsp = 0, pb_l = prev_blk;
-            if (hasb) {  // its bytes from 0 on spill into tile 0's first segment; byte -1 gives prev_blk
-                const uint32_t r = queue[e0], n = r & 7u, cl = r >> 3;
-                const int end = pbp + (int)n;
-                if (n == 0u || end < 0) {
-                    bad = true;
-                } else {
-                    const uint32_t sp = (1u << end) - 1u;
-                    bsp = sp | ((cl == MRG_CLS_W ? sp : 0u) << 4) | ((cl == MRG_CLS_S ? sp : 0u) << 8);
-                    pb_l = cl == MRG_CLS_S ? 1u : 0u;
-                }
-            }
-            own(ld0, e0 + hasb, W0, S0, C0);
+            uint32_t bsp = 0, pb_l = prev_blk, Wh = 0, Sh = 0, Ch = 0;
             // spills (C | W << 4 | S << 8 of bits 16..18) into the next segment: lane l+1, tile 1's lane
             // 0 after tile 0's lane 63, the halo segment after tile 1's lane 63 (same lane)
             auto pack = [](uint32_t W, uint32_t S, uint32_t C) { return (C >> 16) | ((W >> 16) << 4) | ((S >> 16) << 8); };
+            if (lane == 0 && has_b) {
+                bad |= (CE & 0x8000u) == 0u;  // the codepoint must reach byte -1
+                bsp = pack(WE, SE, CE);
+                pb_l = (SE >> 15) & 1u;
+            }
+            if (lane == 63) {
+                Wh = WE;
+                Sh = SE;
+                Ch = CE;
+            }
             const uint32_t sp0 = pack(W0, S0, C0), sp1 = pack(W1, S1, C1);
             uint32_t in0 = from_prev_lane(sp0), in1 = from_prev_lane(sp1);
             const uint32_t sp0_last = lane_u32(sp0, 63);
@@ -1129,7 +1129,6 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             prev_blk = lane_u32(pb_l, 0);
             defer_blk = __any(bad);
             if (!defer_blk && lane == 0) atomicAdd(&s_nuni, Ab + (uint64_t)TILE < doc_hi ? 2u : 1u);
-            }
 #endif
         }
         MRG_PT(1);
@@ -1407,6 +1406,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         g_add(&A.counters[CNT_REC], (unsigned long long)s_tot[1]);
         if (s_tot[2]) g_add(&A.counters[CNT_REC16], (unsigned long long)s_tot[2]);
         if (s_ngen + s_nuni) g_add(&A.counters[CNT_NONASCII], (unsigned long long)(s_ngen + s_nuni));
+        gp(A.lcount)[blockIdx.x] = s_lcnt;
+        if (s_lcnt) g_add(&A.counters[CNT_LONG], (unsigned long long)s_lcnt);
     }
     MRG_PT(6);
 #ifdef MRG_MAP_PROF
@@ -1478,7 +1479,37 @@ __global__ void k_long_gather(const uint8_t *in, const uint64_t *lstart, const u
     }
 }
 
+// Dense long-token records (see mrg_launch_long_compact): block w < grid copies region w, block grid
+// the shared list; each block finds its output offset by summing the regions before it.
+__global__ void k_long_compact(const uint64_t *__restrict__ rs, const uint32_t *__restrict__ rl,
+                               const uint32_t *__restrict__ rd, const uint32_t *__restrict__ lcount, uint32_t lper,
+                               uint64_t lovf, const unsigned long long *__restrict__ counters, uint32_t grid,
+                               uint64_t *__restrict__ start, uint32_t *__restrict__ len, uint32_t *__restrict__ doc) {
+    __shared__ unsigned long long s_off;
+    const uint32_t w = blockIdx.x;
+    if (threadIdx.x == 0) s_off = 0;
+    __syncthreads();
+    unsigned long long part = 0;
+    for (uint32_t v = threadIdx.x; v < w; v += blockDim.x) part += min(lcount[v], lper);
+    if (part) atomicAdd(&s_off, part);
+    __syncthreads();
+    const uint64_t off = s_off;
+    const uint64_t n = w < grid ? (uint64_t)min(lcount[w], lper) : umin64(counters[CNT_LONGX], lovf);
+    const uint64_t src = (uint64_t)w * lper;  // block grid: the list right after the regions
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        start[off + i] = rs[src + i];
+        len[off + i] = rl[src + i];
+        doc[off + i] = rd[src + i];
+    }
+}
+
 }  // namespace
+
+void mrg_launch_long_compact(const MapArgs &A, int grid, uint64_t *start, uint32_t *len, uint32_t *doc,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(k_long_compact, dim3((unsigned)grid + 1), dim3(256), 0, s, A.lstart, A.llen, A.ldoc, A.lcount,
+                       A.lper, A.lovf, A.counters, (uint32_t)grid, start, len, doc);
+}
 
 template <int CAP, bool IDX>
 static void launch_map_t(const MapArgs *a, int grid, hipStream_t s) {

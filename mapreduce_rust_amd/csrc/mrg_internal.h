@@ -36,7 +36,8 @@ enum {
     CNT_OVF2 = 6,     // keys that did not fit their bucket's LDS table (exact overflow path)
     CNT_NONASCII = 7, // 1 KiB tiles that took the non-ASCII tokenizer
     CNT_REC16 = 8,    // of CNT_REC: 16-byte tail records (wc keys of 13..16 bytes)
-    CNT_N = 9
+    CNT_LONGX = 9,    // long-token records beyond their workgroup's region (the shared list)
+    CNT_N = 10
 };
 
 // Stream-ordered caching allocator interface (all work of a context runs on one stream, so a
@@ -76,10 +77,15 @@ struct MapArgs {
     // foff[g * (NBUCKET + 1) + b] = start of bucket b in that region
     uint64_t *fk0, *fk1;
     uint32_t *fcnt, *fdoc, *foff;
-    // long-key token records (> 16 key bytes)
+    // long-key token records (> 16 key bytes): map workgroup w appends to its region, records
+    // [w * lper, + lper), through an LDS cursor; beyond it to the shared list [grid * lper, + lovf)
+    // (a device atomic each; a full list reruns the launch).  lcount[w] = records workgroup w produced
+    // (may exceed lper); mrg_launch_long_compact packs them densely afterwards.
     uint64_t *lstart;
     uint32_t *llen, *ldoc;
-    uint64_t lcap;
+    uint32_t lper;
+    uint64_t lovf;
+    uint32_t *lcount;
     // non-ASCII tiles, recorded by the main loop and processed after it: workgroup g appends the
     // index of each such tile (relative to its first block's first tile) to gbits[g * kwords ..)
     uint32_t *gbits;
@@ -152,6 +158,11 @@ void mrg_launch_map(const MapArgs *h, MapArgs *dev_args, int app, int grid, int 
 uint64_t mrg_map_tiles(uint64_t doc_lo, uint64_t doc_hi);  // wave blocks (NSUB KiB) of a document (16-B grid)
 int mrg_map_cap(int app, int lds_cap);  // LDS-table entries per map workgroup actually used for lds_cap
 int mrg_map_max_grid(int app, int lds_cap, int device);
+// Dense long-token records from the map's per-workgroup regions and shared list (A as launched):
+// region w's min(lcount[w], lper) records, then min(counters[CNT_LONGX], lovf) list records, to
+// [0, n) of (start, len, doc); n = their total (on the device: counters[CNT_LONG] when nothing was lost).
+void mrg_launch_long_compact(const MapArgs &A, int grid, uint64_t *start, uint32_t *len, uint32_t *doc,
+                             hipStream_t s);
 void mrg_launch_long_prep(const uint8_t *base, const uint64_t *start, const uint32_t *rawlen, uint64_t n,
                           uint64_t *k0, uint64_t *k1, uint32_t *flen, uint64_t *flen64, uint64_t *fp,
                           uint32_t hash_bits, int verbatim, hipStream_t s);

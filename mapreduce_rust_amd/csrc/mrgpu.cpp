@@ -211,6 +211,7 @@ struct mrg_ctx {
     int lds_cap = 4096;
     int map_grid = 0;
     uint64_t long_hint = 0, ovf_hint = 0;
+    uint64_t lper_hint = 0;  // long-token records per map workgroup region (grown on a rerun)
     uint32_t agg_nsub = 1;  // bucket-aggregation workgroups per bucket (grown when the tables overflow)
     std::vector<double> bcap_rate;  // tail records per (bucket, map workgroup) per input byte of the workgroup
     std::vector<double> bcap16_rate;  // the same for the 16-byte regions (wc keys of 13..16 bytes)
@@ -433,11 +434,14 @@ struct MapBufs {
     uint64_t *fk0 = nullptr, *fk1 = nullptr;
     uint32_t *fcnt = nullptr, *fdoc = nullptr, *foff = nullptr;
     uint64_t *lstart = nullptr;
-    uint32_t *llen = nullptr, *ldoc = nullptr;
+    uint32_t *llen = nullptr, *ldoc = nullptr, *lcount = nullptr;
+    uint64_t *dstart = nullptr;  // long-token records packed densely after the map
+    uint32_t *dlen = nullptr, *ddoc = nullptr;
     uint32_t *gbits = nullptr;
     unsigned long long *prof = nullptr;
     void release(Pool &p) {
         p.put(prof);
+        p.put(lcount); p.put(dstart); p.put(dlen); p.put(ddoc);
         p.put(pool); p.put(rbase); p.put(bcap); p.put(bcount); p.put(dargs); p.put(ovf); p.put(onext);
         p.put(pool16); p.put(rbase16); p.put(bcap16); p.put(bcount16);
         p.put(fk0); p.put(fk1); p.put(fcnt); p.put(fdoc); p.put(foff);
@@ -525,7 +529,7 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         AggLaunch L;
         // the queued launch is reused only when it ran with this job's parameters: sub-ranges, overflow
         // capacity, count width, and key slots for at least the long keys the map produced (the map
-        // reruns whenever its long keys exceed lcap, which drops the queued launch, so li.n <= nlong
+        // reruns whenever its long keys exceed their capacity, which drops the queued launch, so li.n <= nlong
         // holds here; it is checked rather than assumed)
         if (pre && pre->live && agg_launches == 1 && pre->B.nsub == nsub && pre->B.ocap == ocap &&
             li.n <= pre->nlong &&
@@ -1051,14 +1055,25 @@ void job_map(mrg_ctx *c) {
         M.fcnt = pget<uint32_t>(p, (uint64_t)grid * cap);
         M.fdoc = idx ? pget<uint32_t>(p, (uint64_t)grid * cap) : nullptr;
         M.foff = pget<uint32_t>(p, (uint64_t)grid * (MRG_NBUCKET + 1));
-        M.lstart = pget<uint64_t>(p, lcap);
-        M.llen = pget<uint32_t>(p, lcap);
-        M.ldoc = pget<uint32_t>(p, lcap);
+        // long tokens: per-workgroup regions of lper records + a shared list of lovf
+        uint64_t lper = std::max<uint64_t>(c->lper_hint, (lcap + grid - 1) / grid + 16);
+        uint64_t lovf = lcap / 4 + 1024;
+        if (launches == 0) {  // test knobs (first launch only: a rerun grows them from the measured demand)
+            if (const uint64_t t = env_u64("MRG_TEST_LONG_PER", 0)) lper = t;
+            if (const uint64_t t = env_u64("MRG_TEST_LONG_LIST", 0)) lovf = t;
+        }
+        if (lper > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
+        const uint64_t lslots = (uint64_t)grid * lper + lovf;
+        M.lstart = pget<uint64_t>(p, lslots);
+        M.llen = pget<uint32_t>(p, lslots);
+        M.ldoc = pget<uint32_t>(p, lslots);
+        M.lcount = pget<uint32_t>(p, (uint64_t)grid);
         A.pool = M.pool; A.rbase = M.rbase; A.bcap = M.bcap; A.bcount = M.bcount;
         A.pool16 = M.pool16; A.rbase16 = M.rbase16; A.bcap16 = M.bcap16; A.bcount16 = M.bcount16;
         A.ovf = M.ovf; A.onext = M.onext; A.ocap = (uint32_t)ocap;
         A.fk0 = M.fk0; A.fk1 = M.fk1; A.fcnt = M.fcnt; A.fdoc = M.fdoc; A.foff = M.foff;
-        A.lstart = M.lstart; A.llen = M.llen; A.ldoc = M.ldoc; A.lcap = lcap;
+        A.lstart = M.lstart; A.llen = M.llen; A.ldoc = M.ldoc; A.lper = (uint32_t)lper; A.lovf = lovf;
+        A.lcount = M.lcount;
         {  // non-ASCII tile lists: one entry per tile of a workgroup's share at most
             const uint64_t per_wg_blocks = (n_chunks + grid - 1) / grid + 1;
             A.kwords = (uint32_t)(MRG_MAP_NSUB * per_wg_blocks);
@@ -1092,7 +1107,7 @@ void job_map(mrg_ctx *c) {
             ev_rec(c, 2);
             uint32_t nsub = c->agg_nsub;
             if (const uint64_t t = env_u64("MRG_TEST_AGG_NSUB", 0)) nsub = (uint32_t)t;
-            spec = agg_launch(c, A, (uint32_t)grid, cap, agg_ocap(c), nsub, lcap, c->spec_c32 && grid <= 512, false);
+            spec = agg_launch(c, A, (uint32_t)grid, cap, agg_ocap(c), nsub, lslots, c->spec_c32 && grid <= 512, false);
         }
         // overflow-list fill into pinned scratch, then the counters: one host wait for both
         uint32_t *onext = (uint32_t *)&c->h_cnt[CNT_N + 8];
@@ -1132,7 +1147,8 @@ void job_map(mrg_ctx *c) {
             }
         }
         const uint64_t nl = c->h_cnt[CNT_LONG];
-        if (c->h_cnt[CNT_OVF] == 0 && nl <= lcap) break;
+        const bool long_full = c->h_cnt[CNT_LONGX] > A.lovf;
+        if (c->h_cnt[CNT_OVF] == 0 && !long_full) break;
         if (spec.live) c->st.spec_agg = 2;  // the rerun invalidates the queued aggregation
         agg_put(c, spec);
         // capacity exceeded: grow each bucket's regions to its demand (remembered), run again
@@ -1158,10 +1174,18 @@ void job_map(mrg_ctx *c) {
             }
             ocap = c->ocap_hint = 4 * ocap;
         }
-        if (nl > lcap) lcap = c->long_hint = nl + nl / 8 + 1024;
+        if (long_full) {  // a workgroup's long tokens overflowed its region and the list: grow both
+            std::vector<uint32_t> lc((uint64_t)grid);
+            HIPCHK(hipMemcpyAsync(lc.data(), M.lcount, 4ull * grid, hipMemcpyDeviceToHost, s));
+            sync(c);
+            const uint64_t mx = *std::max_element(lc.begin(), lc.end());
+            c->lper_hint = mx + mx / 4 + 64;
+            lcap = c->long_hint = std::max<uint64_t>(lcap, nl + nl / 8 + 1024);
+        }
         if (getenv("MRG_DEBUG"))
-            fprintf(stderr, "[mrgpu] map rerun: tail overflow %llu, long %llu/%llu\n",
-                    (unsigned long long)c->h_cnt[CNT_OVF], (unsigned long long)nl, (unsigned long long)lcap);
+            fprintf(stderr, "[mrgpu] map rerun: tail overflow %llu, long %llu (list %llu of %llu)\n",
+                    (unsigned long long)c->h_cnt[CNT_OVF], (unsigned long long)nl,
+                    (unsigned long long)c->h_cnt[CNT_LONGX], (unsigned long long)A.lovf);
         M.release(p);
     }
     if (getenv("MRG_DEBUG"))
@@ -1191,8 +1215,15 @@ void job_map(mrg_ctx *c) {
     }
     if (!spec.live) ev_rec(c, 2);
     LongItems li{};
-    li.base = c->d_in; li.start = M.lstart; li.rawlen = M.llen; li.doc = M.ldoc; li.cnt = nullptr;
+    li.base = c->d_in; li.cnt = nullptr;
     li.n = c->h_cnt[CNT_LONG];
+    if (li.n) {  // pack the workgroups' regions and the shared list densely
+        M.dstart = pget<uint64_t>(p, li.n);
+        M.dlen = pget<uint32_t>(p, li.n);
+        M.ddoc = pget<uint32_t>(p, li.n);
+        mrg_launch_long_compact(A, grid, M.dstart, M.dlen, M.ddoc, s);
+    }
+    li.start = M.dstart; li.rawlen = M.dlen; li.doc = M.ddoc;
     // high cardinality (most tokens missed the map-side combine): sort-based aggregation
     bool wide = !idx && c->h_cnt[CNT_REC] > (32ull << 20) && 2 * c->h_cnt[CNT_REC] > c->h_cnt[CNT_TOKENS];
     if (const char *v = getenv("MRG_WIDE")) wide = !idx && atoi(v) != 0;  // test / tuning override

@@ -122,7 +122,7 @@ def _mixed_keys_doc(seed, n_words=200_000):
 def knobs():
     keys = ["MRG_TEST_TAIL_CAP", "MRG_TEST_OVF_CAP", "MRG_TEST_AGG_OCAP", "MRG_WIDE", "MRG_TEST_LEAF_CAP",
             "MRG_TEST_LEAF_TARGET", "MRG_TEST_SORT_LCAP", "MRG_TEST_AGG_WIDE_OVF", "MRG_TEST_AGG_NSUB",
-            "MRG_TEST_NO_PACK"]
+            "MRG_TEST_NO_PACK", "MRG_TEST_LONG_PER", "MRG_TEST_LONG_LIST"]
     saved = {k: os.environ.get(k) for k in keys}
 
     def set_(**kw):
@@ -273,6 +273,43 @@ def test_bucket_overflow_falls_back_to_wide_vs_oracle(ctx, corpus, knobs):
         got = run_wc(ctx, corpus, R, flags=M.debug_hash_bits(4))
         assert ctx.stats()["agg_launches"] == 0  # no completed bucket aggregation: the wide path ran
         assert got == O.wc(corpus, R, O.FAST), R
+
+
+def _long_token_docs(seed, n_docs=6, n_tokens=60_000):
+    """Text where about a third of the tokens have keys of more than 16 bytes: em-dash-joined word
+    pairs (the long tokens of Gutenberg text), long Unicode words, a few hundred distinct each."""
+    import random
+    rng = random.Random(seed)
+    short = ["the", "of", "and", "wine", "don\u2019t", "caf\u00e9"]
+    longs = ["".join(rng.choice("abcdefghij") for _ in range(rng.randint(17, 40))) for _ in range(300)]
+    longs += [a + "\u2014" + b for a, b in zip(rng.choices(short + longs[:20], k=200), rng.choices(longs, k=200))]
+    longs += ["\u017f" * 9 + "x" for _ in range(3)]   # 19 key bytes of 2-byte letters
+    docs = []
+    for _ in range(n_docs):
+        toks = [rng.choice(longs) if rng.random() < 0.35 else rng.choice(short) for _ in range(n_tokens)]
+        docs.append(" ".join(toks).encode())
+    return docs
+
+
+@pytest.mark.parametrize("per,lst", [(0, 0), (1, 100_000), (1, 3)])
+def test_long_token_regions_vs_oracle(ctx, knobs, per, lst):
+    """Long tokens (keys > 16 bytes) go to the map workgroup's own region through an LDS cursor; a full
+    region spills into the shared list (MRG_TEST_LONG_PER=1: every workgroup's second long token), a full
+    list reruns the launch with regions grown to the measured demand (MRG_TEST_LONG_LIST=3).  The
+    regions are packed densely after the map: wc and indexer outputs equal the oracle's."""
+    import oracle_lib as O
+    import mapreduce_rust_amd as M
+    from gpu_util import run_wc
+    docs = _long_token_docs(per * 7 + lst)
+    knobs(**({"MRG_TEST_LONG_PER": per, "MRG_TEST_LONG_LIST": lst} if per else {}))
+    for R in (1, 10):
+        assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST), R
+        st = ctx.stats()
+        assert st["long_tokens"] > 50_000
+        if lst == 3:
+            assert st["map_launches"] >= 2
+    names = [f"data/gut-{m}.txt" for m in range(len(docs))]
+    assert run_wc(ctx, docs, 10, app=M.APP_INDEXER, names=names) == O.indexer(docs, names, 10)
 
 
 def test_library_shuffle_single_rank(ctx, corpus):
