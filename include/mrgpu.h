@@ -97,12 +97,16 @@ typedef struct {
                                   others are 12-byte records); 0 for the indexer (all 24-byte records) */
     uint32_t spec_agg;         /* the aggregation queued behind the map: 0 none, 1 used, 2 dropped */
     uint32_t agg_path;         /* aggregation taken: 0 none, 1 bucket tables, 2 wide (sort-based) */
+    uint32_t map_kind;         /* map kernel: 0 LDS combine + hash-bucketed tail records, 1 the wide map
+                                  (near-unique keys: every key straight to its sort bucket) */
+    uint32_t reserved;
 } mrg_stats;
 
 /* ABI history: 1 = round-1 layout; 2 = mrg_run_job's last argument is n_gpus (was a device index);
  * 3 = 24-byte exchange records (were 40), mrg_run_get_stats; 4 = mrg_stats gains nonascii_tiles,
- * tail_records_16, spec_agg, agg_path.  mrg_version() names the ABI it implements. */
-#define MRG_ABI_VERSION 4
+ * tail_records_16, spec_agg, agg_path; 5 = mrg_stats gains map_kind, mrg_comm_count, mrg_pool_stats.
+ * mrg_version() names the ABI it implements. */
+#define MRG_ABI_VERSION 5
 
 const char *mrg_last_error(void);
 const char *mrg_version(void);

@@ -62,12 +62,28 @@ __global__ void k_fix_runs(SortRec *r, uint64_t n, KeySet ks, const uint8_t *hea
 }
 
 // ---------------------------------------------------------------- wc
-__global__ void k_wc_len(const SortRec *r, uint64_t n, KeySet ks, int drop_last, uint64_t *L) {
+// a record's key length and count: from the record itself when carried (mrg_launch_make_sortrec),
+// else gathered from the key set
+__device__ __forceinline__ void len_cnt(const SortRec &r, const KeySet &ks, int carried, uint32_t &len, uint64_t &c) {
+    if (carried) {
+        c = (uint64_t)r.doc | ((uint64_t)(r.pad >> 8) << 32);
+        len = r.pad & 0xFFu;
+        if (len > 16u) len = ks.len[r.idx];
+    } else {
+        len = ks.len[r.idx];
+        c = ks.cnt[r.idx];
+    }
+}
+
+__global__ void k_wc_len(const SortRec *r, uint64_t n, KeySet ks, int drop_last, int carried, uint64_t *L) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const bool last = (i + 1 == n) || r[i + 1].part != r[i].part;
-    const uint32_t e = r[i].idx;
-    L[i] = (drop_last && last) ? 0ull : (uint64_t)ks.len[e] + 2u + mrg_ndigits(ks.cnt[e]);
+    const SortRec x = r[i];
+    const bool last = (i + 1 == n) || r[i + 1].part != x.part;
+    uint32_t len;
+    uint64_t c;
+    len_cnt(x, ks, carried, len, c);
+    L[i] = (drop_last && last) ? 0ull : (uint64_t)len + 2u + mrg_ndigits(c);
 }
 
 __device__ __forceinline__ uint8_t *put_u64(uint8_t *o, uint64_t v, uint32_t nd) {
@@ -87,15 +103,17 @@ __device__ __forceinline__ uint8_t *put_u64(uint8_t *o, uint64_t v, uint32_t nd)
 }
 
 __global__ void k_wc_write(const SortRec *r, uint64_t n, KeySet ks, const uint8_t *heap, const uint64_t *L,
-                           const uint64_t *O, uint8_t *out) {
+                           const uint64_t *O, int carried, uint8_t *out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || L[i] == 0) return;
-    const uint32_t e = r[i].idx;
-    const uint32_t len = ks.len[e];  // read once: the byte stores below may alias any global pointer
-    const uint64_t c = ks.cnt[e];
+    const SortRec x = r[i];  // read once: the byte stores below may alias any global pointer
+    const uint32_t e = x.idx;
+    uint32_t len;
+    uint64_t c;
+    len_cnt(x, ks, carried, len, c);
     uint8_t *o = out + O[i];
     if (len <= 16u) {
-        const uint64_t k0 = r[i].k0, k1 = r[i].k1;
+        const uint64_t k0 = x.k0, k1 = x.k1;
         for (uint32_t b = 0; b < len; ++b) o[b] = (uint8_t)mrg_key_byte(k0, k1, b);
     } else {
         const uint8_t *src = heap + ks.hoff[e];
@@ -234,7 +252,7 @@ uint64_t mrg_format(const FormatArgs &f, DevPool &pool, uint8_t **out_buf, uint6
         uint64_t *L = (uint64_t *)pool.get(sizeof(uint64_t) * (n + 1));
         uint64_t *O = (uint64_t *)pool.get(sizeof(uint64_t) * (n + 1));
         if (n) {
-            hipLaunchKernelGGL(k_wc_len, grid_for(n), dim3(256), 0, s, recs, n, f.ks, f.drop_last, L);
+            hipLaunchKernelGGL(k_wc_len, grid_for(n), dim3(256), 0, s, recs, n, f.ks, f.drop_last, f.carried, L);
             mrg_scan_u64(L, O, n, scantmp, s);
         }
         hipLaunchKernelGGL(k_total, dim3(1), dim3(1), 0, s, L, O, n, total_d);
@@ -246,7 +264,8 @@ uint64_t mrg_format(const FormatArgs &f, DevPool &pool, uint8_t **out_buf, uint6
             *out_cap = bound;
             *out_buf = (uint8_t *)pool.get(*out_cap);
         }
-        if (n) hipLaunchKernelGGL(k_wc_write, grid_for(n), dim3(256), 0, s, recs, n, f.ks, f.heap, L, O, *out_buf);
+        if (n)
+            hipLaunchKernelGGL(k_wc_write, grid_for(n), dim3(256), 0, s, recs, n, f.ks, f.heap, L, O, f.carried, *out_buf);
         hipLaunchKernelGGL(k_part_off, grid_for(n + 1), dim3(256), 0, s, recs, O, n, R, (const uint64_t *)nullptr,
                            (const uint64_t *)total_d, part_off);
         hipMemcpyAsync(&total, total_d, sizeof total, hipMemcpyDeviceToHost, s);

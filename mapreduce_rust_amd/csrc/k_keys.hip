@@ -871,7 +871,11 @@ __global__ __launch_bounds__(EXP_WG) void k_export_pack(KeySet ks, const uint8_t
     }
 }
 
-__global__ void k_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, SortRec *out) {
+// carry (wc): the key's count and length ride in the record (doc = count bits 0..31, pad = length
+// (0xFF: a long key, length in the key set) | count bits 32..55 << 8), so the formatter reads each
+// sorted record once instead of gathering len / cnt from the key set twice.  (wc keys are distinct:
+// doc only orders long keys with equal 16-byte prefixes, which k_fix_runs orders by full bytes.)
+__global__ void k_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, SortRec *out, int carry) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     SortRec r;
@@ -881,6 +885,12 @@ __global__ void k_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, 
     r.doc = doc_rank ? doc_rank[ks.doc[i]] : 0u;
     r.idx = (uint32_t)i;
     r.pad = 0;
+    if (carry) {
+        const uint64_t c = ks.cnt[i];
+        const uint32_t len = ks.len[i];
+        r.doc = (uint32_t)c;
+        r.pad = (len <= 16u ? len : 0xFFu) | ((uint32_t)(c >> 32) << 8);
+    }
     out[i] = r;
 }
 
@@ -969,9 +979,9 @@ void mrg_launch_export_pack(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t
     hipLaunchKernelGGL(k_export_pack, grid_for(n, EXP_WG), dim3(EXP_WG), 0, s, ks, heap, n, n_owners, rec_base,
                        heap_base, rec_cur, heap_cur, out, out_heap, indexer, vmax);
 }
-void mrg_launch_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, void *recs, hipStream_t s) {
+void mrg_launch_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, void *recs, hipStream_t s, bool carry) {
     if (!n) return;
-    hipLaunchKernelGGL(k_make_sortrec, grid_for(n), dim3(256), 0, s, ks, n, doc_rank, (SortRec *)recs);
+    hipLaunchKernelGGL(k_make_sortrec, grid_for(n), dim3(256), 0, s, ks, n, doc_rank, (SortRec *)recs, carry ? 1 : 0);
 }
 void mrg_launch_wide_counts(const BucketArgs &a, uint64_t *cnt, uint64_t nseg, hipStream_t s) {
     hipLaunchKernelGGL(k_wide_counts, grid_for(nseg), dim3(256), 0, s, a, cnt);

@@ -38,6 +38,7 @@
 // workgroup's flush region.
 #include "mrg_device.h"
 #include "mrg_internal.h"
+#include "mrg_split.h"
 
 namespace {
 
@@ -347,7 +348,47 @@ struct TailRegions {
     unsigned long long *cur16;  // wc keys of 13..16 bytes: their own regions of 16-byte records
     const unsigned long long *end16;
     unsigned int *lcnt;         // long-token records of this workgroup so far (its region's cursor)
+    // wide map: cursors of this workgroup's L1-bucket regions and the splitters (LDS)
+    unsigned int *wcur;
+    const uint64_t *wspl;
+    const uint8_t *wix;
 };
+
+// Wide map: the L1 bucket of a short key (partition = SipHash-1-3 % R, worker.rs:111-115, 129; then
+// the number of the partition's splitters <= key, through the LDS index when there is one)
+__device__ __forceinline__ uint32_t wide_bucket(const MapArgs &A, const TailRegions &R, uint64_t k0, uint64_t k1) {
+    const uint32_t r = part_of(k0, k1, A.wR);
+    const uint32_t m = A.wB1r - 1u;
+    if (m == 0u) return r;
+    const uint64_t *sp = R.wspl + 2ull * r * m;
+    uint32_t q;
+    if (R.wix) {
+        const uint8_t *ixr = R.wix + r * MRG_WIDE_IX1;
+        const SplitIndex<8, uint8_t> li{sp, ixr, m, ixr[257]};
+        q = li.upper(k0, k1);
+    } else {
+        uint32_t lo = 0, hi = m;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (key_lt(k0, k1, sp[2 * mid], sp[2 * mid + 1])) hi = mid;
+            else lo = mid + 1;
+        }
+        q = lo;
+    }
+    return r * A.wB1r + q;
+}
+
+// Wide map: append short key (k0, k1) to its L1 bucket's region of this workgroup (an LDS cursor per
+// bucket; the count goes on past the region's capacity so the host can size a rerun)
+__device__ __forceinline__ void wide_store(const MapArgs &A, const TailRegions &R, bool act, uint64_t k0, uint64_t k1) {
+    if (!act) return;
+    const uint32_t b = wide_bucket(A, R, k0, k1);
+    const uint32_t pos = atomicAdd(&R.wcur[b], 1u);
+    if (pos < A.wcap) {
+        const uint64_t i = ((uint64_t)b * gridDim.x + blockIdx.x) * A.wcap + pos;
+        *reinterpret_cast<GAS u64x2 *>(gp(A.wrec) + 2u * i) = u64x2{k0, k1};
+    }
+}
 typedef uint32_t u32x3a __attribute__((ext_vector_type(3), aligned(4)));  // one 12-byte tail record
 
 // wc tail record i: keys of <= 12 bytes as 12 bytes {k0, high word of k1} in pool, longer ones as
@@ -469,11 +510,14 @@ __device__ __forceinline__ void emit_fastN(const MapArgs &A, uint32_t abl, uint3
 // One round of token emission by a whole wave (all 64 lanes call it): LDS-table insert of short
 // keys; a miss is appended to its hash bucket's region of this workgroup (an LDS counter per
 // bucket, no HBM atomics).  Long keys become long-token records.
-template <int CAP, bool IDX>
+template <int CAP, bool IDX, bool WIDE>
 __device__ __forceinline__ void emit(const MapArgs &A, LdsTable<CAP, IDX> &table, TailRegions R, bool have,
                                      uint64_t tk0, uint64_t tk1, uint32_t tlen, uint64_t tstart, uint32_t traw,
                                      uint32_t docid) {
     const bool is_long = have && tlen > 16u;
+    if constexpr (WIDE) {
+        wide_store(A, R, have && !is_long, tk0, tk1);
+    } else {
     bool tail = false;
     uint32_t h = 0;
     const uint32_t dkey = IDX ? docid : MRG_EMPTY_DOC;
@@ -502,6 +546,7 @@ __device__ __forceinline__ void emit(const MapArgs &A, LdsTable<CAP, IDX> &table
                 g_add(&A.counters[CNT_OVF], 1ull);
             }
         }
+    }
     }
     // long tokens: the workgroup's own region through an LDS cursor (one LDS atomic per wave).  Until
     // r04 every such wave took its slots from ONE device-wide counter: a returning atomic on a single
@@ -535,7 +580,7 @@ __device__ __forceinline__ void emit(const MapArgs &A, LdsTable<CAP, IDX> &table
 // decode + two-level class table), one token per lane per emission round.  Called after the main
 // loop (the main loop only records which tiles need it), so its registers never add to the hot
 // loop's.
-template <int CAP, bool IDX>
+template <int CAP, bool IDX, bool WIDE>
 __device__ __forceinline__ uint32_t generic_tile(const MapArgs &A, LdsTable<CAP, IDX> table, TailRegions R,
                                               const uint8_t *win, uint64_t At, uint64_t t0, uint64_t t1,
                                               uint64_t doc_lo, uint64_t doc_hi, uint64_t wlo, uint64_t whi,
@@ -601,7 +646,7 @@ __device__ __forceinline__ uint32_t generic_tile(const MapArgs &A, LdsTable<CAP,
             }
             if (!__any(have)) break;
             my_tokens += have ? 1u : 0u;
-            emit(A, table, R, have, tk0, tk1, tlen, tstart, traw, docid);
+            emit<CAP, IDX, WIDE>(A, table, R, have, tk0, tk1, tlen, tstart, traw, docid);
         }
     return my_tokens;
 }
@@ -617,7 +662,7 @@ __device__ __forceinline__ uint32_t uni_class(const LDS uint8_t *uc, uint32_t cp
     else return mrg_uclass(cp);
     return (byte >> (2u * (cp & 3u))) & 3u;
 }
-template <int CAP, bool IDX>
+template <int CAP, bool IDX, bool WIDE>
 __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // the arguments live in device memory (not the kernarg segment): fields are loaded where they
     // are used instead of being held in SGPRs for the whole kernel
@@ -636,14 +681,18 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // v_perm selectors per (key length, 1-byte gap position; 16 = none) over the r-aligned window
     __shared__ __attribute__((aligned(16))) uint32_t s_sel[17 * 17][4];
     // workgroup: combine table + tail-region cursors
-    __shared__ KeyPair s_key[CAP];
-    __shared__ unsigned int s_cnt[CAP];
+    // (the wide map has no table and no tail regions: their LDS holds its bucket cursors and splitters)
+    __shared__ KeyPair s_key[WIDE ? 2 : CAP];
+    __shared__ unsigned int s_cnt[WIDE ? 2 : CAP];
     __shared__ __attribute__((aligned(16))) unsigned int s_doc[IDX ? CAP : 1];
-    __shared__ unsigned long long s_tcur[MRG_NBUCKET];  // next pool record of (bucket, this WG)
-    __shared__ unsigned long long s_tend[MRG_NBUCKET];  // end of that region
-    __shared__ unsigned long long s_tcur16[IDX ? 1 : MRG_NBUCKET];  // wc: the 16-byte regions
-    __shared__ unsigned long long s_tend16[IDX ? 1 : MRG_NBUCKET];
-    __shared__ uint32_t s_hist[MRG_NBUCKET + 1];
+    __shared__ unsigned long long s_tcur[WIDE ? 1 : MRG_NBUCKET];  // next pool record of (bucket, this WG)
+    __shared__ unsigned long long s_tend[WIDE ? 1 : MRG_NBUCKET];  // end of that region
+    __shared__ unsigned long long s_tcur16[(IDX || WIDE) ? 1 : MRG_NBUCKET];  // wc: the 16-byte regions
+    __shared__ unsigned long long s_tend16[(IDX || WIDE) ? 1 : MRG_NBUCKET];
+    __shared__ uint32_t s_hist[WIDE ? 1 : MRG_NBUCKET + 1];
+    __shared__ unsigned int s_wcur[WIDE ? MRG_WMAP_MAXB1 : 1];                  // wide: records per L1 bucket
+    __shared__ __attribute__((aligned(16))) uint64_t s_wspl[WIDE ? 2 * MRG_WMAP_MAXB1 : 1];  // its splitters
+    __shared__ __attribute__((aligned(4))) uint8_t s_wix[WIDE ? MRG_WMAP_IXR * MRG_WIDE_IX1 : 4];
     __shared__ uint32_t s_next, s_ngen;                  // next block of the workgroup's share; list length
     __shared__ uint32_t s_nuni;                          // non-ASCII tiles tokenized with UTF-8-exact masks
     // the class table's blocks for U+0000..U+07FF (2-byte codepoints: Latin-1, Latin Extended, Greek,
@@ -653,21 +702,29 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ uint32_t s_tot[3];                        // workgroup totals: tokens, tail records, 16-byte ones
     __shared__ unsigned int s_fill;                      // table slots claimed
     __shared__ unsigned int s_lcnt;                      // long-token records (region cursor)
-    __shared__ unsigned int s_door[MRG_MAP_DOOR ? LdsTable<CAP, IDX>::DW : 1];  // admission bitmap
-    static_assert(sizeof(s_q) >= CAP * sizeof(uint16_t), "flush ranks reuse the queues");
+    __shared__ unsigned int s_door[(MRG_MAP_DOOR && !WIDE) ? LdsTable<CAP, IDX>::DW : 1];  // admission bitmap
+    static_assert(WIDE || sizeof(s_q) >= CAP * sizeof(uint16_t), "flush ranks reuse the queues");
 
     const int tid = threadIdx.x;
     // wave index through readfirstlane: the compiler then knows everything derived from it (tile
     // index, document bounds) is wave-uniform and keeps it in SGPRs
     const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (int i = tid; i < CAP; i += WG) {
+    if constexpr (WIDE) {
+        const uint32_t nb1 = A.wR * A.wB1r, nsp = 2u * A.wR * (A.wB1r - 1u);
+        for (uint32_t b = tid; b < nb1; b += WG) s_wcur[b] = 0;
+        for (uint32_t i = tid; i < nsp; i += WG) s_wspl[i] = gp(A.wspl)[i];
+        if (A.wix)
+            for (uint32_t i = tid; i < A.wR * (MRG_WIDE_IX1 / 4); i += WG)
+                reinterpret_cast<uint32_t *>(s_wix)[i] = gp(reinterpret_cast<const uint32_t *>(A.wix))[i];
+    }
+    for (int i = tid; i < (WIDE ? 2 : CAP); i += WG) {
         s_key[i] = KeyPair{MRG_EMPTY_K0, MRG_EMPTY_K1};
         s_cnt[i] = 0;
         if (IDX) s_doc[i] = MRG_EMPTY_DOC;
     }
-    if (MRG_MAP_DOOR)
+    if (MRG_MAP_DOOR && !WIDE)
         for (int i = tid; i < (int)LdsTable<CAP, IDX>::DW; i += WG) s_door[i] = 0;
-    for (int b = tid; b < MRG_NBUCKET; b += WG) {
+    for (int b = tid; b < (WIDE ? 0 : MRG_NBUCKET); b += WG) {
         const uint32_t cap = gp(A.bcap)[b];
         const uint64_t base = gp(A.rbase)[b] + (uint64_t)blockIdx.x * cap;
         s_tcur[b] = base;
@@ -711,7 +768,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         s_sel[L * 17u + g][j] = ((0x00010203u + (gm & 0x01010101u)) & ~zm) | (0x0C0C0C0Cu & zm);
     }
     LdsTable<CAP, IDX> table{s_key, s_cnt, s_doc, s_door, &s_fill};
-    const TailRegions tails{s_tcur, s_tend, s_tcur16, s_tend16, &s_lcnt};
+    const TailRegions tails{s_tcur, s_tend, s_tcur16, s_tend16, &s_lcnt, s_wcur, s_wspl, A.wix ? s_wix : nullptr};
     uint32_t my_tokens = 0;
     // uniform job parameters used in the hot loop, read once
     // ablation knobs (MRG_ABLATE, timing only) exist in -DMRG_MAP_ABLATION builds; in the product
@@ -984,7 +1041,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         // carries its class, so the W / S masks mean the same.  Invalid UTF-8 defers the block's tiles
         // to generic_tile after the main loop (which reports the first bad byte).
         bool defer_blk = false;
-        if (__any(n0 || n1 || (lane <= 1 && ne))) {
+        if (!(abl & 256u) && __any(n0 || n1 || (lane <= 1 && ne))) {
 #ifdef MRG_MAP_NO_UNI
             defer_blk = true;  // A/B builds only: every such block to the exact walker, as in r03
 #else
@@ -1215,7 +1272,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 const uint32_t ra = queue[min(qa, (uint32_t)QCAP - 1u)], rb = queue[min(qb, (uint32_t)QCAP - 1u)];
                 uint32_t ga = extract(qa, ra, total, fa, sa, sA, a0, a1);
                 uint32_t gb = extract(qb, rb, total, fb, sb, sB, b0, b1);
-                if (__any((ga | gb) != 0u)) {
+                if (!(abl & 1024u) && __any((ga | gb) != 0u)) {
                     squeeze(ga, a0, a1);
                     squeeze(gb, b0, b1);
                 }
@@ -1234,13 +1291,18 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 my_tokens += (fa ? 1u : 0u) + (fb ? 1u : 0u);
                 const bool hv[2] = {fa, fb};
                 const uint64_t kk0[2] = {a0, b0}, kk1[2] = {a1, b1};
-                emit_fastN<2>(A, abl, hbits, table, tails, pool, pool16, hv, kk0, kk1, docid, may_claim);
+                if constexpr (WIDE) {
+                    wide_store(A, tails, fa, a0, a1);
+                    wide_store(A, tails, fb, b0, b1);
+                } else {
+                    emit_fastN<2>(A, abl, hbits, table, tails, pool, pool16, hv, kk0, kk1, docid, may_claim);
+                }
             }
             // deferred slow tokens, one per lane: through the tile's masks, or (a token running past
             // the first halo segment) the exact per-codepoint walker (forward reads only: the staged
             // bytes are [At, whi))
             MRG_PT(3);
-            if (nslow) {
+            if (nslow && !(abl & 512u)) {
                 wave_sync_lds();
                 auto rd = [&](uint64_t a) -> uint32_t {
                     if (a >= At && a < whi) return (uint32_t)win[a - wbase];
@@ -1265,7 +1327,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                         }
                     }
                     my_tokens += have ? 1u : 0u;
-                    emit(A, table, tails, have, tk0, tk1, tlen, a, traw, docid);
+                    emit<CAP, IDX, WIDE>(A, table, tails, have, tk0, tk1, tlen, a, traw, docid);
                 }
             }
         }
@@ -1330,7 +1392,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 if (j0 >= T.v0 && j0 < T.v1) reinterpret_cast<uint4 *>(win)[j0] = x0;
                 if (has1 && j1 >= T.v0 && j1 < T.v1) reinterpret_cast<uint4 *>(win)[j1] = x1;
                 wave_sync_lds();
-                my_tokens += generic_tile<CAP, IDX>(A, table, tails, win, T.At, T.t0, T.t1,
+                my_tokens += generic_tile<CAP, IDX, WIDE>(A, table, tails, win, T.At, T.t0, T.t1,
                                                     T.doc_lo, T.doc_hi, T.wlo, T.whi, T.docid);
             }
         }
@@ -1339,9 +1401,19 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     MRG_PT(5);
     // ---- flush the LDS table into this workgroup's region, sorted by bucket
     __syncthreads();
+    uint32_t my_tail = 0, my_tail16 = 0;
+    if constexpr (WIDE) {  // the wide map: records per L1 bucket; a region past its capacity -> rerun
+        uint32_t over = 0;
+        for (uint32_t b = tid; b < A.wR * A.wB1r; b += WG) {
+            const uint32_t n = s_wcur[b];
+            gp(A.wcnt)[(uint64_t)b * gridDim.x + blockIdx.x] = n;
+            my_tail += n;
+            over += n > A.wcap ? n - A.wcap : 0u;
+        }
+        if (over) g_add(&A.counters[CNT_OVF], (unsigned long long)over);
+    } else {
     uint16_t *s_rank = &s_q[0][0];
     GAS uint32_t *bcount = gp(A.bcount) + (uint64_t)blockIdx.x * MRG_NBUCKET;
-    uint32_t my_tail = 0, my_tail16 = 0;
     for (int b = tid; b < MRG_NBUCKET; b += WG) {  // appends made (may exceed the capacity)
         const uint32_t n = (uint32_t)(s_tcur[b] - (s_tend[b] - gp(A.bcap)[b]));
         my_tail += n;
@@ -1386,6 +1458,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         gp(A.fk1)[pos2] = k.b;
         gp(A.fcnt)[pos2] = s_cnt[i];
         if (IDX) gp(A.fdoc)[pos2] = d;
+    }
     }
     // token and tail totals: waves -> LDS -> one device atomic per workgroup and counter (a wave
     // atomic each put 8 K atomics on two counters at the very end of the launch)
@@ -1511,9 +1584,9 @@ void mrg_launch_long_compact(const MapArgs &A, int grid, uint64_t *start, uint32
                        A.lper, A.lovf, A.counters, (uint32_t)grid, start, len, doc);
 }
 
-template <int CAP, bool IDX>
+template <int CAP, bool IDX, bool WIDE = false>
 static void launch_map_t(const MapArgs *a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((k_map<CAP, IDX>), dim3(grid), dim3(WG), 0, s, a);
+    hipLaunchKernelGGL((k_map<CAP, IDX, WIDE>), dim3(grid), dim3(WG), 0, s, a);
 }
 
 static int map_cap_for(int app, int lds_cap) {
@@ -1521,9 +1594,13 @@ static int map_cap_for(int app, int lds_cap) {
     return lds_cap >= 4096 ? 4096 : 2048;
 }
 
-void mrg_launch_map(const MapArgs *h, MapArgs *a, int app, int grid, int lds_cap, hipStream_t s) {
+void mrg_launch_map(const MapArgs *h, MapArgs *a, int app, int grid, int lds_cap, hipStream_t s, bool wide) {
     const bool idx = app == 1;
     if (h) (void)hipMemcpyAsync(a, h, sizeof(MapArgs), hipMemcpyHostToDevice, s);
+    if (wide && !idx) {  // the wide map (no LDS table): one layout whatever lds_cap
+        launch_map_t<2048, false, true>(a, grid, s);
+        return;
+    }
     if (map_cap_for(app, lds_cap) == 4096) {
         if (idx) launch_map_t<4096, true>(a, grid, s);
         else launch_map_t<4096, false>(a, grid, s);
@@ -1547,10 +1624,10 @@ int mrg_map_max_grid(int app, int lds_cap, int device) {
     int per = 1;
     hipError_t e;
     if (map_cap_for(app, lds_cap) == 4096)
-        e = app == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<4096, true>, WG, 0)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<4096, false>, WG, 0);
-    else if (app == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<2048, true>, WG, 0);
-    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<2048, false>, WG, 0);
+        e = app == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<4096, true, false>, WG, 0)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<4096, false, false>, WG, 0);
+    else if (app == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<2048, true, false>, WG, 0);
+    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_map<2048, false, false>, WG, 0);
     if (e != hipSuccess || per < 1) per = 1;
     return ncu * per;
 }

@@ -22,6 +22,7 @@
 // Order within a leaf: (k0, k1) unsigned = key bytes (mrg_device.h), one partition per L1 bucket.
 #include "mrg_device.h"
 #include "mrg_internal.h"
+#include "mrg_split.h"
 
 namespace {
 
@@ -40,6 +41,7 @@ constexpr int W_LNW = W_LWG / 64;
 constexpr uint32_t W_SLOTS = 1024;    // leaf LDS table slots
 constexpr uint32_t W_MAXD = 768;      // distinct keys a leaf may hold (75 % load)
 constexpr uint32_t W_SEGLDS = 2048;   // segment offsets cached in LDS per L1 tile
+constexpr uint32_t W_MAXSEG = 512;    // segmented L2: map workgroups (segments per bucket) at most
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() also makes every wave wait for its
 // outstanding global stores (vmcnt(0)) -- a store's full round trip at each of the many barriers of a
@@ -48,64 +50,6 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-__device__ __forceinline__ bool key_lt(uint64_t a0, uint64_t a1, uint64_t b0, uint64_t b1) {
-    return a0 < b0 || (a0 == b0 && a1 < b1);
-}
-
-// The 64 key bits from bit h on (bit 0 = the most significant bit of k0), zero past bit 127.
-__device__ __forceinline__ uint64_t key_bits_from(uint64_t k0, uint64_t k1, uint32_t h) {
-    return h == 0 ? k0 : (h < 64 ? (k0 << h) | (k1 >> (64 - h)) : k1 << (h - 64));
-}
-// leading bits two keys share (128 if equal)
-__device__ __forceinline__ uint32_t common_bits(uint64_t a0, uint64_t a1, uint64_t b0, uint64_t b1) {
-    const uint64_t x0 = a0 ^ b0, x1 = a1 ^ b1;
-    return x0 ? (uint32_t)__builtin_clzll(x0) : (x1 ? 64u + (uint32_t)__builtin_clzll(x1) : 128u);
-}
-
-// Splitter index: m sorted splitters share their top cp bits; the next IB bits of a key select
-// ix[v] .. ix[v + 1], the splitters carrying those same bits, so a lookup compares the key with
-// that handful (usually 0-2) instead of walking log2(m) levels of 16-byte LDS reads.  A key whose
-// top cp bits differ from the splitters' lies below all of them or above all of them.
-template <uint32_t IB, class IX>
-struct SplitIndex {
-    const uint64_t *spl;  // m (k0, k1) pairs in LDS
-    const IX *ix;         // [2^IB + 1] in LDS
-    uint32_t m, cp;
-    __device__ __forceinline__ static uint32_t slot(uint64_t k0, uint64_t k1, uint32_t cp) {
-        return (uint32_t)(key_bits_from(k0, k1, cp) >> (64 - IB));
-    }
-    __device__ __forceinline__ static uint32_t prefix_bits(const uint64_t *spl, uint32_t m) {
-        return min(common_bits(spl[0], spl[1], spl[2 * (m - 1)], spl[2 * (m - 1) + 1]), 128u - IB);
-    }
-    // the index of m >= 1 splitters, by threads tid, tid + nt, ... (the caller synchronises)
-    __device__ __forceinline__ static void build(const uint64_t *spl, uint32_t m, IX *ix, uint32_t tid, uint32_t nt) {
-        const uint32_t cp = prefix_bits(spl, m);
-        for (uint32_t v = tid; v <= (1u << IB); v += nt) {  // first splitter whose slot is >= v
-            uint32_t lo = 0, hi = m;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (slot(spl[2 * mid], spl[2 * mid + 1], cp) < v) lo = mid + 1;
-                else hi = mid;
-            }
-            ix[v] = (IX)lo;
-        }
-    }
-    // number of splitters <= key (m >= 1)
-    __device__ __forceinline__ uint32_t upper(uint64_t k0, uint64_t k1) const {
-        const uint64_t p0 = spl[0], p1 = spl[1];
-        if (common_bits(k0, k1, p0, p1) < cp) return key_lt(k0, k1, p0, p1) ? 0u : m;
-        const uint32_t v = slot(k0, k1, cp);
-        uint32_t lo = ix[v], hi = ix[v + 1];
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (key_lt(k0, k1, spl[2 * mid], spl[2 * mid + 1])) hi = mid;
-            else lo = mid + 1;
-        }
-        return lo;
-    }
-};
-typedef SplitIndex<12, uint16_t> LeafIndex;   // L2: <= 1023 leaf splitters per L1 bucket
-typedef SplitIndex<8, uint8_t> L1Index;       // L1: <= 63 splitters per partition
 
 // ---------------------------------------------------------------- the map's records (count 1)
 // main segments: the tail regions of 12-byte records (bucket-major, map workgroup minor), the
@@ -157,11 +101,6 @@ __device__ __forceinline__ uint64_t seg_find(const OFF &off, uint64_t lo, uint64
     return lo;
 }
 
-__device__ __forceinline__ uint32_t part_of(uint64_t k0, uint64_t k1, uint32_t R) {
-    const uint64_t h = mrg_siphash_short(k0, k1, mrg_short_len(k0, k1));
-    if ((R & (R - 1u)) == 0u) return (uint32_t)h & (R - 1u);   // uniform: no 64-bit division
-    return (uint32_t)(h % (uint64_t)R);
-}
 
 // number of splitters <= key among sp[0 .. m)
 template <class SP>
@@ -259,6 +198,73 @@ __global__ void k_wsplit1(const SortRec *smp, uint32_t S, uint32_t R, uint32_t B
     spl[2ull * t + 1] = b;
 }
 
+// ---------------------------------------------------------------- wide map: input sample, regions
+// Sample j of S from the input text, for the wide map's L1 splitters and its near-unique test: the
+// first token after byte (2j + 1) * total / 2S of the documents.  The key is approximated on ASCII
+// classes (bytes >= 0x80 count as word bytes, ASCII punctuation is dropped, the first 16 key bytes):
+// splitters only steer bucket sizes, so any key-ordered value is a valid one (exactness comes from
+// the map itself).
+__global__ void k_wsample_text(const uint8_t *in, const uint64_t *doc_off, uint32_t n_docs, uint64_t total,
+                               uint32_t S, uint32_t R, SortRec *out) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= S) return;
+    const uint64_t g = ((2ull * j + 1ull) * total) / (2ull * S);
+    uint32_t lo = 0, hi = n_docs;  // doc_off[lo] - doc_off[0] <= g < ...
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (doc_off[mid] - doc_off[0] <= g) lo = mid;
+        else hi = mid;
+    }
+    const uint64_t dhi = doc_off[lo + 1];
+    uint64_t p = doc_off[0] + g;
+    auto cls = [](uint32_t c) -> uint32_t {  // 0 space, 1 word byte, 2 other (deleted)
+        if (c >= 0x80u) return 1u;
+        const uint32_t k = mrg_uclass(c);
+        return k == MRG_CLS_S ? 0u : (k == MRG_CLS_W ? 1u : 2u);
+    };
+    for (int k = 0; k < 64 && p < dhi && cls(in[p]) != 0u; ++k) ++p;  // the rest of the current token
+    for (int k = 0; k < 64 && p < dhi && cls(in[p]) == 0u; ++k) ++p;  // the separator
+    uint64_t k0 = 0, k1 = 0;
+    uint32_t L = 0;
+    for (int k = 0; k < 64 && p < dhi && L < 16u; ++k, ++p) {
+        const uint32_t c = in[p], t = cls(c);
+        if (t == 0u) break;
+        if (t == 1u) mrg_key_append(k0, k1, L++, c);
+    }
+    SortRec r;
+    r.k0 = k0;
+    r.k1 = k1;
+    r.part = L ? part_of(k0, k1, R) : 0u;
+    r.doc = 0;
+    r.idx = j;
+    r.pad = 0;
+    out[j] = r;
+}
+
+// sorted samples: adjacent equal keys (the near-unique test)
+__global__ void k_wsample_dups(const SortRec *r, uint32_t S, unsigned long long *dups) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool d = j > 0 && j < S && r[j].part == r[j - 1].part && r[j].k0 == r[j - 1].k0 && r[j].k1 == r[j - 1].k1;
+    const uint64_t m = __ballot(d);
+    if ((threadIdx.x & 63u) == 0 && m) atomicAdd(dups, (unsigned long long)__popcll(m));
+}
+
+// wide map regions of bucket b (one thread block): segment starts soff[b][w] (bucket-relative, the
+// records a region holds: its count clipped to the capacity) and the bucket's total in nb[b]
+__global__ void k_wmap_seg(const uint32_t *wcnt, uint32_t grid, uint32_t wcap, uint32_t *soff, uint64_t *nb) {
+    const uint32_t b = blockIdx.x;
+    if (threadIdx.x != 0) return;
+    uint32_t run = 0;
+    const uint32_t *c = wcnt + (uint64_t)b * grid;
+    uint32_t *so = soff + (uint64_t)b * (grid + 1u);
+    for (uint32_t w = 0; w < grid; ++w) {
+        so[w] = run;
+        run += min(c[w], wcap);
+    }
+    so[grid] = run;
+    nb[b] = run;
+}
+
 struct L1Args {
     BucketArgs A;
     const uint64_t *off;     // main segment offsets [nseg + 1]
@@ -273,7 +279,7 @@ struct L1Args {
 };
 
 // L1 splitter index of partition r: 257 entries, then the prefix bit count (L1Index)
-constexpr uint32_t W_IX1 = 260;
+constexpr uint32_t W_IX1 = MRG_WIDE_IX1;
 __global__ void k_wl1ix(const uint64_t *spl1, uint32_t m, uint8_t *ix1) {
     const uint32_t r = blockIdx.x;
     const uint64_t *sp = spl1 + 2ull * r * m;
@@ -423,8 +429,26 @@ struct L2Args {
     uint64_t *leaf_lo;       // [B1 * MAXB2 + 1] first record of each leaf (absolute)
     uint64_t *leaf_lb;       // [B1 * MAXB2][2] lower key bound of each leaf
     uint16_t *sub;           // [n] leaf (inside its L1 bucket) of each record: histogram pass -> scatter
+    // segmented input (the wide map's regions): L1 bucket b's records are segments w < grid, segment w =
+    // rin records [(b * grid + w) * wcap, + its count), at bucket-relative offsets soff[b * (grid + 1) + w]
+    const uint64_t *rin;
+    const uint32_t *soff;
+    uint32_t grid, wcap;
 };
 
+// Segmented input: record i (bucket-relative) of bucket b, through its segment (binary search)
+__device__ __forceinline__ const GASW uint64_t *seg_record(const L2Args &L, uint32_t b, const uint32_t *so,
+                                                           uint64_t i) {
+    uint32_t lo = 0, hi = L.grid;  // so[lo] <= i < so[hi]
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (so[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    return gw(L.rin) + 2ull * (((uint64_t)b * L.grid + lo) * L.wcap + (i - so[lo]));
+}
+
+template <bool SEG>
 __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     __shared__ uint64_t s_smp[2 * W_S2];            // samples (k0, k1), bitonic-sorted
     __shared__ uint64_t s_spl[2 * MRG_WIDE_MAXB2];  // (one spare pair: the scatter's leaf ids fill it all)
@@ -434,7 +458,12 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     static_assert(W_SC * sizeof(uint64_t) * 2 <= sizeof(s_smp) && W_SC * sizeof(uint16_t) <= sizeof(s_spl),
                   "the scatter's stage fits the sample and splitter arrays");
     __shared__ uint32_t s_ws[W_NW];
+    __shared__ uint32_t s_cseg[SEG ? W_MAXSEG + 1 : 1];   // SEG: the bucket's segment starts
     const uint32_t tid = threadIdx.x, b = blockIdx.x;
+    if (SEG) {
+        for (uint32_t w = tid; w <= L.grid; w += W_WG) s_cseg[w] = L.soff[(uint64_t)b * (L.grid + 1u) + w];
+        lds_barrier();
+    }
     const uint64_t base = L.bstart[b], nb = L.bstart[b + 1] - base;
     uint32_t B2 = (uint32_t)min<uint64_t>((nb + L.target - 1) / L.target, MRG_WIDE_MAXB2);
     if (B2 < 1) B2 = 1;
@@ -448,8 +477,9 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
             uint64_t a = ~0ull, c = ~0ull;  // padding sorts last
             if (k < S) {
                 const uint64_t i = ((2ull * k + 1ull) * nb) / (2ull * S);
-                a = in[2 * i];
-                c = in[2 * i + 1];
+                const GASW uint64_t *x = SEG ? seg_record(L, b, s_cseg, i) : in + 2 * i;
+                a = x[0];
+                c = x[1];
             }
             s_smp[2 * k] = a;
             s_smp[2 * k + 1] = c;
@@ -491,17 +521,38 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     constexpr int U = 4;
     typedef uint64_t v2 __attribute__((ext_vector_type(2)));
     const GASW v2 *inv = reinterpret_cast<const GASW v2 *>(in);
-    for (uint64_t i0 = tid; i0 < nb; i0 += (uint64_t)U * W_WG) {
-        v2 x[U];
+    if (SEG) {  // segment by segment, one wave each: reads stay inside a segment
+        const uint32_t *so = s_cseg;
+        const uint32_t lane = tid & 63u;
+        for (uint32_t w = tid >> 6; w < L.grid; w += W_NW) {
+            const uint32_t o = so[w], nw = so[w + 1] - o;
+            const GASW v2 *sv = reinterpret_cast<const GASW v2 *>(gw(L.rin) + 2ull * (((uint64_t)b * L.grid + w) * L.wcap));
+            for (uint32_t j0 = lane; j0 < nw; j0 += (uint32_t)U * 64u) {
+                v2 x[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = inv[min(i0 + (uint64_t)u * W_WG, (uint64_t)(nb - 1u))];
+                for (int u = 0; u < U; ++u) x[u] = sv[min(j0 + (uint32_t)u * 64u, nw - 1u)];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (i0 + (uint64_t)u * W_WG < nb) {
-                const uint32_t j = sub_of(x[u].x, x[u].y);
-                atomicAdd(&s_cnt[j], 1u);
-                gw(L.sub)[base + i0 + (uint64_t)u * W_WG] = (uint16_t)j;
+                for (int u = 0; u < U; ++u)
+                    if (j0 + (uint32_t)u * 64u < nw) {
+                        const uint32_t j = sub_of(x[u].x, x[u].y);
+                        atomicAdd(&s_cnt[j], 1u);
+                        gw(L.sub)[base + o + j0 + (uint64_t)u * 64u] = (uint16_t)j;
+                    }
             }
+        }
+    } else {
+        for (uint64_t i0 = tid; i0 < nb; i0 += (uint64_t)U * W_WG) {
+            v2 x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = inv[min(i0 + (uint64_t)u * W_WG, (uint64_t)(nb - 1u))];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (i0 + (uint64_t)u * W_WG < nb) {
+                    const uint32_t j = sub_of(x[u].x, x[u].y);
+                    atomicAdd(&s_cnt[j], 1u);
+                    gw(L.sub)[base + i0 + (uint64_t)u * W_WG] = (uint16_t)j;
+                }
+        }
     }
     lds_barrier();
     {  // exclusive scan of the B2 <= 1024 counts, one per thread
@@ -542,11 +593,30 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         const uint32_t nc = (uint32_t)min<uint64_t>(W_SC, nb - c0);
         v2 x[SU];
         uint32_t j[SU], r[SU];
+        // SEG: each thread finds its first record's segment by a search over the bucket's segment starts
+        // (s_cseg, LDS), then walks forward (its records are W_WG apart; segments hold ~1 K records)
+        uint32_t sw = 0;
+        if (SEG) {
+            const uint64_t q0 = c0 + min(tid, nc - 1u);
+            uint32_t lo = 0, hi = L.grid;  // s_cseg[lo] <= q0 < s_cseg[hi]
+            while (hi - lo > 1u) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_cseg[mid] <= q0) lo = mid;
+                else hi = mid;
+            }
+            sw = lo;
+        }
 #pragma unroll
         for (uint32_t u = 0; u < SU; ++u) {
             const uint32_t p = tid + u * W_WG;
             const uint64_t i = c0 + min(p, nc - 1u);
-            x[u] = inv[i];
+            if (SEG) {
+                while (s_cseg[sw + 1] <= i) ++sw;
+                x[u] = *reinterpret_cast<const GASW v2 *>(gw(L.rin) + 2ull * (((uint64_t)b * L.grid + sw) * L.wcap +
+                                                                              (i - s_cseg[sw])));
+            } else {
+                x[u] = inv[i];
+            }
             j[u] = gw(L.sub)[base + i];   // the histogram pass's leaf: no second splitter search
         }
         if (tid < B2) s_cnt[tid] = 0;
@@ -1871,9 +1941,11 @@ void mrg_wide_launch_bstart(const uint32_t *cnt, uint32_t B1, uint32_t ntiles, u
 }
 void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstart, const uint64_t *spl1, uint32_t B1,
                         uint32_t B1r, uint32_t target, uint32_t *nleaf, uint64_t *leaf_lo, uint64_t *leaf_lb,
-                        uint16_t *sub, hipStream_t s) {
-    L2Args L{in, out, bstart, spl1, B1r, target, nleaf, leaf_lo, leaf_lb, sub};
-    hipLaunchKernelGGL(k_wl2, dim3(B1), dim3(W_WG), 0, s, L);
+                        uint16_t *sub, hipStream_t s, const uint64_t *rin, const uint32_t *soff, uint32_t grid,
+                        uint32_t wcap) {
+    L2Args L{in, out, bstart, spl1, B1r, target, nleaf, leaf_lo, leaf_lb, sub, rin, soff, grid, wcap};
+    if (rin) hipLaunchKernelGGL(k_wl2<true>, dim3(B1), dim3(W_WG), 0, s, L);
+    else hipLaunchKernelGGL(k_wl2<false>, dim3(B1), dim3(W_WG), 0, s, L);
 }
 void mrg_wide_launch_weights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *wk0, uint64_t *wk1, uint64_t *wcnt,
                              uint32_t *wpart, hipStream_t s) {
@@ -1955,4 +2027,20 @@ void mrg_wide_launch_dense(const uint64_t *keys, const uint64_t *ocnt, const uin
                            hipStream_t s) {
     hipLaunchKernelGGL(k_wdense, dim3(B1 * MRG_WIDE_MAXB2), dim3(256), 0, s, keys, ocnt, leaf_pk, leaf_out, leaf_nd,
                        dense_off, B1r, ks);
+}
+
+void mrg_wide_launch_sample_text(const uint8_t *in, const uint64_t *doc_off, uint32_t n_docs, uint64_t total,
+                                 uint32_t S, uint32_t R, SortRec *out, hipStream_t s) {
+    if (S) hipLaunchKernelGGL(k_wsample_text, dim3((S + 255) / 256), dim3(256), 0, s, in, doc_off, n_docs, total, S, R,
+                              out);
+}
+void mrg_wide_launch_sample_dups(const SortRec *r, uint32_t S, unsigned long long *dups, hipStream_t s) {
+    if (S) hipLaunchKernelGGL(k_wsample_dups, dim3((S + 255) / 256), dim3(256), 0, s, r, S, dups);
+}
+void mrg_wide_launch_l1ix(const uint64_t *spl1, uint32_t R, uint32_t B1r, uint8_t *ix1, hipStream_t s) {
+    if (B1r > 1) hipLaunchKernelGGL(k_wl1ix, dim3(R), dim3(256), 0, s, spl1, B1r - 1u, ix1);
+}
+void mrg_wmap_launch_seg(const uint32_t *wcnt, uint32_t B1, uint32_t grid, uint32_t wcap, uint32_t *soff, uint64_t *nb,
+                         hipStream_t s) {
+    hipLaunchKernelGGL(k_wmap_seg, dim3(B1), dim3(64), 0, s, wcnt, grid, wcap, soff, nb);
 }

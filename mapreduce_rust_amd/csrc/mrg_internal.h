@@ -98,9 +98,24 @@ struct MapArgs {
                                  // 8 = every block loads its document's first block (L2-resident),
                                  // 16 = no LDS count add on table hits, 32 = classification
                                  // only, 64 = no queue writes (and no tokens), 128 = every slow
-                                 // token through the codepoint walker (results exact: an A/B knob)
+                                 // token through the codepoint walker (results exact: an A/B knob),
+                                 // 256 = no UTF-8 class fix of non-ASCII blocks, 512 = no slow
+                                 // tokens, 1024 = no squeeze of multi-byte gaps
     unsigned long long *prof;    // perf diagnostics (env MRG_PROF): per-phase wave clocks, [7]; else null
+    // wide map (near-unique keys, wc): no LDS combine -- every short key goes
+    // straight to its L1 bucket b = partition * wB1r + quantile (SipHash-1-3 % R, then the splitters of a
+    // sample of the input), into the region of (b, this workgroup): records
+    // [(b * grid + w) * wcap, + wcap) of wrec, 16 bytes {k0, k1} each; wcnt[b * grid + w] = records the
+    // workgroup produced for b (may exceed wcap: the launch is then rerun with larger regions)
+    uint64_t *wrec;
+    uint32_t *wcnt;
+    const uint64_t *wspl;        // [wR][wB1r - 1] splitter keys (k0, k1)
+    const uint8_t *wix;          // [wR][MRG_WIDE_IX1] splitter index (null: binary search)
+    uint32_t wR, wB1r, wcap;
 };
+#define MRG_WMAP_MAXB1 4096      // L1 buckets the wide map's LDS cursors hold
+#define MRG_WIDE_IX1 260         // bytes of one partition's L1 splitter index (257 entries + prefix bits)
+#define MRG_WMAP_IXR 64          // partitions whose index fits the wide map's LDS
 
 // A set of keys with counts (SoA).  len > 16 keys have their bytes at heap[hoff .. hoff+len).
 struct KeySet {
@@ -154,7 +169,8 @@ struct LongItems {
 // ---- k_map.hip
 // `dev_args` is device memory for one MapArgs (the kernel reads its arguments from there)
 // h: the args to copy to dev_args first (nullptr: already there)
-void mrg_launch_map(const MapArgs *h, MapArgs *dev_args, int app, int grid, int lds_cap, hipStream_t s);
+void mrg_launch_map(const MapArgs *h, MapArgs *dev_args, int app, int grid, int lds_cap, hipStream_t s,
+                    bool wide = false);
 uint64_t mrg_map_tiles(uint64_t doc_lo, uint64_t doc_hi);  // wave blocks (NSUB KiB) of a document (16-B grid)
 int mrg_map_cap(int app, int lds_cap);  // LDS-table entries per map workgroup actually used for lds_cap
 int mrg_map_max_grid(int app, int lds_cap, int device);
@@ -232,7 +248,9 @@ void mrg_launch_export_pack(KeySet ks, const uint8_t *heap, uint64_t n, uint32_t
                             const uint64_t *rec_base, const uint64_t *heap_base, unsigned long long *rec_cur,
                             unsigned long long *heap_cur, XRec *out, uint8_t *out_heap, bool indexer, uint64_t vmax,
                             hipStream_t s);
-void mrg_launch_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, void *recs, hipStream_t s);
+// carry (wc, counts not changed after the sort): count and length in the record's doc / pad words
+void mrg_launch_make_sortrec(KeySet ks, uint64_t n, const uint32_t *doc_rank, void *recs, hipStream_t s,
+                             bool carry = false);
 void mrg_launch_fill_u32(uint32_t *p, uint32_t v, uint64_t n, hipStream_t s);
 void mrg_launch_fill_u64(uint64_t *p, uint64_t v, uint64_t n, hipStream_t s);
 void mrg_launch_iota_u32(uint32_t *p, uint64_t n, hipStream_t s);
@@ -284,6 +302,7 @@ struct FormatArgs {
     int drop_last;
     int indexer;
     int any_long;
+    int carried;                // wc: count and length carried in the records (mrg_launch_make_sortrec)
     const uint8_t *names;       // indexer: doc names concatenated in rank order
     const uint64_t *name_off;   // [n_docs + 1], by rank
 };
@@ -359,9 +378,19 @@ void mrg_wide_launch_l1(const BucketArgs &a, const uint64_t *off, const uint64_t
                         uint16_t *bid, uint8_t *ix1, bool scatter, hipStream_t s);
 void mrg_wide_launch_bstart(const uint32_t *cnt, uint32_t B1, uint32_t ntiles, uint64_t n, uint64_t *bstart,
                             hipStream_t s);
+// rin != null: the input is the wide map's regions (segments per bucket at soff, MapArgs::wrec layout)
 void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstart, const uint64_t *spl1, uint32_t B1,
                         uint32_t B1r, uint32_t target, uint32_t *nleaf, uint64_t *leaf_lo, uint64_t *leaf_lb,
-                        uint16_t *sub, hipStream_t s);
+                        uint16_t *sub, hipStream_t s, const uint64_t *rin = nullptr, const uint32_t *soff = nullptr,
+                        uint32_t grid = 0, uint32_t wcap = 0);
+// wide map (near-unique input): a sample of the input text's tokens (k_wsample_text), adjacent
+// duplicates of the sorted sample, the L1 splitter index, the regions' per-bucket segment starts
+void mrg_wide_launch_sample_text(const uint8_t *in, const uint64_t *doc_off, uint32_t n_docs, uint64_t total,
+                                 uint32_t S, uint32_t R, SortRec *out, hipStream_t s);
+void mrg_wide_launch_sample_dups(const SortRec *r, uint32_t S, unsigned long long *dups, hipStream_t s);
+void mrg_wide_launch_l1ix(const uint64_t *spl1, uint32_t R, uint32_t B1r, uint8_t *ix1, hipStream_t s);
+void mrg_wmap_launch_seg(const uint32_t *wcnt, uint32_t B1, uint32_t grid, uint32_t wcap, uint32_t *soff, uint64_t *nb,
+                         hipStream_t s);
 void mrg_wide_launch_weights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *wk0, uint64_t *wk1, uint64_t *wcnt,
                              uint32_t *wpart, hipStream_t s);
 void mrg_wide_launch_leaf(const WideLeafArgs &w, uint32_t B1, hipStream_t s);

@@ -80,6 +80,11 @@ bool wide_forced() {
     const char *v = getenv("MRG_WIDE");
     return v && *v && atoi(v) != 0;
 }
+// MRG_WIDE=0 pins the bucket path, so it also rules out the wide map
+bool wide_forced_off() {
+    const char *v = getenv("MRG_WIDE");
+    return v && *v && atoi(v) == 0;
+}
 
 template <class F>
 int guard(F &&f) {
@@ -217,6 +222,8 @@ struct mrg_ctx {
     std::vector<double> bcap16_rate;  // the same for the 16-byte regions (wc keys of 13..16 bytes)
     uint64_t ocap_hint = 0;         // records per bucket overflow list
     bool spec_agg = false, spec_c32 = false;  // last wc job took the bucket path (with 32-bit counts)
+    bool wide_hint = false;   // last wc job took the wide aggregation (the next one may take the wide map)
+    uint64_t wcap_hint = 0;   // wide map: records per (L1 bucket, workgroup) region the last run needed
     // job
     bool job = false;
     int app = 0;
@@ -586,6 +593,7 @@ bool bucket_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regc
         c->spec_agg = !idx;
         c->spec_c32 = c32;  // the width this job allowed (not the one a reused launch happened to use)
         c->st.agg_path = 1;
+        c->wide_hint = false;
         {  // the next job's workgroups per bucket: enough sub-ranges for this job's key count, each
            // sub-range's table at most 5/6 full.  Each sub-range is one more pass over the bucket's
            // tail stream: zipf_u (2.9 M keys) aggregates in 6.9 ms at 1 (2 M records overflow to the
@@ -697,6 +705,133 @@ void wide_densify(mrg_ctx *c, uint64_t extra) {
 // Wide aggregation by the two-level sample sort (k_wide.hip): the map's count-1 records go through
 // L1 (partition + global quantile splitters) and L2 (per-bucket splitters) into leaves; the flushed
 // map-table entries (weighted) are aggregated apart, sorted, and merged into their leaves.
+// The wide aggregation after L1: L2 leaves inside every L1 bucket (input: the L1 output K1 in bucket
+// order with bstart, or -- rin != null -- the wide map's regions, segments soff), the leaves, the
+// overflowing leaves' fallback, then the long keys.  K1 becomes the output key array; bid holds the
+// L2 leaf id of every record.  Takes ownership of K1 (kept in c->wide), bstart, spl1, bid, wk*.
+void wide_finish(mrg_ctx *c, LongItems li, uint64_t n, uint64_t nw, uint32_t B1, uint32_t B1r, uint64_t *K1,
+                 uint64_t *bstart, uint64_t *spl1, uint16_t *bid, uint64_t *wk0, uint64_t *wk1, uint64_t *wcnt,
+                 uint32_t *wpart, bool dbg, hipEvent_t *pe, int &npe, const uint64_t *rin, const uint32_t *soff,
+                 uint32_t grid, uint32_t wcap) {
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const uint32_t R = c->R;
+    auto mark = [&]() {
+        if (!dbg || npe >= 8) return;
+        HIPCHK(hipEventCreate(&pe[npe]));
+        HIPCHK(hipEventRecord(pe[npe++], s));
+    };
+    // ---- L2: leaves inside every L1 bucket
+    const uint64_t NL = (uint64_t)B1 * MRG_WIDE_MAXB2;
+    uint64_t *K2 = pget<uint64_t>(p, 2 * n + 2);
+    uint32_t *nleaf = pget<uint32_t>(p, B1);
+    uint64_t *leaf_lo = pget<uint64_t>(p, NL + 1), *leaf_lb = pget<uint64_t>(p, 2 * NL + 2);
+    const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", 256);
+    mrg_wide_launch_l2(rin ? nullptr : K1, K2, bstart, spl1, B1, B1r, target, nleaf, leaf_lo, leaf_lb, bid, s, rin,
+                       soff, grid, wcap);
+    p.put(bid);
+    mark();  // 4: L2
+    // ---- leaves: aggregate + sort + line bytes (K1 becomes the output key array)
+    WideRes &w = c->wide;
+    w.release(p);
+    w.B1 = B1;
+    w.B1r = B1r;
+    w.kout = K1;
+    w.ocnt = pget<uint64_t>(p, n + nw + 1);
+    w.nleaf = nleaf;
+    w.leaf_out = pget<uint64_t>(p, NL);
+    w.leaf_nd = pget<uint32_t>(p, NL + 1);
+    w.leaf_bytes = pget<uint64_t>(p, NL + 1);
+    w.leaf_last = pget<uint32_t>(p, NL);
+    w.leaf_pk = pget<uint32_t>(p, NL);
+    HIPCHK(hipMemsetAsync(w.leaf_pk, 0, 4 * NL, s));
+    HIPCHK(hipMemsetAsync(w.leaf_nd, 0, 4 * (NL + 1), s));
+    HIPCHK(hipMemsetAsync(w.leaf_bytes, 0, 8 * (NL + 1), s));
+    uint32_t *ovf_list = pget<uint32_t>(p, NL);
+    HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
+    HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
+    WideLeafArgs L{};
+    L.kin = K2; L.kout = K1; L.bstart = bstart; L.nleaf = nleaf; L.leaf_lo = leaf_lo; L.leaf_lb = leaf_lb;
+    L.B1r = B1r; L.R = R; L.wk0 = wk0; L.wk1 = wk1; L.wcnt = wcnt; L.wpart = wpart; L.nw = nw;
+    L.maxd = (uint32_t)env_u64("MRG_TEST_LEAF_CAP", 0);
+    L.ocnt = w.ocnt; L.leaf_out = w.leaf_out; L.leaf_nd = w.leaf_nd; L.leaf_bytes = w.leaf_bytes;
+    L.leaf_last = w.leaf_last; L.ovf_list = ovf_list; L.ovf_n = &c->d_cnt[CNT_OVF2]; L.nkeys = &c->d_cnt[CNT_KEYS];
+    L.wr = pget<uint64_t>(p, 2 * NL);
+    L.prof = pget<unsigned long long>(p, 8);
+    HIPCHK(hipMemsetAsync(L.prof, 0, 64, s));
+    L.big_list = pget<uint32_t>(p, NL);
+    L.big_n = pget<unsigned long long>(p, 1);
+    L.leaf_pk = w.leaf_pk;
+    // counts packed into the key slots of leaves whose keys are <= 12 bytes: every count fits 32 bits
+    // when the job has fewer than 2^32 tokens (MRG_TEST_NO_PACK: the unpacked layout everywhere)
+    L.pack = (c->h_cnt[CNT_TOKENS] < 0xFFFFFFFFull && !getenv("MRG_TEST_NO_PACK")) ? 1u : 0u;
+    HIPCHK(hipMemsetAsync(L.big_n, 0, 8, s));
+    mrg_wide_launch_leaf(L, B1, s);
+    mark();  // 5: leaves
+    read_counters(c);
+    const uint64_t novf = c->h_cnt[CNT_OVF2];
+    if (novf) mrg_wide_launch_fallback(L, ovf_list, (uint32_t)novf, p, s);
+    mark();  // 6: fallback
+    read_counters(c);
+    w.distinct = c->h_cnt[CNT_KEYS];
+    w.ready = true;
+    if (dbg) {
+        static const char *nm[] = {"weights", "splitters", "L1", "L2", "leaves", "fallback"};
+        fprintf(stderr, "[mrgpu] wide phases (ms):");
+        for (int i = 1; i < npe; ++i) {
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, pe[i - 1], pe[i]));
+            fprintf(stderr, " %s %.2f", nm[i - 1], ms);
+        }
+        fprintf(stderr, "\n");
+        for (int i = 0; i < npe; ++i) (void)hipEventDestroy(pe[i]);
+        unsigned long long pr[8], nbig = 0;
+        HIPCHK(hipMemcpy(pr, L.prof, sizeof pr, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&nbig, L.big_n, 8, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[mrgpu] wide: %llu passed to the workgroup kernel (%llu by size, %llu by bucket)\n", nbig,
+                pr[6], pr[7]);
+        {  // leaf sizes (records)
+            std::vector<uint32_t> hn(B1);
+            std::vector<uint64_t> hlo(NL), hbs(B1 + 1);
+            HIPCHK(hipMemcpy(hn.data(), nleaf, 4ull * B1, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hlo.data(), leaf_lo, 8ull * NL, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hbs.data(), bstart, 8ull * (B1 + 1), hipMemcpyDeviceToHost));
+            std::vector<uint64_t> sz;
+            for (uint32_t bb = 0; bb < B1; ++bb)
+                for (uint32_t j = 0; j < hn[bb]; ++j) {
+                    const uint64_t lid = (uint64_t)bb * MRG_WIDE_MAXB2 + j;
+                    sz.push_back((j + 1 < hn[bb] ? hlo[lid + 1] : hbs[bb + 1]) - hlo[lid]);
+                }
+            std::sort(sz.begin(), sz.end());
+            if (!sz.empty())
+                fprintf(stderr, "[mrgpu] wide: %zu leaves, records p10 %llu p50 %llu p63 %llu p87 %llu p99 %llu max %llu\n",
+                        sz.size(), (unsigned long long)sz[sz.size() / 10], (unsigned long long)sz[sz.size() / 2],
+                        (unsigned long long)sz[sz.size() * 63 / 100], (unsigned long long)sz[sz.size() * 87 / 100],
+                        (unsigned long long)sz[sz.size() * 99 / 100], (unsigned long long)sz.back());
+        }
+        if (pr[0] | pr[1] | pr[5])
+            fprintf(stderr, "[mrgpu] leaf phase clocks (wave 0, all WGs): clear %.3g insert %.3g list %.3g digits %.3g "
+                            "order %.3g write %.3g\n", (double)pr[0], (double)pr[1], (double)pr[2], (double)pr[3],
+                    (double)pr[4], (double)pr[5]);
+    }
+    if (getenv("MRG_DEBUG"))
+        fprintf(stderr, "[mrgpu] wide: %llu records, %llu weighted, B1 %u (x%u), %llu distinct, %llu leaves overflowed\n",
+                (unsigned long long)n, (unsigned long long)nw, B1, B1r, (unsigned long long)w.distinct,
+                (unsigned long long)novf);
+    p.put(K2); p.put(leaf_lo); p.put(leaf_lb); p.put(ovf_list); p.put(spl1); p.put(bstart); p.put(L.wr);
+    p.put(L.prof); p.put(L.big_list); p.put(L.big_n);
+    p.put(wk0); p.put(wk1); p.put(wcnt); p.put(wpart);
+    c->st.overflow_keys = novf;
+    c->keys.n = 0;
+    c->st.distinct_keys = w.distinct;
+    if (li.n) {  // long keys: the dense key set plus the long keys, sorted by the generic path
+        wide_densify(c, li.n);
+        long_aggregate(c, li);
+        finish_keys(c);
+        c->keys.sorted = false;
+    }
+}
+
 void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap, LongItems li) {
     const uint32_t R = c->R;
     if (R > 4096 || getenv("MRG_WIDE_RADIX")) {  // the L1 histogram holds R x B1r buckets in LDS
@@ -815,114 +950,7 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     p.put(cnt1); p.put(st2); p.put(cm); p.put(om); p.put(cf); p.put(of); p.put(st1); p.put(segptr);
     if (ix1) p.put(ix1);
     mark();  // 3: L1
-    // ---- L2: leaves inside every L1 bucket
-    const uint64_t NL = (uint64_t)B1 * MRG_WIDE_MAXB2;
-    uint64_t *K2 = pget<uint64_t>(p, 2 * n + 2);
-    uint32_t *nleaf = pget<uint32_t>(p, B1);
-    uint64_t *leaf_lo = pget<uint64_t>(p, NL + 1), *leaf_lb = pget<uint64_t>(p, 2 * NL + 2);
-    const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", 256);
-    mrg_wide_launch_l2(K1, K2, bstart, spl1, B1, B1r, target, nleaf, leaf_lo, leaf_lb, bid, s);
-    p.put(bid);
-    mark();  // 4: L2
-    // ---- leaves: aggregate + sort + line bytes (K1 becomes the output key array)
-    WideRes &w = c->wide;
-    w.release(p);
-    w.B1 = B1;
-    w.B1r = B1r;
-    w.kout = K1;
-    w.ocnt = pget<uint64_t>(p, n + nw + 1);
-    w.nleaf = nleaf;
-    w.leaf_out = pget<uint64_t>(p, NL);
-    w.leaf_nd = pget<uint32_t>(p, NL + 1);
-    w.leaf_bytes = pget<uint64_t>(p, NL + 1);
-    w.leaf_last = pget<uint32_t>(p, NL);
-    w.leaf_pk = pget<uint32_t>(p, NL);
-    HIPCHK(hipMemsetAsync(w.leaf_pk, 0, 4 * NL, s));
-    HIPCHK(hipMemsetAsync(w.leaf_nd, 0, 4 * (NL + 1), s));
-    HIPCHK(hipMemsetAsync(w.leaf_bytes, 0, 8 * (NL + 1), s));
-    uint32_t *ovf_list = pget<uint32_t>(p, NL);
-    HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_KEYS], 0, 8, s));
-    HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
-    WideLeafArgs L{};
-    L.kin = K2; L.kout = K1; L.bstart = bstart; L.nleaf = nleaf; L.leaf_lo = leaf_lo; L.leaf_lb = leaf_lb;
-    L.B1r = B1r; L.R = R; L.wk0 = wk0; L.wk1 = wk1; L.wcnt = wcnt; L.wpart = wpart; L.nw = nw;
-    L.maxd = (uint32_t)env_u64("MRG_TEST_LEAF_CAP", 0);
-    L.ocnt = w.ocnt; L.leaf_out = w.leaf_out; L.leaf_nd = w.leaf_nd; L.leaf_bytes = w.leaf_bytes;
-    L.leaf_last = w.leaf_last; L.ovf_list = ovf_list; L.ovf_n = &c->d_cnt[CNT_OVF2]; L.nkeys = &c->d_cnt[CNT_KEYS];
-    L.wr = pget<uint64_t>(p, 2 * NL);
-    L.prof = pget<unsigned long long>(p, 8);
-    HIPCHK(hipMemsetAsync(L.prof, 0, 64, s));
-    L.big_list = pget<uint32_t>(p, NL);
-    L.big_n = pget<unsigned long long>(p, 1);
-    L.leaf_pk = w.leaf_pk;
-    // counts packed into the key slots of leaves whose keys are <= 12 bytes: every count fits 32 bits
-    // when the job has fewer than 2^32 tokens (MRG_TEST_NO_PACK: the unpacked layout everywhere)
-    L.pack = (c->h_cnt[CNT_TOKENS] < 0xFFFFFFFFull && !getenv("MRG_TEST_NO_PACK")) ? 1u : 0u;
-    HIPCHK(hipMemsetAsync(L.big_n, 0, 8, s));
-    mrg_wide_launch_leaf(L, B1, s);
-    mark();  // 5: leaves
-    read_counters(c);
-    const uint64_t novf = c->h_cnt[CNT_OVF2];
-    if (novf) mrg_wide_launch_fallback(L, ovf_list, (uint32_t)novf, p, s);
-    mark();  // 6: fallback
-    read_counters(c);
-    w.distinct = c->h_cnt[CNT_KEYS];
-    w.ready = true;
-    if (dbg) {
-        static const char *nm[] = {"weights", "splitters", "L1", "L2", "leaves", "fallback"};
-        fprintf(stderr, "[mrgpu] wide phases (ms):");
-        for (int i = 1; i < npe; ++i) {
-            float ms = 0;
-            HIPCHK(hipEventElapsedTime(&ms, pe[i - 1], pe[i]));
-            fprintf(stderr, " %s %.2f", nm[i - 1], ms);
-        }
-        fprintf(stderr, "\n");
-        for (int i = 0; i < npe; ++i) (void)hipEventDestroy(pe[i]);
-        unsigned long long pr[8], nbig = 0;
-        HIPCHK(hipMemcpy(pr, L.prof, sizeof pr, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(&nbig, L.big_n, 8, hipMemcpyDeviceToHost));
-        fprintf(stderr, "[mrgpu] wide: %llu passed to the workgroup kernel (%llu by size, %llu by bucket)\n", nbig,
-                pr[6], pr[7]);
-        {  // leaf sizes (records)
-            std::vector<uint32_t> hn(B1);
-            std::vector<uint64_t> hlo(NL), hbs(B1 + 1);
-            HIPCHK(hipMemcpy(hn.data(), nleaf, 4ull * B1, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(hlo.data(), leaf_lo, 8ull * NL, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(hbs.data(), bstart, 8ull * (B1 + 1), hipMemcpyDeviceToHost));
-            std::vector<uint64_t> sz;
-            for (uint32_t bb = 0; bb < B1; ++bb)
-                for (uint32_t j = 0; j < hn[bb]; ++j) {
-                    const uint64_t lid = (uint64_t)bb * MRG_WIDE_MAXB2 + j;
-                    sz.push_back((j + 1 < hn[bb] ? hlo[lid + 1] : hbs[bb + 1]) - hlo[lid]);
-                }
-            std::sort(sz.begin(), sz.end());
-            if (!sz.empty())
-                fprintf(stderr, "[mrgpu] wide: %zu leaves, records p10 %llu p50 %llu p63 %llu p87 %llu p99 %llu max %llu\n",
-                        sz.size(), (unsigned long long)sz[sz.size() / 10], (unsigned long long)sz[sz.size() / 2],
-                        (unsigned long long)sz[sz.size() * 63 / 100], (unsigned long long)sz[sz.size() * 87 / 100],
-                        (unsigned long long)sz[sz.size() * 99 / 100], (unsigned long long)sz.back());
-        }
-        if (pr[0] | pr[1] | pr[5])
-            fprintf(stderr, "[mrgpu] leaf phase clocks (wave 0, all WGs): clear %.3g insert %.3g list %.3g digits %.3g "
-                            "order %.3g write %.3g\n", (double)pr[0], (double)pr[1], (double)pr[2], (double)pr[3],
-                    (double)pr[4], (double)pr[5]);
-    }
-    if (getenv("MRG_DEBUG"))
-        fprintf(stderr, "[mrgpu] wide: %llu records, %llu weighted, B1 %u (x%u), %llu distinct, %llu leaves overflowed\n",
-                (unsigned long long)n, (unsigned long long)nw, B1, B1r, (unsigned long long)w.distinct,
-                (unsigned long long)novf);
-    p.put(K2); p.put(leaf_lo); p.put(leaf_lb); p.put(ovf_list); p.put(spl1); p.put(bstart); p.put(L.wr);
-    p.put(L.prof); p.put(L.big_list); p.put(L.big_n);
-    p.put(wk0); p.put(wk1); p.put(wcnt); p.put(wpart);
-    c->st.overflow_keys = novf;
-    c->keys.n = 0;
-    c->st.distinct_keys = w.distinct;
-    if (li.n) {  // long keys: the dense key set plus the long keys, sorted by the generic path
-        wide_densify(c, li.n);
-        long_aggregate(c, li);
-        finish_keys(c);
-        c->keys.sorted = false;
-    }
+    wide_finish(c, li, n, nw, B1, B1r, K1, bstart, spl1, bid, wk0, wk1, wcnt, wpart, dbg, pe, npe, nullptr, nullptr, 0, 0);
 }
 
 void need_job(mrg_ctx *c) {
@@ -954,12 +982,224 @@ void job_begin(mrg_ctx *c, int app, uint32_t R, uint32_t flags) {
     c->st = mrg_stats{};
 }
 
+// ---- the wide map (near-unique keys, wc): the splitters first, from a sample of the input text, then
+// a map that writes every short key to its L1 bucket (R partitions x B1r key ranges) -- the L1 count
+// and scatter passes over the map's records (wide_aggregate) disappear; L2 reads the regions.
+struct WideMapPlan {
+    bool on = false, forced = false;
+    uint32_t B1 = 0, B1r = 0;
+    uint64_t *spl1 = nullptr;
+    uint8_t *ix1 = nullptr;
+};
+
+// Taken when the context's last wc job went the wide way (or MRG_WIDE_MAP=1) and a sample of the
+// input is near-unique: fewer than 1 in 16 sampled tokens repeat a sampled neighbour in key order.
+WideMapPlan wide_map_plan(mrg_ctx *c, const uint64_t *d_doc_off, uint32_t nd, uint64_t total, int grid) {
+    WideMapPlan P;
+    const char *env = getenv("MRG_WIDE_MAP");
+    P.forced = env && atoi(env) != 0;
+    if (is_idx(c) || (env && atoi(env) == 0) || total == 0 || wide_forced_off()) return P;
+    if (!P.forced && (!c->wide_hint || total < (64ull << 20))) return P;
+    const uint32_t R = c->R;
+    if (R > MRG_WMAP_MAXB1 || grid > 512) return P;
+    uint32_t B1r = std::min<uint32_t>(64, std::max<uint32_t>(1, MRG_WMAP_MAXB1 / R));
+    if (const uint64_t t = env_u64("MRG_TEST_WMAP_B1R", 0)) B1r = (uint32_t)std::min<uint64_t>(B1r, t);
+    const uint32_t B1 = R * B1r;
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const uint32_t S = (uint32_t)std::min<uint64_t>(64ull * B1, 1u << 20);
+    SortRec *sa = pget<SortRec>(p, S), *sb = pget<SortRec>(p, S);
+    void *stmp = p.get(mrg_sort_tmp_bytes(S));
+    unsigned long long *dups = pget<unsigned long long>(p, 1);
+    HIPCHK(hipMemsetAsync(dups, 0, 8, s));
+    mrg_wide_launch_sample_text(c->d_in, d_doc_off, nd, total, S, R, sa, s);
+    SortPlan plan{};
+    plan.use_part = R > 1;
+    plan.part_bytes = bytes_for(R - 1);
+    plan.use_k0 = plan.use_k1 = true;
+    int passes = 0;
+    SortRec *srt = mrg_radix_sort(sa, sb, S, plan, stmp, s, &passes);
+    mrg_wide_launch_sample_dups(srt, S, dups, s);
+    uint64_t *spl1 = pget<uint64_t>(p, 2ull * R * B1r + 2);
+    uint8_t *ix1 = nullptr;
+    if (B1r > 1) {
+        mrg_wide_launch_split1(srt, S, R, B1r, spl1, s);
+        if (B1r >= 5 && R <= MRG_WMAP_IXR) {
+            ix1 = pget<uint8_t>(p, (uint64_t)MRG_WIDE_IX1 * R);
+            mrg_wide_launch_l1ix(spl1, R, B1r, ix1, s);
+        }
+    }
+    unsigned long long nd_h = 0;
+    HIPCHK(hipMemcpyAsync(&nd_h, dups, 8, hipMemcpyDeviceToHost, s));
+    sync(c);
+    p.put(sa); p.put(sb); p.put(stmp); p.put(dups);
+    if (!P.forced && nd_h * 16 >= S) {  // repeats: the LDS combine pays
+        p.put(spl1);
+        p.put(ix1);
+        c->wide_hint = false;
+        return P;
+    }
+    P.on = true;
+    P.B1 = B1;
+    P.B1r = B1r;
+    P.spl1 = spl1;
+    P.ix1 = ix1;
+    return P;
+}
+
+void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_cb, uint32_t *d_ids, uint32_t nd,
+                  uint64_t n_chunks, uint64_t total, int grid, const std::vector<uint32_t> &ids) {
+    Pool &p = c->pool;
+    hipStream_t s = c->stream;
+    const uint32_t B1 = wp.B1;
+    // records per (bucket, workgroup) region: the splitters make the buckets about equal; a token per
+    // ~10 input bytes, +30 %, or the last run's demand
+    uint64_t wcap = std::max<uint64_t>(c->wcap_hint,
+                                       (uint64_t)(1.3 * (double)total / 10.0 / (double)grid / (double)B1) + 64);
+    if (const uint64_t t = env_u64("MRG_TEST_WMAP_CAP", 0)) wcap = t;
+    uint64_t lcap = std::max<uint64_t>(c->long_hint, total / 1024 + 1024);
+    MapArgs A{};
+    MapBufs M;
+    uint64_t *wrec = nullptr;
+    uint32_t *wcnt = nullptr;
+    uint32_t launches = 0;
+    for (;;) {
+        if (wcap > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
+        M.dargs = pget<MapArgs>(p, 1);
+        uint64_t lper = std::max<uint64_t>(c->lper_hint, (lcap + grid - 1) / grid + 16);
+        const uint64_t lovf = lcap / 4 + 1024;
+        const uint64_t lslots = (uint64_t)grid * lper + lovf;
+        M.lstart = pget<uint64_t>(p, lslots);
+        M.llen = pget<uint32_t>(p, lslots);
+        M.ldoc = pget<uint32_t>(p, lslots);
+        M.lcount = pget<uint32_t>(p, (uint64_t)grid);
+        const uint64_t per_wg_blocks = (n_chunks + grid - 1) / grid + 1;
+        A = MapArgs{};
+        A.kwords = (uint32_t)(MRG_MAP_NSUB * per_wg_blocks);
+        M.gbits = pget<uint32_t>(p, (uint64_t)grid * A.kwords);
+        wrec = pget<uint64_t>(p, 2ull * B1 * (uint64_t)grid * wcap + 2);
+        wcnt = pget<uint32_t>(p, (uint64_t)B1 * grid);
+        A.in = c->d_in;
+        A.doc_off = d_doc_off;
+        A.chunk_base = d_cb;
+        A.doc_id = d_ids;
+        A.n_docs = nd;
+        A.n_chunks = n_chunks;
+        A.lstart = M.lstart; A.llen = M.llen; A.ldoc = M.ldoc; A.lper = (uint32_t)lper; A.lovf = lovf;
+        A.lcount = M.lcount;
+        A.gbits = M.gbits;
+        A.counters = c->d_cnt;
+        A.hash_bits = hash_bits(c);
+        A.wrec = wrec; A.wcnt = wcnt; A.wspl = wp.spl1; A.wix = wp.ix1;
+        A.wR = c->R; A.wB1r = wp.B1r; A.wcap = (uint32_t)wcap;
+        HIPCHK(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long) * CNT_N, s));
+        HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_ERRPOS], 0xFF, sizeof(unsigned long long), s));
+        ev_rec(c, 0);
+        h2d(c, M.dargs, &A, sizeof(MapArgs));
+        mrg_launch_map(nullptr, M.dargs, c->app, grid, c->lds_cap, s, true);
+        ev_rec(c, 1);
+        HIPCHK(hipGetLastError());
+        ++launches;
+        read_counters(c);
+        const uint64_t nl = c->h_cnt[CNT_LONG];
+        const bool long_full = c->h_cnt[CNT_LONGX] > A.lovf;
+        if (c->h_cnt[CNT_OVF] == 0 && !long_full) break;
+        if (c->h_cnt[CNT_OVF]) {  // a region overflowed: every region sized to the largest demand
+            std::vector<uint32_t> wc((uint64_t)B1 * grid);
+            HIPCHK(hipMemcpyAsync(wc.data(), wcnt, 4ull * wc.size(), hipMemcpyDeviceToHost, s));
+            sync(c);
+            const uint64_t mx = *std::max_element(wc.begin(), wc.end());
+            wcap = c->wcap_hint = std::max<uint64_t>(wcap, mx + mx / 4 + 64);
+        }
+        if (long_full) {
+            std::vector<uint32_t> lc((uint64_t)grid);
+            HIPCHK(hipMemcpyAsync(lc.data(), M.lcount, 4ull * grid, hipMemcpyDeviceToHost, s));
+            sync(c);
+            const uint64_t mx = *std::max_element(lc.begin(), lc.end());
+            c->lper_hint = mx + mx / 4 + 64;
+            lcap = c->long_hint = std::max<uint64_t>(lcap, nl + nl / 8 + 1024);
+        }
+        if (getenv("MRG_DEBUG"))
+            fprintf(stderr, "[mrgpu] wide map rerun: region overflow %llu (cap now %llu), long %llu\n",
+                    (unsigned long long)c->h_cnt[CNT_OVF], (unsigned long long)wcap, (unsigned long long)nl);
+        M.release(p);
+        p.put(wrec);
+        p.put(wcnt);
+    }
+    c->st.ms_map = ev_ms(c, 0, 1);
+    c->st.map_launches = launches;
+    c->st.input_bytes = total;
+    c->st.tokens = c->h_cnt[CNT_TOKENS];
+    c->st.long_tokens = c->h_cnt[CNT_LONG];
+    c->st.map_records = c->h_cnt[CNT_REC];
+    c->st.nonascii_tiles = c->h_cnt[CNT_NONASCII];
+    c->st.tail_records_16 = 0;
+    c->st.map_spill = 0;
+    const uint64_t errpos = c->h_cnt[CNT_ERRPOS];
+    auto release_all = [&]() {
+        M.release(p);
+        p.put(wrec); p.put(wcnt);
+        p.put(d_doc_off); p.put(d_cb); p.put(d_ids);
+    };
+    if (errpos != ~0ull) {
+        release_all();
+        p.put(wp.spl1); p.put(wp.ix1);
+        uint32_t d = 0;
+        while (d + 1 < nd && c->doc_off[d + 1] <= errpos) ++d;
+        raise(MRG_EUTF8, "stream did not contain valid UTF-8: document %u (id %u), byte offset %llu", d, ids[d],
+              (unsigned long long)(errpos - c->doc_off[d]));
+    }
+    ev_rec(c, 2);
+    LongItems li{};
+    li.base = c->d_in; li.cnt = nullptr;
+    li.n = c->h_cnt[CNT_LONG];
+    if (li.n) {
+        M.dstart = pget<uint64_t>(p, li.n);
+        M.dlen = pget<uint32_t>(p, li.n);
+        M.ddoc = pget<uint32_t>(p, li.n);
+        mrg_launch_long_compact(A, grid, M.dstart, M.dlen, M.ddoc, s);
+    }
+    li.start = M.dstart; li.rawlen = M.dlen; li.doc = M.ddoc;
+    // ---- the regions as L1 buckets: per-bucket segment starts, bucket offsets, then L2 and the leaves
+    uint32_t *soff = pget<uint32_t>(p, (uint64_t)B1 * (grid + 1));
+    uint64_t *nbk = pget<uint64_t>(p, (uint64_t)B1 + 1);
+    uint64_t *bstart = pget<uint64_t>(p, (uint64_t)B1 + 1);
+    uint64_t *tmp = pget<uint64_t>(p, mrg_scan_tmp_elems((uint64_t)B1 + 1));
+    HIPCHK(hipMemsetAsync(nbk + B1, 0, 8, s));
+    mrg_wmap_launch_seg(wcnt, B1, (uint32_t)grid, (uint32_t)wcap, soff, nbk, s);
+    mrg_scan_u64(nbk, bstart, (uint64_t)B1 + 1, tmp, s);  // bstart[B1] = records
+    uint64_t n = 0;
+    HIPCHK(hipMemcpyAsync(&n, bstart + B1, 8, hipMemcpyDeviceToHost, s));
+    sync(c);
+    if (n >= 0xFFFFFFF0ull) raise(MRG_ENOMEM, "wide aggregation: %llu records exceed one GPU's 32-bit record index",
+                                  (unsigned long long)n);
+    uint64_t *K1 = pget<uint64_t>(p, 2 * n + 2);  // the leaves' output keys
+    uint16_t *bid = pget<uint16_t>(p, std::max<uint64_t>(n, 1));
+    uint64_t *wk0 = pget<uint64_t>(p, 1), *wk1 = pget<uint64_t>(p, 1), *wk = pget<uint64_t>(p, 1);
+    uint32_t *wpart = pget<uint32_t>(p, 1);
+    const bool dbg = getenv("MRG_DEBUG") != nullptr;
+    hipEvent_t pe[8] = {};
+    int npe = 0;
+    c->st.agg_path = 2;
+    c->spec_agg = false;
+    wide_finish(c, li, n, 0, B1, wp.B1r, K1, bstart, wp.spl1, bid, wk0, wk1, wk, wpart, dbg, pe, npe, wrec, soff,
+                (uint32_t)grid, (uint32_t)wcap);
+    p.put(soff); p.put(nbk); p.put(tmp); p.put(wp.ix1);
+    c->st.map_kind = 1;
+    ev_rec(c, 3);
+    release_all();
+    c->st.ms_aggregate = ev_ms(c, 2, 3);
+    // the hint holds while the input stays near-unique
+    c->wide_hint = 2 * c->st.distinct_keys > c->st.tokens;
+    c->mapped = true;
+}
+
 void job_map(mrg_ctx *c) {
     need_job(c);
     if (c->doc_off.empty()) raise(MRG_EINVAL, "no input: call mrg_job_set_input first");
     c->wide.release(c->pool);  // a second map of the same job replaces the first one's keys
     c->mapped = c->reduced = false;
-    c->st.spec_agg = c->st.agg_path = 0;
+    c->st.spec_agg = c->st.agg_path = c->st.map_kind = 0;
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     const uint32_t nd = (uint32_t)c->doc_off.size() - 1;
@@ -978,6 +1218,13 @@ void job_map(mrg_ctx *c) {
 
     if (!c->map_grid) c->map_grid = mrg_map_max_grid(c->app, c->lds_cap, c->device);
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->map_grid, n_chunks));
+    {  // near-unique input: the wide map (every key straight to its L1 bucket)
+        WideMapPlan wp = wide_map_plan(c, d_doc_off, nd, total, grid);
+        if (wp.on) {
+            job_map_wide(c, wp, d_doc_off, d_cb, d_ids, nd, n_chunks, total, grid, ids);
+            return;
+        }
+    }
     const uint32_t cap = (uint32_t)mrg_map_cap(c->app, c->lds_cap);
     const bool idx = is_idx(c);
     const uint32_t RW = idx ? 3u : 2u;
@@ -1237,6 +1484,7 @@ void job_map(mrg_ctx *c) {
     if (wide || !bucket_aggregate(c, A, (uint32_t)grid, cap, li, &spec)) {
         c->spec_agg = false;
         c->st.agg_path = 2;
+        c->wide_hint = !idx;
         wide_aggregate(c, A, (uint32_t)grid, cap, li);
     }
     ev_rec(c, 3);
@@ -1301,9 +1549,9 @@ SortPlan sort_plan(mrg_ctx *c, uint32_t R) {
 }
 
 SortRec *sort_keys(mrg_ctx *c, KeySet ks, uint32_t R, const uint32_t *d_rank, SortRec *a, SortRec *b, void *stmp,
-                   bool defer = false) {
+                   bool defer = false, bool carry = false) {
     const uint64_t n = c->keys.n;
-    mrg_launch_make_sortrec(ks, n, d_rank, a, c->stream);
+    mrg_launch_make_sortrec(ks, n, d_rank, a, c->stream, carry);
     check_sort_n(n, "key sort");
     const uint32_t pbits = R > 1 ? 32u - (uint32_t)__builtin_clz(R - 1u) : 0u;
     uint32_t *h_nbig = (uint32_t *)&c->h_cnt[CNT_N];
@@ -1315,8 +1563,10 @@ SortRec *sort_keys(mrg_ctx *c, KeySet ks, uint32_t R, const uint32_t *d_rank, So
     return mrg_msd_sort(a, b, n, pbits, sort_plan(c, R), stmp, c->stream, &n_big, h_nbig);
 }
 
-FormatArgs format_args(mrg_ctx *c, const SortRec *recs, KeySet ks, uint32_t R, int drop_last, const DocRank &dr) {
+FormatArgs format_args(mrg_ctx *c, const SortRec *recs, KeySet ks, uint32_t R, int drop_last, const DocRank &dr,
+                       bool carried = false) {
     FormatArgs f{};
+    f.carried = carried ? 1 : 0;
     f.recs = recs;
     f.n = c->keys.n;
     f.ks = ks;
@@ -1392,8 +1642,11 @@ void job_reduce(mrg_ctx *c) {
     // the oversized-bucket check of the key sort waits for format's own sync (add_first below is
     // not idempotent: that path checks at once)
     const bool defer = !presorted && !(c->extra_first && n);
-    if (presorted) mrg_launch_make_sortrec(c->keys.ks, n, nullptr, a, s);
-    else sorted = sort_keys(c, c->keys.ks, c->R, dr.rank, a, b, stmp, defer);
+    // wc: counts and lengths carried in the sort records, unless the text reduce's empty-key quirk
+    // adds to the first key's count after the sort
+    const bool carry = !is_idx(c) && !c->extra_first;
+    if (presorted) mrg_launch_make_sortrec(c->keys.ks, n, nullptr, a, s, carry);
+    else sorted = sort_keys(c, c->keys.ks, c->R, dr.rank, a, b, stmp, defer, carry);
     // text reduce (worker.rs:169-173): lines with an empty key sort first and, since `prev` is still
     // empty when the first real key arrives, their values join that key's group
     if (c->extra_first && n) {
@@ -1401,13 +1654,13 @@ void job_reduce(mrg_ctx *c) {
         mrg_launch_add_first(sorted, c->keys.ks, c->extra_first, s);
     }
     ev_rec(c, 5);
-    const FormatArgs f = format_args(c, sorted, c->keys.ks, c->R, compat_drop_last(c), dr);
+    const FormatArgs f = format_args(c, sorted, c->keys.ks, c->R, compat_drop_last(c), dr, carry);
     c->part_off.assign(c->R + 1, 0);
     c->out_bytes = mrg_format(f, p, &c->d_out, &c->out_cap, c->part_off.data(), s);
     const uint32_t n_big = *(const uint32_t *)&c->h_cnt[CNT_N];  // written by the sort's async copy
     if (defer && n > 1 && n_big) {  // oversized MSD buckets: sort them, format again
         sorted = mrg_msd_sort_finish(a, b, n, sort_plan(c, c->R), stmp, s, n_big);
-        const FormatArgs f2 = format_args(c, sorted, c->keys.ks, c->R, compat_drop_last(c), dr);
+        const FormatArgs f2 = format_args(c, sorted, c->keys.ks, c->R, compat_drop_last(c), dr, carry);
         c->out_bytes = mrg_format(f2, p, &c->d_out, &c->out_cap, c->part_off.data(), s);
     }
     ev_rec(c, 6);
@@ -1972,7 +2225,7 @@ void text_reduce(mrg_ctx *c, const uint8_t *const *files, const uint64_t *sizes,
 extern "C" {
 
 const char *mrg_last_error(void) { return g_err.c_str(); }
-const char *mrg_version(void) { return "mrgpu 0.4 (gfx950, abi 4)"; }
+const char *mrg_version(void) { return "mrgpu 0.5 (gfx950, abi 5)"; }
 
 int mrg_open(int device, mrg_ctx **out) {
     return guard([&] {

@@ -14,7 +14,7 @@ APP_INDEXER = 1
 FLAG_NO_COMPAT_DROP_LAST = 0x1
 FLAG_FINAL_TXT = 0x2
 XREC_BYTES = 24  # include/mrgpu.h MRG_XREC_BYTES (ABI 3)
-ABI_VERSION = 4  # include/mrgpu.h MRG_ABI_VERSION
+ABI_VERSION = 5  # include/mrgpu.h MRG_ABI_VERSION
 
 OK, EINVAL, EUTF8, EHIP, ENOMEM, EIO, ECOMM = 0, -1, -2, -3, -4, -5, -6
 _CODES = {EINVAL: "EINVAL", EUTF8: "EUTF8", EHIP: "EHIP", ENOMEM: "ENOMEM", EIO: "EIO", ECOMM: "ECOMM"}
@@ -57,7 +57,7 @@ class Stats(C.Structure):
                 ("overflow_keys", C.c_uint64), ("ms_exchange", C.c_double), ("exchange_sent", C.c_uint64),
                 ("exchange_recv", C.c_uint64), ("map_spill", C.c_uint64),
                 ("nonascii_tiles", C.c_uint64), ("tail_records_16", C.c_uint64), ("spec_agg", C.c_uint32),
-                ("agg_path", C.c_uint32)]
+                ("agg_path", C.c_uint32), ("map_kind", C.c_uint32), ("reserved", C.c_uint32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -26,7 +26,7 @@ pub const fn mrg_flag_debug_hash_bits(n: u32) -> u32 {
     (n & 0xFF) << 8
 }
 pub const MRG_XREC_BYTES: usize = 24;
-pub const MRG_ABI_VERSION: u32 = 4;
+pub const MRG_ABI_VERSION: u32 = 5;
 pub const MRG_COMM_ID_BYTES: usize = 128;
 
 #[repr(C)]
@@ -66,6 +66,8 @@ pub struct mrg_stats {
     pub tail_records_16: u64,
     pub spec_agg: u32,
     pub agg_path: u32,
+    pub map_kind: u32,
+    pub reserved: u32,
 }
 
 #[repr(C)]

@@ -90,20 +90,58 @@ def test_c3_full_size_vs_oracle(ctx):
 
 
 def test_c5_slice_vs_oracle(ctx):
-    """configs[4] (1e9 near-unique keys), a 1 GiB slice: 4 x 256 MiB, ~8e7 distinct 12-byte keys,
-    taken by the wide (sort-based) aggregation; byte-identical to the oracle."""
+    """configs[4] (1e9 near-unique keys), a 1 GiB slice: 4 x 256 MiB, ~8e7 distinct 12-byte keys.  The
+    first job takes the LDS-combine map and the wide (sort-based) aggregation; the second, on the same
+    context, the wide map (the sample of the input is near-unique: keys straight to their sort
+    buckets).  Both byte-identical to the oracle."""
     import oracle_lib as O
     nf, fb = 4, 256 * MIB
     buf = _generate(ctx, "unique", nf, fb, 0xC5C5)
     got = _run_job(ctx, buf, nf, fb, 64)
     st = ctx.stats()
+    got2 = _run_job(ctx, buf, nf, fb, 64)
+    st2 = ctx.stats()
     files = _host_files(buf, nf, fb)
     del buf
-    assert st["distinct_keys"] > 70_000_000
+    assert st["distinct_keys"] > 70_000_000 and st["agg_path"] == 2 and st["map_kind"] == 0
+    assert st2["map_kind"] == 1 and st2["distinct_keys"] == st["distinct_keys"]
     exp = O.wc_mt(files, 64, threads=THREADS)
-    assert len(got) == len(exp)
+    assert len(got) == len(exp) == len(got2)
     for r in range(64):
         assert got[r] == exp[r], r
+        assert got2[r] == exp[r], r
+
+
+@pytest.mark.parametrize("knob", [{}, {"MRG_TEST_WMAP_CAP": 2}, {"MRG_TEST_WMAP_B1R": 1}, {"MRG_TEST_WMAP_B1R": 3}])
+def test_wide_map_forced_vs_oracle(ctx, corpus, knobs, knob):
+    """The wide map forced on (MRG_WIDE_MAP=1): every short key goes from the map straight to its L1
+    bucket (SipHash-1-3 partition, then the splitters of a sample of the input), L2 reads the map's
+    regions.  C1 golden digests at R = 1/10/64; near-unique, Unicode and long-key documents, and forced
+    internal hash collisions, against the oracle.  Knobs: regions of 2 records (every region overflows:
+    the launch reruns with regions sized to the demand), one bucket per partition (B1r = 1), three
+    (binary splitter search instead of the index)."""
+    import torch
+    import oracle_lib as O
+    import mapreduce_rust_amd as M
+    from gpu_util import run_wc
+    knobs(MRG_WIDE_MAP=1, **knob)
+    for R in (1, 10, 64):
+        outs = run_wc(ctx, corpus, R)
+        st = ctx.stats()
+        assert st["map_kind"] == 1 and st["agg_path"] == 2, st
+        if knob.get("MRG_TEST_WMAP_CAP"):
+            assert st["map_launches"] >= 2, st
+        assert [sha(o) for o in outs] == [GOLDEN["wc"][str(R)][f"mr-{r}.txt"] for r in range(R)], R
+    n = 8 * MIB
+    t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
+    ctx.gen_unique(t.data_ptr(), n, 0xC5, 3)
+    docs = [t[:n].cpu().numpy().tobytes()] + _long_token_docs(5, n_docs=2, n_tokens=20_000) + [
+        "naïve café ’tis Ærø ſtraße 東京 — x".encode() * 300]
+    for R in (7, 64):
+        exp = O.wc(docs, R, O.FAST)
+        assert run_wc(ctx, docs, R) == exp, R
+        assert ctx.stats()["map_kind"] == 1
+    assert run_wc(ctx, docs, 10, flags=M.debug_hash_bits(4)) == O.wc(docs, 10, O.FAST)
 
 
 def _mixed_keys_doc(seed, n_words=200_000):
@@ -122,7 +160,8 @@ def _mixed_keys_doc(seed, n_words=200_000):
 def knobs():
     keys = ["MRG_TEST_TAIL_CAP", "MRG_TEST_OVF_CAP", "MRG_TEST_AGG_OCAP", "MRG_WIDE", "MRG_TEST_LEAF_CAP",
             "MRG_TEST_LEAF_TARGET", "MRG_TEST_SORT_LCAP", "MRG_TEST_AGG_WIDE_OVF", "MRG_TEST_AGG_NSUB",
-            "MRG_TEST_NO_PACK", "MRG_TEST_LONG_PER", "MRG_TEST_LONG_LIST"]
+            "MRG_TEST_NO_PACK", "MRG_TEST_LONG_PER", "MRG_TEST_LONG_LIST", "MRG_WIDE_MAP", "MRG_TEST_WMAP_CAP",
+            "MRG_TEST_WMAP_B1R"]
     saved = {k: os.environ.get(k) for k in keys}
 
     def set_(**kw):
