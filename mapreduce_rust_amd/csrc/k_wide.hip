@@ -249,22 +249,6 @@ __global__ void k_wsample_dups(const SortRec *r, uint32_t S, unsigned long long 
     if ((threadIdx.x & 63u) == 0 && m) atomicAdd(dups, (unsigned long long)__popcll(m));
 }
 
-// wide map regions of bucket b (one thread block): segment starts soff[b][w] (bucket-relative, the
-// records a region holds: its count clipped to the capacity) and the bucket's total in nb[b]
-__global__ void k_wmap_seg(const uint32_t *wcnt, uint32_t grid, uint32_t wcap, uint32_t *soff, uint64_t *nb) {
-    const uint32_t b = blockIdx.x;
-    if (threadIdx.x != 0) return;
-    uint32_t run = 0;
-    const uint32_t *c = wcnt + (uint64_t)b * grid;
-    uint32_t *so = soff + (uint64_t)b * (grid + 1u);
-    for (uint32_t w = 0; w < grid; ++w) {
-        so[w] = run;
-        run += min(c[w], wcap);
-    }
-    so[grid] = run;
-    nb[b] = run;
-}
-
 struct L1Args {
     BucketArgs A;
     const uint64_t *off;     // main segment offsets [nseg + 1]
@@ -416,6 +400,27 @@ __device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t *s_ws, 
     lds_barrier();
     *total = tot;
     return base + inc - v;
+}
+
+// wide map regions of bucket b (one thread block): segment starts soff[b][w] (bucket-relative, the
+// records a region holds: its count clipped to the capacity) and the bucket's total in nb[b]
+__global__ __launch_bounds__(64) void k_wmap_seg(const uint32_t *wcnt, uint32_t grid, uint32_t wcap, uint32_t *soff,
+                                                 uint64_t *nb) {
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;  // one wave per bucket
+    const uint32_t *c = wcnt + (uint64_t)b * grid;
+    uint32_t *so = soff + (uint64_t)b * (grid + 1u);
+    uint32_t run = 0;
+    for (uint32_t w0 = 0; w0 < grid; w0 += 64) {
+        const uint32_t w = w0 + lane;
+        const uint32_t v = w < grid ? min(c[w], wcap) : 0u;
+        const uint32_t inc = wave_scan_incl(v);
+        if (w < grid) so[w] = run + inc - v;
+        run += (uint32_t)__shfl(inc, 63);
+    }
+    if (lane == 0) {
+        so[grid] = run;
+        nb[b] = run;
+    }
 }
 
 // ---------------------------------------------------------------- L2: per L1 bucket
