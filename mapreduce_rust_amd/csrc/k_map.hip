@@ -673,11 +673,13 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ uint16_t s_q[NW][QCAP];
     // LUT and length masks first in LDS (highest alignment): their base then fits the 16-bit
     // offset field of ds_read, so a lookup needs no separate address add
-    // ASCII class per byte position p of a dword: s_lut[p][c] = (W | S << 4) << p, one byte per
-    // character, so the four lookups of a dword OR straight into its nibble pair (no per-byte shift).
-    // Each table is 128 bytes = 32 dwords, one per LDS bank, and one instruction reads one table: a
-    // wave's lookups never conflict (lanes reading the same dword share it)
-    __shared__ __attribute__((aligned(1024))) uint8_t s_lut[4][128];
+    // Byte class per byte position p of a dword: s_lut[p][c] = (W | S << 4) << p, one byte per byte
+    // value, so the four lookups of a dword OR straight into its nibble pair (no per-byte shift).
+    // ASCII entries are the exact classes; every byte >= 0x80 gets W and S both (a pair no ASCII byte
+    // has), which marks the block's non-ASCII bytes for the UTF-8 class fix at no cost.  The ASCII
+    // half of a table is 128 bytes = 32 dwords, one per LDS bank, and one instruction reads one table:
+    // on ASCII text a wave's lookups never conflict (lanes reading the same dword share it)
+    __shared__ __attribute__((aligned(1024))) uint8_t s_lut[4][256];
     // v_perm selectors per (key length, 1-byte gap position; 16 = none) over the r-aligned window
     __shared__ __attribute__((aligned(16))) uint32_t s_sel[17 * 17][4];
     // workgroup: combine table + tail-region cursors
@@ -750,9 +752,10 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const uint32_t blk = tid < 512 ? (uint32_t)tid >> 6 : 0x20u;
         s_uc[tid] = c_uclass_stage2[c_uclass_stage1[blk] * 64u + ((uint32_t)tid & 63u)];
     }
-    if (tid < 512) {
-        const uint32_t c = mrg_uclass((uint32_t)tid & 127u);
-        s_lut[tid >> 7][tid & 127] = (uint8_t)(((c == MRG_CLS_W ? 1u : 0u) | (c == MRG_CLS_S ? 0x10u : 0u)) << (tid >> 7));
+    if (tid < 1024) {
+        const uint32_t v = (uint32_t)tid & 255u, c = mrg_uclass(v & 127u);
+        const uint32_t ws = v >= 128u ? 0x11u : ((c == MRG_CLS_W ? 1u : 0u) | (c == MRG_CLS_S ? 0x10u : 0u));
+        s_lut[tid >> 8][v] = (uint8_t)(ws << (tid >> 8));
     }
     auto zmask = [](uint32_t L, uint32_t j) {  // word j, byte p (p = 0 least significant) holds key byte 4j + 3 - p
         uint32_t m = 0;
@@ -999,7 +1002,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 const uint32_t w = k == 0 ? x.x : (k == 1 ? x.y : (k == 2 ? x.z : x.w));
 #pragma unroll
                 for (int b = 0; b < 4; ++b)
-                    e[4 * k + b] = s_lut[b][b == 0 ? (w & 0x7Fu) : __builtin_amdgcn_ubfe(w, 8 * b, 7)];
+                    e[4 * k + b] = s_lut[b][b == 0 ? (w & 0xFFu) : (b == 3 ? w >> 24 : __builtin_amdgcn_ubfe(w, 8 * b, 8))];
             }
             // nibbles: W of bytes 0-3, S of bytes 0-3, W of bytes 4-7, ... (byte i: bit i % 4):
             // dword k's byte of y is the OR of its four lookups
@@ -1025,7 +1028,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                            e3 = lane_u32(X.e.w, 1);
             const uint32_t k = (uint32_t)lane & 15u;
             const uint32_t dwv = k < 8u ? (k < 4u ? e0 : e1) : (k < 12u ? e2 : e3);
-            const uint32_t cl = s_lut[0][__builtin_amdgcn_ubfe(dwv, 8u * (k & 3u), 7)];
+            const uint32_t cl = s_lut[0][__builtin_amdgcn_ubfe(dwv, 8u * (k & 3u), 8)];
             const bool in = (uint32_t)BLK + k < hi_rel;  // bytes past the document are White_Space
             const uint32_t wm = (uint32_t)__ballot(lane < 16 && in && (cl & 1u));
             const uint32_t sm = (uint32_t)__ballot(lane < 16 && (!in || (cl & 0x10u)));
@@ -1034,7 +1037,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         const bool n0 = na(X.v0), n1 = na(X.v1), ne = na(X.e);
         // class of the byte before the block (lane 0's e, byte 15)
         uint32_t prev_blk =
-            Ab > doc_lo ? (uint32_t)(s_lut[0][(lane_u32(X.e.w, 0) >> 24) & 0x7Fu] >> 4) : 1u;
+            Ab > doc_lo ? (uint32_t)(s_lut[0][lane_u32(X.e.w, 0) >> 24] >> 4) & 1u : 1u;
         // A non-ASCII byte where the fast path reads (either tile, the first halo segment, the bytes
         // before the block): the LUT classes of the non-ASCII bytes are replaced by UTF-8-exact ones,
         // after which both tiles are tokenized exactly like ASCII tiles -- every byte of a codepoint
@@ -1064,20 +1067,24 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             const LDS uint8_t *uc = (const LDS uint8_t *)s_uc;
             bool bad = false;
             auto hb = [](uint32_t d) { return ((((d & 0x80808080u) >> 7) * 0x00204081u) >> 21) & 0xFu; };
-            // non-ASCII bytes and leads of the 16 bytes x at block offset so, inside [lo, hi)
-            auto seg_masks = [&](const uint4 &x, int so, uint32_t &nam, uint32_t &lead) {
-                const int vlo = max(lo - so, 0), vhi = min(hi - so, 16);
-                const uint32_t rm = vhi > vlo ? (((1u << vhi) - 1u) & ~((1u << vlo) - 1u)) : 0u;
-                nam = (hb(x.x) | (hb(x.y) << 4) | (hb(x.z) << 8) | (hb(x.w) << 12)) & rm;
-                lead = (hb(x.x & (x.x << 1)) | (hb(x.y & (x.y << 1)) << 4) | (hb(x.z & (x.z << 1)) << 8) |
-                        (hb(x.w & (x.w << 1)) << 12)) & rm;
+            // the non-ASCII bytes inside the document: W and S both set by the LUT (bytes outside the
+            // document were made White_Space only); of those, the codepoint leads (>= 0xC0)
+            auto nam_of = [](uint32_t m) { return m & (m >> 16) & 0xFFFFu; };
+            auto leads = [&](const uint4 &x, uint32_t nam) {
+                return (hb(x.x & (x.x << 1)) | (hb(x.y & (x.y << 1)) << 4) | (hb(x.z & (x.z << 1)) << 8) |
+                        (hb(x.w & (x.w << 1)) << 12)) & nam;
             };
-            uint32_t nam0, ld0, nam1, ld1, namh, ldh;
-            seg_masks(X.v0, (int)l16, nam0, ld0);
-            seg_masks(X.v1, 1024 + (int)l16, nam1, ld1);
-            const uint4 xh{lane_u32(X.e.x, 1), lane_u32(X.e.y, 1), lane_u32(X.e.z, 1), lane_u32(X.e.w, 1)};
-            seg_masks(xh, BLK, namh, ldh);  // the first halo segment: lane 63's
-            if (lane != 63) namh = ldh = 0u;
+            const uint32_t nam0 = nam_of(m0), nam1 = nam_of(m1), namh_w = nam_of(mh);  // mh: wave-uniform
+            const uint32_t ld0 = leads(X.v0, nam0), ld1 = leads(X.v1, nam1);
+            uint4 xh{0u, 0u, 0u, 0u};
+            uint32_t namh = 0u, ldh = 0u;
+            if (namh_w) {  // the first halo segment (lane 63's) holds non-ASCII bytes (wave-uniform)
+                xh = uint4{lane_u32(X.e.x, 1), lane_u32(X.e.y, 1), lane_u32(X.e.z, 1), lane_u32(X.e.w, 1)};
+                if (lane == 63) {
+                    namh = namh_w;
+                    ldh = leads(xh, namh);
+                }
+            }
             // the byte before the block (inside the document and not ASCII): the lead of its codepoint,
             // 1..4 bytes back (wave-uniform)
             const uint32_t before = lane_u32(X.e.w, 0);  // block bytes -4..-1
@@ -1121,16 +1128,21 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 S |= cl == MRG_CLS_S ? span : 0u;
             };
             uint32_t W0 = 0, S0 = 0, C0 = 0, W1 = 0, S1 = 0, C1 = 0;
-            for (uint32_t mA = ld0, mB = ld1; __any((mA | mB) != 0u);) {
-                if (mA) {
-                    const uint32_t p = (uint32_t)__builtin_ctz(mA);
-                    mA &= mA - 1u;
-                    dec(p, X.v0.x, X.v0.y, X.v0.z, X.v0.w, nA, (int)l16, W0, S0, C0);
-                }
-                if (mB) {
-                    const uint32_t p = (uint32_t)__builtin_ctz(mB);
-                    mB &= mB - 1u;
-                    dec(p, X.v1.x, X.v1.y, X.v1.z, X.v1.w, nB, 1024 + (int)l16, W1, S1, C1);
+            // one codepoint per lane and trip, the lane's two segments' leads in one mask (non-ASCII
+            // text is sparse: most lanes have none, a few one)
+            for (uint32_t mAB = ld0 | (ld1 << 16); __any(mAB != 0u);) {
+                if (mAB) {
+                    const uint32_t q = (uint32_t)__builtin_ctz(mAB);
+                    mAB &= mAB - 1u;
+                    const bool sb = q >= 16u;
+                    uint32_t w = 0, sm = 0, c = 0;
+                    dec(q & 15u, sb ? X.v1.x : X.v0.x, sb ? X.v1.y : X.v0.y, sb ? X.v1.z : X.v0.z,
+                        sb ? X.v1.w : X.v0.w, sb ? nB : nA, (sb ? 1024 : 0) + (int)l16, w, sm, c);
+                    if (sb) {
+                        W1 |= w; S1 |= sm; C1 |= c;
+                    } else {
+                        W0 |= w; S0 |= sm; C0 |= c;
+                    }
                 }
             }
             // lane 0: the codepoint holding the byte before the block (window = the 16 bytes before it +

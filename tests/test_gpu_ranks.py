@@ -269,7 +269,8 @@ def test_c5_forced_collisions_vs_oracle(ctx):
     """SURVEY §8(d) C5's forced-collision run: a 512 MiB near-unique slice (4e7 keys, the wide path)
     plus 260 000 distinct keys of 13..30 bytes (16-byte tail records and the long-key fingerprint sort), every internal hash truncated to 20 bits
     (MRG_FLAG_DEBUG_HASH_BITS(20): map-table sets, tail buckets, HBM tables and the long-key
-    fingerprints all collide massively); output byte-identical to the oracle."""
+    fingerprints all collide massively); output byte-identical to the oracle, through the LDS-combine
+    map and the wide map (MRG_WIDE_MAP=0 / 1)."""
     import random
     import torch
     import mapreduce_rust_amd as M
@@ -288,15 +289,27 @@ def test_c5_forced_collisions_vs_oracle(ctx):
     pad = (-(nf * fb + len(longs))) % 16
     t = torch.from_numpy(np.concatenate([host, np.zeros(64 + pad, dtype=np.uint8)])).to("cuda:0")
     off = [0, fb, 2 * fb, 2 * fb + len(longs)]
-    ctx.job_begin(M.APP_WC, 64, M.debug_hash_bits(20))
-    ctx.set_input(t.data_ptr(), off)
-    ctx.map()
-    ctx.reduce()
-    got = ctx.outputs()
-    st = ctx.stats()
+    runs = []
+    saved = os.environ.get("MRG_WIDE_MAP")
+    try:
+        for wm in ("0", "1"):  # the LDS-combine map + wide aggregation, then the wide map
+            os.environ["MRG_WIDE_MAP"] = wm
+            ctx.job_begin(M.APP_WC, 64, M.debug_hash_bits(20))
+            ctx.set_input(t.data_ptr(), off)
+            ctx.map()
+            ctx.reduce()
+            runs.append((ctx.outputs(), ctx.stats()))
+    finally:
+        if saved is None:
+            os.environ.pop("MRG_WIDE_MAP", None)
+        else:
+            os.environ["MRG_WIDE_MAP"] = saved
     del t
     exp = O.wc_mt([host[:fb], host[fb:2 * fb], host[2 * fb:]], 64, threads=THREADS)
-    assert st["distinct_keys"] > 40_000_000 and st["long_tokens"] >= 150_000, st
-    assert st["tail_records_16"] > 30_000 and st["agg_path"] == 2, st
-    for r in range(64):
-        assert got[r] == exp[r], r
+    for (got, st), kind in zip(runs, (0, 1)):
+        assert st["distinct_keys"] > 40_000_000 and st["long_tokens"] >= 150_000, st
+        assert st["agg_path"] == 2 and st["map_kind"] == kind, st
+        if kind == 0:
+            assert st["tail_records_16"] > 30_000, st
+        for r in range(64):
+            assert got[r] == exp[r], (kind, r)
