@@ -104,6 +104,7 @@ __device__ __forceinline__ const CAS T *cp(const T *p) {
 }
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x3a __attribute__((ext_vector_type(3), aligned(4)));  // one 12-byte tail record
 // byte-aligned LDS views (the key window read of the token rounds)
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
 typedef uint32_t u32u __attribute__((aligned(1)));
@@ -383,13 +384,22 @@ __device__ __forceinline__ uint32_t wide_bucket(const MapArgs &A, const TailRegi
 __device__ __forceinline__ void wide_store(const MapArgs &A, const TailRegions &R, bool act, uint64_t k0, uint64_t k1) {
     if (!act) return;
     const uint32_t b = wide_bucket(A, R, k0, k1);
+    if (A.w12 && (uint32_t)k1 != 0u) {  // 12-byte regions: a key of 13..16 bytes to the bucket's list
+        const uint32_t j = atomicAdd(&A.wl16n[b], 1u);
+        if (j < A.wl16cap) *reinterpret_cast<GAS u64x2 *>(gp(A.wl16) + 2ull * ((uint64_t)b * A.wl16cap + j)) = u64x2{k0, k1};
+        else g_add(&A.counters[CNT_W16], 1ull);
+        return;
+    }
     const uint32_t pos = atomicAdd(&R.wcur[b], 1u);
     if (pos < A.wcap) {
         const uint64_t i = ((uint64_t)b * gridDim.x + blockIdx.x) * A.wcap + pos;
-        *reinterpret_cast<GAS u64x2 *>(gp(A.wrec) + 2u * i) = u64x2{k0, k1};
+        if (A.w12)
+            *reinterpret_cast<GAS u32x3a *>(reinterpret_cast<GAS uint8_t *>(gp(A.wrec)) + 12u * i) =
+                u32x3a{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)(k1 >> 32)};
+        else
+            *reinterpret_cast<GAS u64x2 *>(gp(A.wrec) + 2u * i) = u64x2{k0, k1};
     }
 }
-typedef uint32_t u32x3a __attribute__((ext_vector_type(3), aligned(4)));  // one 12-byte tail record
 
 // wc tail record i: keys of <= 12 bytes as 12 bytes {k0, high word of k1} in pool, longer ones as
 // {k0, k1} in pool16; the indexer's {k0, k1, doc} (24 B) in pool

@@ -241,12 +241,14 @@ __global__ void k_wsample_text(const uint8_t *in, const uint64_t *doc_off, uint3
     out[j] = r;
 }
 
-// sorted samples: adjacent equal keys (the near-unique test)
+// sorted samples: adjacent equal keys (the near-unique test) in dups[0], keys of 13..16 bytes in dups[1]
 __global__ void k_wsample_dups(const SortRec *r, uint32_t S, unsigned long long *dups) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     const bool d = j > 0 && j < S && r[j].part == r[j - 1].part && r[j].k0 == r[j - 1].k0 && r[j].k1 == r[j - 1].k1;
-    const uint64_t m = __ballot(d);
+    const bool w16 = j < S && (uint32_t)r[j].k1 != 0u;
+    const uint64_t m = __ballot(d), m16 = __ballot(w16);
     if ((threadIdx.x & 63u) == 0 && m) atomicAdd(dups, (unsigned long long)__popcll(m));
+    if ((threadIdx.x & 63u) == 0 && m16) atomicAdd(dups + 1, (unsigned long long)__popcll(m16));
 }
 
 struct L1Args {
@@ -402,13 +404,14 @@ __device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t *s_ws, 
     return base + inc - v;
 }
 
-// wide map regions of bucket b (one thread block): segment starts soff[b][w] (bucket-relative, the
-// records a region holds: its count clipped to the capacity) and the bucket's total in nb[b]
-__global__ __launch_bounds__(64) void k_wmap_seg(const uint32_t *wcnt, uint32_t grid, uint32_t wcap, uint32_t *soff,
-                                                 uint64_t *nb) {
-    const uint32_t b = blockIdx.x, lane = threadIdx.x;  // one wave per bucket
+// wide map regions of bucket b (one wave): segment starts soff[b][w] (bucket-relative; a region holds
+// its count clipped to the capacity), w = grid the bucket's 16-byte list (12-byte regions only), then
+// the bucket's total, also in nb[b]
+__global__ __launch_bounds__(64) void k_wmap_seg(const uint32_t *wcnt, uint32_t grid, uint32_t wcap,
+                                                 const uint32_t *wl16n, uint32_t wl16cap, uint32_t *soff, uint64_t *nb) {
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
     const uint32_t *c = wcnt + (uint64_t)b * grid;
-    uint32_t *so = soff + (uint64_t)b * (grid + 1u);
+    uint32_t *so = soff + (uint64_t)b * (grid + 2u);
     uint32_t run = 0;
     for (uint32_t w0 = 0; w0 < grid; w0 += 64) {
         const uint32_t w = w0 + lane;
@@ -419,6 +422,8 @@ __global__ __launch_bounds__(64) void k_wmap_seg(const uint32_t *wcnt, uint32_t 
     }
     if (lane == 0) {
         so[grid] = run;
+        run += wl16n ? min(wl16n[b], wl16cap) : 0u;
+        so[grid + 1] = run;
         nb[b] = run;
     }
 }
@@ -434,23 +439,48 @@ struct L2Args {
     uint64_t *leaf_lo;       // [B1 * MAXB2 + 1] first record of each leaf (absolute)
     uint64_t *leaf_lb;       // [B1 * MAXB2][2] lower key bound of each leaf
     uint16_t *sub;           // [n] leaf (inside its L1 bucket) of each record: histogram pass -> scatter
-    // segmented input (the wide map's regions): L1 bucket b's records are segments w < grid, segment w =
-    // rin records [(b * grid + w) * wcap, + its count), at bucket-relative offsets soff[b * (grid + 1) + w]
+    // segmented input (the wide map's regions): L1 bucket b's records are segments w <= grid at
+    // bucket-relative offsets soff[b * (grid + 2) + w]: w < grid the region of (b, w), records
+    // [(b * grid + w) * wcap, + its count) of rin (12 bytes each when w12, else 16), w = grid the
+    // bucket's list of 16-byte records (wl16 [b * wl16cap, ...); empty unless w12)
     const uint64_t *rin;
     const uint32_t *soff;
-    uint32_t grid, wcap;
+    uint32_t grid, wcap, w12, wl16cap;
+    const uint64_t *wl16;
 };
 
+// record r of segment w of bucket b (segmented input), as (k0, k1)
+typedef uint32_t v4wua __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ void seg_load(const L2Args &L, uint32_t b, uint32_t w, uint64_t r, uint64_t &k0,
+                                         uint64_t &k1) {
+    if (w == L.grid) {
+        const GASW uint64_t *p = gw(L.wl16) + 2ull * ((uint64_t)b * L.wl16cap + r);
+        k0 = p[0];
+        k1 = p[1];
+        return;
+    }
+    const uint64_t i = ((uint64_t)b * L.grid + w) * L.wcap + r;
+    if (L.w12) {  // one 16-byte load (4 bytes of slack after the last region)
+        const v4wua x = *reinterpret_cast<const GASW v4wua *>(reinterpret_cast<const GASW uint8_t *>(gw(L.rin)) + 12u * i);
+        k0 = (uint64_t)x.x | ((uint64_t)x.y << 32);
+        k1 = (uint64_t)x.z << 32;
+    } else {
+        const GASW uint64_t *p = gw(L.rin) + 2ull * i;
+        k0 = p[0];
+        k1 = p[1];
+    }
+}
+
 // Segmented input: record i (bucket-relative) of bucket b, through its segment (binary search)
-__device__ __forceinline__ const GASW uint64_t *seg_record(const L2Args &L, uint32_t b, const uint32_t *so,
-                                                           uint64_t i) {
-    uint32_t lo = 0, hi = L.grid;  // so[lo] <= i < so[hi]
+__device__ __forceinline__ void seg_record(const L2Args &L, uint32_t b, const uint32_t *so, uint64_t i, uint64_t &k0,
+                                           uint64_t &k1) {
+    uint32_t lo = 0, hi = L.grid + 1u;  // so[lo] <= i < so[hi]
     while (hi - lo > 1u) {
         const uint32_t mid = (lo + hi) >> 1;
         if (so[mid] <= i) lo = mid;
         else hi = mid;
     }
-    return gw(L.rin) + 2ull * (((uint64_t)b * L.grid + lo) * L.wcap + (i - so[lo]));
+    seg_load(L, b, lo, i - so[lo], k0, k1);
 }
 
 template <bool SEG>
@@ -463,10 +493,10 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     static_assert(W_SC * sizeof(uint64_t) * 2 <= sizeof(s_smp) && W_SC * sizeof(uint16_t) <= sizeof(s_spl),
                   "the scatter's stage fits the sample and splitter arrays");
     __shared__ uint32_t s_ws[W_NW];
-    __shared__ uint32_t s_cseg[SEG ? W_MAXSEG + 1 : 1];   // SEG: the bucket's segment starts
+    __shared__ uint32_t s_cseg[SEG ? W_MAXSEG + 2 : 1];   // SEG: the bucket's segment starts
     const uint32_t tid = threadIdx.x, b = blockIdx.x;
     if (SEG) {
-        for (uint32_t w = tid; w <= L.grid; w += W_WG) s_cseg[w] = L.soff[(uint64_t)b * (L.grid + 1u) + w];
+        for (uint32_t w = tid; w <= L.grid + 1u; w += W_WG) s_cseg[w] = L.soff[(uint64_t)b * (L.grid + 2u) + w];
         lds_barrier();
     }
     const uint64_t base = L.bstart[b], nb = L.bstart[b + 1] - base;
@@ -482,9 +512,12 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
             uint64_t a = ~0ull, c = ~0ull;  // padding sorts last
             if (k < S) {
                 const uint64_t i = ((2ull * k + 1ull) * nb) / (2ull * S);
-                const GASW uint64_t *x = SEG ? seg_record(L, b, s_cseg, i) : in + 2 * i;
-                a = x[0];
-                c = x[1];
+                if (SEG) {
+                    seg_record(L, b, s_cseg, i, a, c);
+                } else {
+                    a = in[2 * i];
+                    c = in[2 * i + 1];
+                }
             }
             s_smp[2 * k] = a;
             s_smp[2 * k + 1] = c;
@@ -529,13 +562,16 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     if (SEG) {  // segment by segment, one wave each: reads stay inside a segment
         const uint32_t *so = s_cseg;
         const uint32_t lane = tid & 63u;
-        for (uint32_t w = tid >> 6; w < L.grid; w += W_NW) {
+        for (uint32_t w = tid >> 6; w <= L.grid; w += W_NW) {
             const uint32_t o = so[w], nw = so[w + 1] - o;
-            const GASW v2 *sv = reinterpret_cast<const GASW v2 *>(gw(L.rin) + 2ull * (((uint64_t)b * L.grid + w) * L.wcap));
             for (uint32_t j0 = lane; j0 < nw; j0 += (uint32_t)U * 64u) {
                 v2 x[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) x[u] = sv[min(j0 + (uint32_t)u * 64u, nw - 1u)];
+                for (int u = 0; u < U; ++u) {
+                    uint64_t a, c;
+                    seg_load(L, b, w, min(j0 + (uint32_t)u * 64u, nw - 1u), a, c);
+                    x[u] = v2{a, c};
+                }
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     if (j0 + (uint32_t)u * 64u < nw) {
@@ -603,7 +639,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         uint32_t sw = 0;
         if (SEG) {
             const uint64_t q0 = c0 + min(tid, nc - 1u);
-            uint32_t lo = 0, hi = L.grid;  // s_cseg[lo] <= q0 < s_cseg[hi]
+            uint32_t lo = 0, hi = L.grid + 1u;  // s_cseg[lo] <= q0 < s_cseg[hi]
             while (hi - lo > 1u) {
                 const uint32_t mid = (lo + hi) >> 1;
                 if (s_cseg[mid] <= q0) lo = mid;
@@ -617,8 +653,9 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
             const uint64_t i = c0 + min(p, nc - 1u);
             if (SEG) {
                 while (s_cseg[sw + 1] <= i) ++sw;
-                x[u] = *reinterpret_cast<const GASW v2 *>(gw(L.rin) + 2ull * (((uint64_t)b * L.grid + sw) * L.wcap +
-                                                                              (i - s_cseg[sw])));
+                uint64_t a, c;
+                seg_load(L, b, sw, i - s_cseg[sw], a, c);
+                x[u] = v2{a, c};
             } else {
                 x[u] = inv[i];
             }
@@ -1946,10 +1983,10 @@ void mrg_wide_launch_bstart(const uint32_t *cnt, uint32_t B1, uint32_t ntiles, u
 }
 void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstart, const uint64_t *spl1, uint32_t B1,
                         uint32_t B1r, uint32_t target, uint32_t *nleaf, uint64_t *leaf_lo, uint64_t *leaf_lb,
-                        uint16_t *sub, hipStream_t s, const uint64_t *rin, const uint32_t *soff, uint32_t grid,
-                        uint32_t wcap) {
-    L2Args L{in, out, bstart, spl1, B1r, target, nleaf, leaf_lo, leaf_lb, sub, rin, soff, grid, wcap};
-    if (rin) hipLaunchKernelGGL(k_wl2<true>, dim3(B1), dim3(W_WG), 0, s, L);
+                        uint16_t *sub, hipStream_t s, const WmapIn &wm) {
+    L2Args L{in, out, bstart, spl1, B1r, target, nleaf, leaf_lo, leaf_lb, sub,
+             wm.rin, wm.soff, wm.grid, wm.wcap, wm.w12, wm.wl16cap, wm.wl16};
+    if (wm.rin) hipLaunchKernelGGL(k_wl2<true>, dim3(B1), dim3(W_WG), 0, s, L);
     else hipLaunchKernelGGL(k_wl2<false>, dim3(B1), dim3(W_WG), 0, s, L);
 }
 void mrg_wide_launch_weights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *wk0, uint64_t *wk1, uint64_t *wcnt,
@@ -2045,7 +2082,7 @@ void mrg_wide_launch_sample_dups(const SortRec *r, uint32_t S, unsigned long lon
 void mrg_wide_launch_l1ix(const uint64_t *spl1, uint32_t R, uint32_t B1r, uint8_t *ix1, hipStream_t s) {
     if (B1r > 1) hipLaunchKernelGGL(k_wl1ix, dim3(R), dim3(256), 0, s, spl1, B1r - 1u, ix1);
 }
-void mrg_wmap_launch_seg(const uint32_t *wcnt, uint32_t B1, uint32_t grid, uint32_t wcap, uint32_t *soff, uint64_t *nb,
-                         hipStream_t s) {
-    hipLaunchKernelGGL(k_wmap_seg, dim3(B1), dim3(64), 0, s, wcnt, grid, wcap, soff, nb);
+void mrg_wmap_launch_seg(const uint32_t *wcnt, uint32_t B1, uint32_t grid, uint32_t wcap, const uint32_t *wl16n,
+                         uint32_t wl16cap, uint32_t *soff, uint64_t *nb, hipStream_t s) {
+    hipLaunchKernelGGL(k_wmap_seg, dim3(B1), dim3(64), 0, s, wcnt, grid, wcap, wl16n, wl16cap, soff, nb);
 }

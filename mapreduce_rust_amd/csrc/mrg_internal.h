@@ -37,7 +37,8 @@ enum {
     CNT_NONASCII = 7, // 1 KiB tiles that took the non-ASCII tokenizer
     CNT_REC16 = 8,    // of CNT_REC: 16-byte tail records (wc keys of 13..16 bytes)
     CNT_LONGX = 9,    // long-token records beyond their workgroup's region (the shared list)
-    CNT_N = 10
+    CNT_W16 = 10,     // wide map, 12-byte regions: keys of 13..16 bytes that found their bucket's list full
+    CNT_N = 11
 };
 
 // Stream-ordered caching allocator interface (all work of a context runs on one stream, so a
@@ -112,6 +113,13 @@ struct MapArgs {
     const uint64_t *wspl;        // [wR][wB1r - 1] splitter keys (k0, k1)
     const uint8_t *wix;          // [wR][MRG_WIDE_IX1] splitter index (null: binary search)
     uint32_t wR, wB1r, wcap;
+    // w12: the regions hold 12-byte records {k0, high word of k1} (keys of <= 12 bytes; 4 bytes of slack
+    // after the last region); a key of 13..16 bytes goes to its bucket's list of 16-byte records,
+    // wl16 records [b * wl16cap, + wl16n[b]) (a device atomic each: such keys are rare when w12 is
+    // chosen; a full list counts in CNT_W16 and reruns the launch with 16-byte regions)
+    uint32_t w12, wl16cap;
+    uint64_t *wl16;
+    uint32_t *wl16n;
 };
 #define MRG_WMAP_MAXB1 4096      // L1 buckets the wide map's LDS cursors hold
 #define MRG_WIDE_IX1 260         // bytes of one partition's L1 splitter index (257 entries + prefix bits)
@@ -378,19 +386,26 @@ void mrg_wide_launch_l1(const BucketArgs &a, const uint64_t *off, const uint64_t
                         uint16_t *bid, uint8_t *ix1, bool scatter, hipStream_t s);
 void mrg_wide_launch_bstart(const uint32_t *cnt, uint32_t B1, uint32_t ntiles, uint64_t n, uint64_t *bstart,
                             hipStream_t s);
-// rin != null: the input is the wide map's regions (segments per bucket at soff, MapArgs::wrec layout)
+// The wide map's regions as L2 input (MapArgs::wrec / w12 / wl16 layout); rin == null: L1's output
+struct WmapIn {
+    const uint64_t *rin = nullptr;
+    const uint32_t *soff = nullptr;  // [B1][grid + 2] segment starts (mrg_wmap_launch_seg)
+    uint32_t grid = 0, wcap = 0, w12 = 0, wl16cap = 0;
+    const uint64_t *wl16 = nullptr;
+};
 void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstart, const uint64_t *spl1, uint32_t B1,
                         uint32_t B1r, uint32_t target, uint32_t *nleaf, uint64_t *leaf_lo, uint64_t *leaf_lb,
-                        uint16_t *sub, hipStream_t s, const uint64_t *rin = nullptr, const uint32_t *soff = nullptr,
-                        uint32_t grid = 0, uint32_t wcap = 0);
+                        uint16_t *sub, hipStream_t s, const WmapIn &wm = WmapIn{});
 // wide map (near-unique input): a sample of the input text's tokens (k_wsample_text), adjacent
 // duplicates of the sorted sample, the L1 splitter index, the regions' per-bucket segment starts
 void mrg_wide_launch_sample_text(const uint8_t *in, const uint64_t *doc_off, uint32_t n_docs, uint64_t total,
                                  uint32_t S, uint32_t R, SortRec *out, hipStream_t s);
 void mrg_wide_launch_sample_dups(const SortRec *r, uint32_t S, unsigned long long *dups, hipStream_t s);
 void mrg_wide_launch_l1ix(const uint64_t *spl1, uint32_t R, uint32_t B1r, uint8_t *ix1, hipStream_t s);
-void mrg_wmap_launch_seg(const uint32_t *wcnt, uint32_t B1, uint32_t grid, uint32_t wcap, uint32_t *soff, uint64_t *nb,
-                         hipStream_t s);
+// segment starts of bucket b: soff[b * (grid + 2) + w], w < grid the regions, w = grid the 16-byte list
+// (wl16n null: empty), [grid + 1] the bucket's total, also in nb[b]
+void mrg_wmap_launch_seg(const uint32_t *wcnt, uint32_t B1, uint32_t grid, uint32_t wcap, const uint32_t *wl16n,
+                         uint32_t wl16cap, uint32_t *soff, uint64_t *nb, hipStream_t s);
 void mrg_wide_launch_weights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *wk0, uint64_t *wk1, uint64_t *wcnt,
                              uint32_t *wpart, hipStream_t s);
 void mrg_wide_launch_leaf(const WideLeafArgs &w, uint32_t B1, hipStream_t s);

@@ -224,6 +224,7 @@ struct mrg_ctx {
     bool spec_agg = false, spec_c32 = false;  // last wc job took the bucket path (with 32-bit counts)
     bool wide_hint = false;   // last wc job took the wide aggregation (the next one may take the wide map)
     uint64_t wcap_hint = 0;   // wide map: records per (L1 bucket, workgroup) region the last run needed
+    bool w12_off = false;     // wide map: a job overflowed the 16-byte lists of the 12-byte regions
     // job
     bool job = false;
     int app = 0;
@@ -711,8 +712,7 @@ void wide_densify(mrg_ctx *c, uint64_t extra) {
 // L2 leaf id of every record.  Takes ownership of K1 (kept in c->wide), bstart, spl1, bid, wk*.
 void wide_finish(mrg_ctx *c, LongItems li, uint64_t n, uint64_t nw, uint32_t B1, uint32_t B1r, uint64_t *K1,
                  uint64_t *bstart, uint64_t *spl1, uint16_t *bid, uint64_t *wk0, uint64_t *wk1, uint64_t *wcnt,
-                 uint32_t *wpart, bool dbg, hipEvent_t *pe, int &npe, const uint64_t *rin, const uint32_t *soff,
-                 uint32_t grid, uint32_t wcap) {
+                 uint32_t *wpart, bool dbg, hipEvent_t *pe, int &npe, const WmapIn &wm) {
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     const uint32_t R = c->R;
@@ -727,8 +727,7 @@ void wide_finish(mrg_ctx *c, LongItems li, uint64_t n, uint64_t nw, uint32_t B1,
     uint32_t *nleaf = pget<uint32_t>(p, B1);
     uint64_t *leaf_lo = pget<uint64_t>(p, NL + 1), *leaf_lb = pget<uint64_t>(p, 2 * NL + 2);
     const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", 256);
-    mrg_wide_launch_l2(rin ? nullptr : K1, K2, bstart, spl1, B1, B1r, target, nleaf, leaf_lo, leaf_lb, bid, s, rin,
-                       soff, grid, wcap);
+    mrg_wide_launch_l2(wm.rin ? nullptr : K1, K2, bstart, spl1, B1, B1r, target, nleaf, leaf_lo, leaf_lb, bid, s, wm);
     p.put(bid);
     mark();  // 4: L2
     // ---- leaves: aggregate + sort + line bytes (K1 becomes the output key array)
@@ -950,7 +949,7 @@ void wide_aggregate(mrg_ctx *c, const MapArgs &A, uint32_t nreg, uint32_t regcap
     p.put(cnt1); p.put(st2); p.put(cm); p.put(om); p.put(cf); p.put(of); p.put(st1); p.put(segptr);
     if (ix1) p.put(ix1);
     mark();  // 3: L1
-    wide_finish(c, li, n, nw, B1, B1r, K1, bstart, spl1, bid, wk0, wk1, wcnt, wpart, dbg, pe, npe, nullptr, nullptr, 0, 0);
+    wide_finish(c, li, n, nw, B1, B1r, K1, bstart, spl1, bid, wk0, wk1, wcnt, wpart, dbg, pe, npe, WmapIn{});
 }
 
 void need_job(mrg_ctx *c) {
@@ -986,7 +985,8 @@ void job_begin(mrg_ctx *c, int app, uint32_t R, uint32_t flags) {
 // a map that writes every short key to its L1 bucket (R partitions x B1r key ranges) -- the L1 count
 // and scatter passes over the map's records (wide_aggregate) disappear; L2 reads the regions.
 struct WideMapPlan {
-    bool on = false, forced = false;
+    bool on = false, forced = false, w12 = false;
+    uint64_t n16 = 0, S = 0;  // sampled keys of 13..16 bytes, samples
     uint32_t B1 = 0, B1r = 0;
     uint64_t *spl1 = nullptr;
     uint8_t *ix1 = nullptr;
@@ -1010,8 +1010,8 @@ WideMapPlan wide_map_plan(mrg_ctx *c, const uint64_t *d_doc_off, uint32_t nd, ui
     const uint32_t S = (uint32_t)std::min<uint64_t>(64ull * B1, 1u << 20);
     SortRec *sa = pget<SortRec>(p, S), *sb = pget<SortRec>(p, S);
     void *stmp = p.get(mrg_sort_tmp_bytes(S));
-    unsigned long long *dups = pget<unsigned long long>(p, 1);
-    HIPCHK(hipMemsetAsync(dups, 0, 8, s));
+    unsigned long long *dups = pget<unsigned long long>(p, 2);
+    HIPCHK(hipMemsetAsync(dups, 0, 16, s));
     mrg_wide_launch_sample_text(c->d_in, d_doc_off, nd, total, S, R, sa, s);
     SortPlan plan{};
     plan.use_part = R > 1;
@@ -1029,9 +1029,10 @@ WideMapPlan wide_map_plan(mrg_ctx *c, const uint64_t *d_doc_off, uint32_t nd, ui
             mrg_wide_launch_l1ix(spl1, R, B1r, ix1, s);
         }
     }
-    unsigned long long nd_h = 0;
-    HIPCHK(hipMemcpyAsync(&nd_h, dups, 8, hipMemcpyDeviceToHost, s));
+    unsigned long long dh[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(dh, dups, 16, hipMemcpyDeviceToHost, s));
     sync(c);
+    const unsigned long long nd_h = dh[0];
     p.put(sa); p.put(sb); p.put(stmp); p.put(dups);
     if (!P.forced && nd_h * 16 >= S) {  // repeats: the LDS combine pays
         p.put(spl1);
@@ -1040,6 +1041,12 @@ WideMapPlan wide_map_plan(mrg_ctx *c, const uint64_t *d_doc_off, uint32_t nd, ui
         return P;
     }
     P.on = true;
+    // 12-byte regions when keys of 13..16 bytes are rare (under 1 in 256 sampled tokens): those go to
+    // per-bucket lists of 16-byte records (MRG_TEST_WMAP_W12=0/1 overrides)
+    P.n16 = dh[1];
+    P.S = S;
+    P.w12 = !c->w12_off && dh[1] * 256 < S;
+    if (const char *e = getenv("MRG_TEST_WMAP_W12")) P.w12 = atoi(e) != 0;
     P.B1 = B1;
     P.B1r = B1r;
     P.spl1 = spl1;
@@ -1060,9 +1067,14 @@ void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_
     uint64_t lcap = std::max<uint64_t>(c->long_hint, total / 1024 + 1024);
     MapArgs A{};
     MapBufs M;
-    uint64_t *wrec = nullptr;
-    uint32_t *wcnt = nullptr;
+    uint64_t *wrec = nullptr, *wl16 = nullptr;
+    uint32_t *wcnt = nullptr, *wl16n = nullptr;
     uint32_t launches = 0;
+    bool w12 = wp.w12;
+    // the 16-byte lists of 12-byte regions: four times the sampled share of such keys, at least 2 K each
+    uint64_t wl16cap = std::max<uint64_t>(2048, (uint64_t)(4.0 * (double)total / 10.0 / (double)B1 *
+                                                            (double)(wp.n16 + 1) / (double)std::max<uint64_t>(wp.S, 1)));
+    if (const uint64_t t = env_u64("MRG_TEST_WMAP_L16", 0)) wl16cap = t;
     for (;;) {
         if (wcap > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
         M.dargs = pget<MapArgs>(p, 1);
@@ -1077,8 +1089,15 @@ void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_
         A = MapArgs{};
         A.kwords = (uint32_t)(MRG_MAP_NSUB * per_wg_blocks);
         M.gbits = pget<uint32_t>(p, (uint64_t)grid * A.kwords);
-        wrec = pget<uint64_t>(p, 2ull * B1 * (uint64_t)grid * wcap + 2);
+        const uint64_t nslots = (uint64_t)B1 * grid * wcap;
+        wrec = pget<uint64_t>(p, w12 ? (12 * nslots + 16 + 7) / 8 : 2 * nslots + 2);
         wcnt = pget<uint32_t>(p, (uint64_t)B1 * grid);
+        if (w12) {
+            if (wl16cap > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
+            wl16 = pget<uint64_t>(p, 2ull * B1 * wl16cap + 2);
+            wl16n = pget<uint32_t>(p, B1);
+            HIPCHK(hipMemsetAsync(wl16n, 0, 4ull * B1, s));
+        }
         A.in = c->d_in;
         A.doc_off = d_doc_off;
         A.chunk_base = d_cb;
@@ -1092,6 +1111,7 @@ void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_
         A.hash_bits = hash_bits(c);
         A.wrec = wrec; A.wcnt = wcnt; A.wspl = wp.spl1; A.wix = wp.ix1;
         A.wR = c->R; A.wB1r = wp.B1r; A.wcap = (uint32_t)wcap;
+        A.w12 = w12 ? 1u : 0u; A.wl16cap = (uint32_t)wl16cap; A.wl16 = wl16; A.wl16n = wl16n;
         HIPCHK(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long) * CNT_N, s));
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_ERRPOS], 0xFF, sizeof(unsigned long long), s));
         ev_rec(c, 0);
@@ -1103,7 +1123,12 @@ void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_
         read_counters(c);
         const uint64_t nl = c->h_cnt[CNT_LONG];
         const bool long_full = c->h_cnt[CNT_LONGX] > A.lovf;
-        if (c->h_cnt[CNT_OVF] == 0 && !long_full) break;
+        const bool l16_full = c->h_cnt[CNT_W16] != 0;
+        if (c->h_cnt[CNT_OVF] == 0 && !long_full && !l16_full) break;
+        if (l16_full) {  // too many keys of 13..16 bytes for the lists: 16-byte regions from now on
+            w12 = false;
+            c->w12_off = true;
+        }
         if (c->h_cnt[CNT_OVF]) {  // a region overflowed: every region sized to the largest demand
             std::vector<uint32_t> wc((uint64_t)B1 * grid);
             HIPCHK(hipMemcpyAsync(wc.data(), wcnt, 4ull * wc.size(), hipMemcpyDeviceToHost, s));
@@ -1123,8 +1148,9 @@ void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_
             fprintf(stderr, "[mrgpu] wide map rerun: region overflow %llu (cap now %llu), long %llu\n",
                     (unsigned long long)c->h_cnt[CNT_OVF], (unsigned long long)wcap, (unsigned long long)nl);
         M.release(p);
-        p.put(wrec);
-        p.put(wcnt);
+        p.put(wrec); p.put(wcnt); p.put(wl16); p.put(wl16n);
+        wl16 = nullptr;
+        wl16n = nullptr;
     }
     c->st.ms_map = ev_ms(c, 0, 1);
     c->st.map_launches = launches;
@@ -1138,7 +1164,7 @@ void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_
     const uint64_t errpos = c->h_cnt[CNT_ERRPOS];
     auto release_all = [&]() {
         M.release(p);
-        p.put(wrec); p.put(wcnt);
+        p.put(wrec); p.put(wcnt); p.put(wl16); p.put(wl16n);
         p.put(d_doc_off); p.put(d_cb); p.put(d_ids);
     };
     if (errpos != ~0ull) {
@@ -1161,12 +1187,12 @@ void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_
     }
     li.start = M.dstart; li.rawlen = M.dlen; li.doc = M.ddoc;
     // ---- the regions as L1 buckets: per-bucket segment starts, bucket offsets, then L2 and the leaves
-    uint32_t *soff = pget<uint32_t>(p, (uint64_t)B1 * (grid + 1));
+    uint32_t *soff = pget<uint32_t>(p, (uint64_t)B1 * (grid + 2));
     uint64_t *nbk = pget<uint64_t>(p, (uint64_t)B1 + 1);
     uint64_t *bstart = pget<uint64_t>(p, (uint64_t)B1 + 1);
     uint64_t *tmp = pget<uint64_t>(p, mrg_scan_tmp_elems((uint64_t)B1 + 1));
     HIPCHK(hipMemsetAsync(nbk + B1, 0, 8, s));
-    mrg_wmap_launch_seg(wcnt, B1, (uint32_t)grid, (uint32_t)wcap, soff, nbk, s);
+    mrg_wmap_launch_seg(wcnt, B1, (uint32_t)grid, (uint32_t)wcap, w12 ? wl16n : nullptr, (uint32_t)wl16cap, soff, nbk, s);
     mrg_scan_u64(nbk, bstart, (uint64_t)B1 + 1, tmp, s);  // bstart[B1] = records
     uint64_t n = 0;
     HIPCHK(hipMemcpyAsync(&n, bstart + B1, 8, hipMemcpyDeviceToHost, s));
@@ -1182,8 +1208,10 @@ void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_
     int npe = 0;
     c->st.agg_path = 2;
     c->spec_agg = false;
-    wide_finish(c, li, n, 0, B1, wp.B1r, K1, bstart, wp.spl1, bid, wk0, wk1, wk, wpart, dbg, pe, npe, wrec, soff,
-                (uint32_t)grid, (uint32_t)wcap);
+    WmapIn wm;
+    wm.rin = wrec; wm.soff = soff; wm.grid = (uint32_t)grid; wm.wcap = (uint32_t)wcap;
+    wm.w12 = w12 ? 1u : 0u; wm.wl16cap = (uint32_t)wl16cap; wm.wl16 = wl16;
+    wide_finish(c, li, n, 0, B1, wp.B1r, K1, bstart, wp.spl1, bid, wk0, wk1, wk, wpart, dbg, pe, npe, wm);
     p.put(soff); p.put(nbk); p.put(tmp); p.put(wp.ix1);
     c->st.map_kind = 1;
     ev_rec(c, 3);

@@ -112,14 +112,16 @@ def test_c5_slice_vs_oracle(ctx):
         assert got2[r] == exp[r], r
 
 
-@pytest.mark.parametrize("knob", [{}, {"MRG_TEST_WMAP_CAP": 2}, {"MRG_TEST_WMAP_B1R": 1}, {"MRG_TEST_WMAP_B1R": 3}])
+@pytest.mark.parametrize("knob", [{}, {"MRG_TEST_WMAP_CAP": 2}, {"MRG_TEST_WMAP_B1R": 1}, {"MRG_TEST_WMAP_B1R": 3},
+                                  {"MRG_TEST_WMAP_W12": 0}, {"MRG_TEST_WMAP_W12": 1, "MRG_TEST_WMAP_L16": 1}])
 def test_wide_map_forced_vs_oracle(ctx, corpus, knobs, knob):
     """The wide map forced on (MRG_WIDE_MAP=1): every short key goes from the map straight to its L1
     bucket (SipHash-1-3 partition, then the splitters of a sample of the input), L2 reads the map's
     regions.  C1 golden digests at R = 1/10/64; near-unique, Unicode and long-key documents, and forced
     internal hash collisions, against the oracle.  Knobs: regions of 2 records (every region overflows:
     the launch reruns with regions sized to the demand), one bucket per partition (B1r = 1), three
-    (binary splitter search instead of the index)."""
+    (binary splitter search instead of the index), 16-byte regions only (W12=0), and 12-byte regions
+    whose lists of 13..16-byte keys hold one record each (the launch reruns with 16-byte regions)."""
     import torch
     import oracle_lib as O
     import mapreduce_rust_amd as M
@@ -136,11 +138,14 @@ def test_wide_map_forced_vs_oracle(ctx, corpus, knobs, knob):
     t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
     ctx.gen_unique(t.data_ptr(), n, 0xC5, 3)
     docs = [t[:n].cpu().numpy().tobytes()] + _long_token_docs(5, n_docs=2, n_tokens=20_000) + [
-        "naïve café ’tis Ærø ſtraße 東京 — x".encode() * 300]
+        "naïve café ’tis Ærø ſtraße 東京 — x".encode() * 300, _mixed_keys_doc(11, 50_000)]
     for R in (7, 64):
         exp = O.wc(docs, R, O.FAST)
         assert run_wc(ctx, docs, R) == exp, R
-        assert ctx.stats()["map_kind"] == 1
+        st = ctx.stats()
+        assert st["map_kind"] == 1
+        if knob.get("MRG_TEST_WMAP_L16"):
+            assert st["map_launches"] >= 2, st
     assert run_wc(ctx, docs, 10, flags=M.debug_hash_bits(4)) == O.wc(docs, 10, O.FAST)
 
 
@@ -161,7 +166,7 @@ def knobs():
     keys = ["MRG_TEST_TAIL_CAP", "MRG_TEST_OVF_CAP", "MRG_TEST_AGG_OCAP", "MRG_WIDE", "MRG_TEST_LEAF_CAP",
             "MRG_TEST_LEAF_TARGET", "MRG_TEST_SORT_LCAP", "MRG_TEST_AGG_WIDE_OVF", "MRG_TEST_AGG_NSUB",
             "MRG_TEST_NO_PACK", "MRG_TEST_LONG_PER", "MRG_TEST_LONG_LIST", "MRG_WIDE_MAP", "MRG_TEST_WMAP_CAP",
-            "MRG_TEST_WMAP_B1R"]
+            "MRG_TEST_WMAP_B1R", "MRG_TEST_WMAP_W12", "MRG_TEST_WMAP_L16"]
     saved = {k: os.environ.get(k) for k in keys}
 
     def set_(**kw):
