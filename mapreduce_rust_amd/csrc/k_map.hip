@@ -175,12 +175,22 @@ __device__ __forceinline__ TileInfo sub_tile(const BlkInfo &b, uint32_t j) {
     return t;
 }
 
+// timing variants only: an ablation compiled in as a constant (the product build: 0)
+#ifndef MRG_MAP_ABL_CONST
+#define MRG_MAP_ABL_CONST 0u
+#endif
+// per-wave dedup of a round's repeated keys (timing variant, MRG_MAP_DEDUP = leader rounds; 0 = off):
+// see emit_fastN
+#ifndef MRG_MAP_DEDUP
+#define MRG_MAP_DEDUP 0
+#endif
+
 __device__ __forceinline__ uint32_t map_ablate(const MapArgs &A) {
 #ifdef MRG_MAP_ABLATION
     return A.ablate;
 #else
     (void)A;
-    return 0u;
+    return MRG_MAP_ABL_CONST;
 #endif
 }
 
@@ -271,7 +281,7 @@ struct LdsTable {
 
     // claim an empty way of set s0 (ways seen empty: e0, e1); true if the key got a slot and its count
     __device__ __forceinline__ bool claim(uint32_t s0, bool e0, bool e1, uint64_t a, uint64_t b, uint32_t d,
-                                          uint32_t h) {
+                                          uint32_t h, uint32_t add = 1u) {
         if (!admitted(h)) return false;
         for (uint32_t w = 0; w < 2; ++w) {
             if (!(w ? e1 : e0)) continue;
@@ -280,7 +290,7 @@ struct LdsTable {
             if (old == MRG_EMPTY_K0) {
                 key[s].b = b;
                 if (IDX) doc[s] = d;
-                atomicAdd(&cnt[s], 1u);
+                atomicAdd(&cnt[s], add);
                 atomicAdd(fill, 1u);
                 return true;
             }
@@ -437,6 +447,69 @@ __device__ __forceinline__ void emit_fastN(const MapArgs &A, uint32_t abl, uint3
     for (int t = 0; t < N; ++t) {
         h[t] = key_hash(k0[t], k1[t], dkey, hbits);
         act[t] = has[t] && !(abl & 2u);
+    }
+#if MRG_MAP_DEDUP
+    // Per-wave dedup (timing variant): MRG_MAP_DEDUP leader rounds over the round's N x 64 tokens.  A
+    // leader is the first token still pending; every token with the leader's key joins its group,
+    // skips the probe and the count add, and the leader adds the group's size.  When the leader
+    // misses the table, the members go to the tail with it (one record each, as without dedup).
+    uint32_t gadd[N], grp[N];
+    bool pend[N];
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+        gadd[t] = 1u;
+        grp[t] = 0xFFu;
+        pend[t] = act[t] && !IDX;
+    }
+    uint32_t gl_lane[MRG_MAP_DEDUP], gl_tok[MRG_MAP_DEDUP];
+#pragma unroll
+    for (int g = 0; g < MRG_MAP_DEDUP; ++g) {
+        gl_tok[g] = 0xFFu;
+        gl_lane[g] = 0;
+        uint64_t pm[N];
+#pragma unroll
+        for (int t = 0; t < N; ++t) pm[t] = __ballot(pend[t]);
+        int tl0 = -1;
+#pragma unroll
+        for (int t = N - 1; t >= 0; --t)
+            if (pm[t]) tl0 = t;
+        if (tl0 < 0) break;
+        uint64_t la = 0, lb = 0;
+        uint32_t src = 0;
+#pragma unroll
+        for (int t = 0; t < N; ++t)
+            if (t == tl0) {
+                src = (uint32_t)__builtin_ctzll(pm[t]);
+                la = __builtin_amdgcn_readlane(k0[t] & 0xFFFFFFFFull, src) |
+                     ((uint64_t)__builtin_amdgcn_readlane(k0[t] >> 32, src) << 32);
+                lb = __builtin_amdgcn_readlane(k1[t] & 0xFFFFFFFFull, src) |
+                     ((uint64_t)__builtin_amdgcn_readlane(k1[t] >> 32, src) << 32);
+            }
+        uint32_t gs = 0;
+        bool eq[N];
+#pragma unroll
+        for (int t = 0; t < N; ++t) {
+            eq[t] = pend[t] && k0[t] == la && k1[t] == lb;
+            gs += (uint32_t)__popcll(__ballot(eq[t]));
+        }
+        const uint32_t me = __lane_id();
+#pragma unroll
+        for (int t = 0; t < N; ++t) {
+            if (!eq[t]) continue;
+            pend[t] = false;
+            if (t == tl0 && me == src) {
+                gadd[t] = gs;
+            } else {
+                grp[t] = (uint32_t)g;
+                act[t] = false;   // a member: no probe, no count
+            }
+        }
+        gl_tok[g] = (uint32_t)tl0;
+        gl_lane[g] = src;
+    }
+#endif
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
         s[t] = act[t] ? (h[t] & (NS - 1)) : 0u;
         b[t] = bucket_of(h[t]);
         w16[t] = !IDX && (uint32_t)k1[t] != 0u;  // wc keys of 13..16 bytes: the 16-byte regions
@@ -458,7 +531,11 @@ __device__ __forceinline__ void emit_fastN(const MapArgs &A, uint32_t abl, uint3
     if (!(abl & 16u)) {
 #pragma unroll
         for (int t = 0; t < N; ++t)
+#if MRG_MAP_DEDUP
+            if (hit[t]) atomicAdd(&T.cnt[m0[t] ? s[t] : s[t] + NS], gadd[t]);
+#else
             if (hit[t]) atomicAdd(&T.cnt[m0[t] ? s[t] : s[t] + NS], 1u);
+#endif
     }
     // empty ways exist only until the table has filled (wave-uniform: a stale count only means
     // an unneeded test)
@@ -474,9 +551,27 @@ __device__ __forceinline__ void emit_fastN(const MapArgs &A, uint32_t abl, uint3
         if (__any(any)) {
 #pragma unroll
             for (int t = 0; t < N; ++t)
+#if MRG_MAP_DEDUP
+                if (need[t]) hit[t] = T.claim(s[t], e0[t], e1[t], k0[t], k1[t], dkey, h[t], gadd[t]);
+#else
                 if (need[t]) hit[t] = T.claim(s[t], e0[t], e1[t], k0[t], k1[t], dkey, h[t]);
+#endif
         }
     }
+#if MRG_MAP_DEDUP
+    // members take their leader's outcome (a leader that missed: every member to the tail)
+#pragma unroll
+    for (int g = 0; g < MRG_MAP_DEDUP; ++g) {
+        if (gl_tok[g] == 0xFFu) break;
+        uint32_t lh = 0;
+#pragma unroll
+        for (int t = 0; t < N; ++t)
+            if ((uint32_t)t == gl_tok[g]) lh = __builtin_amdgcn_readlane(hit[t] ? 1u : 0u, gl_lane[g]);
+#pragma unroll
+        for (int t = 0; t < N; ++t)
+            if (grp[t] == (uint32_t)g) hit[t] = lh != 0u;
+    }
+#endif
     bool tl[N], anyt = false;
 #pragma unroll
     for (int t = 0; t < N; ++t) {
@@ -789,7 +884,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
 #ifdef MRG_MAP_ABLATION
     const uint32_t abl = A.ablate;
 #else
-    constexpr uint32_t abl = 0;
+    constexpr uint32_t abl = MRG_MAP_ABL_CONST;
 #endif
     const uint32_t hbits = A.hash_bits;
     GAS uint64_t *const pool = gp(A.pool);
