@@ -1305,18 +1305,24 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
 // The common case: a leaf of at most W_VC items (records + weighted keys) is finished by ONE wave,
 // wave-synchronously (LDS traffic inside a wave is ordered; no workgroup barrier), so a CU keeps
 // eight independent leaves in flight.  Items sit in registers (W_VIPL per lane).
-//   digit   bit hb = the first bit the leaf's keys differ on splits them into two sides; inside
-//           each side the keys agree above that side's own first differing bit hs, so
-//           digit = side : the 8 key bits from hs  orders the keys (a window from hb alone collapses
-//           when the leaf straddles a carry such as '9' -> 'a' or 'o' -> 'p').
+//   digit   the three key bytes from the first byte the leaf's items differ on, each as its rank
+//           among the values present in the leaf, in mixed radix scaled to 512 (below)
 //   order   counting sort of the items by digit in LDS, then each item's rank inside its (small)
-//           bucket by comparisons (equal keys by bucket slot);
-//   runs    the sorted order is walked once: each run of equal keys becomes one distinct key, stored
-//           with its summed count at leaf_out + its rank among the distinct keys (stores coalesced).
+//           bucket by comparisons (equal keys by bucket slot), which also tells the item whether
+//           it heads its run of equal keys, and gives a head the run's summed count;
+//   runs    the heads in sorted order, each stored at leaf_out + its rank among the heads (stores
+//           coalesced).
 // Leaves with more items, or with a bucket of more than W_VMAXB items, are listed for k_wleaf.
 constexpr uint32_t W_VC = 448;
 constexpr uint32_t W_VIPL = W_VC / 64;
-constexpr uint32_t W_VND = 512;         // digits: side bit + 8 key bits
+constexpr uint32_t W_VND = 512;         // digits
+#ifndef MRG_WIDE_ABL
+#define MRG_WIDE_ABL 0
+#endif
+#ifndef MRG_WIDE_VRG
+#define MRG_WIDE_VRG 2
+#endif
+constexpr uint32_t W_VRG = MRG_WIDE_VRG; // rows whose buckets one trip of the rank loop reads
 constexpr uint32_t W_VMAXB = 64;
 constexpr uint32_t W_VQ = 4;            // waves (one-wave workgroups) per L1 bucket
 constexpr uint32_t W_VPASS = MRG_WIDE_MAXB2 / W_VQ;   // leaves one wave may pass on
@@ -1339,7 +1345,7 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
     typedef uint64_t v2 __attribute__((ext_vector_type(2)));
     __shared__ v2 s_kb[W_VC];            // items in digit-bucket order
     __shared__ uint32_t s_cb[W_VC];      // their counts (a leaf with a larger weighted count is passed on)
-    __shared__ uint16_t s_ix[W_VC];      // sorted position -> bucket slot
+    __shared__ __attribute__((aligned(16))) uint16_t s_ix[W_VC];   // sorted position -> bucket slot (and the digit code tables)
     __shared__ uint32_t s_dc[W_VND];     // digit counts
     __shared__ uint16_t s_ds[W_VND];     // digit starts
     __shared__ uint32_t s_pass[W_VPASS]; // leaves passed on to k_wleaf
@@ -1354,7 +1360,14 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
     GASW uint64_t *cout = gw(L.ocnt);
     unsigned long long keys = 0;
     uint32_t npass = 0;
+#ifdef MRG_WIDE_PROF  // diagnostic build: phase clocks of every wave, summed into L.prof[8..13]
+    uint64_t vacc[6] = {0, 0, 0, 0, 0, 0}, vtl = clock64();
+#define VP(i) { const uint64_t t_ = clock64(); vacc[i] += t_ - vtl; vtl = t_; }
+#else
+#define VP(i)
+#endif
     for (uint32_t j = q0; j < nl; j += W_VQ) {
+        VP(5);
         const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + j;
         const uint64_t mlo = L.leaf_lo[lid], mhi = j + 1 < nl ? L.leaf_lo[lid + 1] : bend;
         const uint64_t wlo = L.wr[2 * lid], whi = L.wr[2 * lid + 1];
@@ -1385,9 +1398,14 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
                 cnt[k] = L.wcnt[wlo + p - nm];
             }
         }
-        bool big = false;
+        // run totals are summed in 32-bit LDS words: a leaf whose counts add up to 2^32 or more goes to
+        // the workgroup kernel
+        uint64_t csum = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < W_VIPL; ++k) big |= cnt[k] > 0xFFFFFFFFull;
+        for (uint32_t k = 0; k < W_VIPL; ++k) csum += cnt[k];
+        for (int o = 32; o > 0; o >>= 1) csum += __shfl_xor(csum, o);
+        bool big = csum > 0xFFFFFFFFull;
+        VP(0);
         if (__any(big)) {   // a count beyond the LDS count width: the workgroup kernel
             if (lane == 0) s_pass[npass] = (uint32_t)lid;
             ++npass;
@@ -1436,36 +1454,58 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
                 }
             }
         } else {
-            // the other side's reference: the first item whose bit hb differs from f's
-            const uint32_t sf = key_bit(f.x, f.y, hb);
-            v2 g = f;
-            bool found = false;
+            // digit: the key bytes P, P + 1, P + 2 from the first byte the items differ on, each
+            // replaced by its rank among the values that byte takes in this leaf (a per-leaf code
+            // table in LDS), combined in mixed radix and scaled to W_VND digits (monotone: a
+            // multiply by a rounded-down reciprocal and a shift).  The items agree on every byte
+            // before P, so the digit orders them.  Text keys use ~36 of a byte's 256 values; dense
+            // codes spread a leaf's items over the digits (r04's 8 raw bits after each side's
+            // first differing bit held 7.5 items per bucket on letter keys: the rank loop below
+            // took 53 % of the wave cycles; simulated for C5 keys, profiles/r05/v47_*).
+            const uint32_t P = hb >> 3;
+            uint8_t *code = reinterpret_cast<uint8_t *>(s_ix);   // 3 x 256 bytes (s_ix is free until the rank step)
+            auto kbyte = [&](const v2 &k, uint32_t j) -> uint32_t {
+                return j < 8u ? (uint32_t)(k.x >> (56u - 8u * j)) & 0xFFu
+                              : (j < 16u ? (uint32_t)(k.y >> (56u - 8u * (j - 8u))) & 0xFFu : 0u);
+            };
+            for (uint32_t i = lane; i < 3u * 64u; i += 64) reinterpret_cast<uint32_t *>(code)[i] = 0;
+            wave_lds_sync();
 #pragma unroll
             for (uint32_t k = 0; k < W_VIPL; ++k) {
-                const uint64_t m = __ballot(key_bit(key[k].x, key[k].y, hb) != sf);
-                if (m && !found) {
-                    const int src = __ffsll((long long)m) - 1;
-                    g = v2{__shfl(key[k].x, src), __shfl(key[k].y, src)};
-                    found = true;
-                }
+                if ((uint64_t)k * 64u + lane >= NT) continue;
+#pragma unroll
+                for (uint32_t t = 0; t < 3; ++t) code[256u * t + kbyte(key[k], P + t)] = 1;
             }
-            uint64_t a0 = 0, a1 = 0, c0 = 0, c1 = 0;   // OR (key ^ reference) of side sf, of the other side
+            wave_lds_sync();
+            uint32_t nv[3];
+#pragma unroll
+            for (uint32_t t = 0; t < 3; ++t) {   // presence -> rank among the present values
+                uint32_t *cw = reinterpret_cast<uint32_t *>(code + 256u * t);
+                const uint32_t w = cw[lane];
+                const uint32_t c = (w & 1u) + ((w >> 8) & 1u) + ((w >> 16) & 1u) + (w >> 24);
+                const uint32_t inc = wave_scan_incl(c);
+                uint32_t r = inc - c, o = 0;
+#pragma unroll
+                for (uint32_t bb = 0; bb < 4; ++bb) {
+                    o |= r << (8u * bb);
+                    r += (w >> (8u * bb)) & 1u;
+                }
+                cw[lane] = o;
+                nv[t] = (uint32_t)__shfl(inc, 63);
+            }
+            const uint32_t N = nv[0] * nv[1] * nv[2];
+            const uint64_t Mr = N > W_VND ? ((uint64_t)W_VND << 32) / N : (1ull << 32);
+            wave_lds_sync();
+            uint32_t dgv[W_VIPL];
 #pragma unroll
             for (uint32_t k = 0; k < W_VIPL; ++k) {
-                if (key_bit(key[k].x, key[k].y, hb) == sf) {
-                    a0 |= key[k].x ^ f.x;
-                    a1 |= key[k].y ^ f.y;
-                } else {
-                    c0 |= key[k].x ^ g.x;
-                    c1 |= key[k].y ^ g.y;
-                }
+                const uint32_t c0 = code[kbyte(key[k], P)], c1 = code[256u + kbyte(key[k], P + 1u)],
+                               c2 = code[512u + kbyte(key[k], P + 2u)];
+                const uint32_t x = (c0 * nv[1] + c1) * nv[2] + c2;
+                dgv[k] = (uint32_t)(((uint64_t)x * Mr) >> 32);
             }
-            a0 = wave_or(a0);
-            a1 = wave_or(a1);
-            c0 = wave_or(c0);
-            c1 = wave_or(c1);
-            const uint32_t hf = min(first_bit(a0, a1), 120u), hg = min(first_bit(c0, c1), 120u);
             for (uint32_t i = lane; i < W_VND; i += 64) s_dc[i] = 0;
+            VP(1);
             wave_lds_sync();
             uint32_t dg[W_VIPL], wi[W_VIPL];
 #pragma unroll
@@ -1473,11 +1513,7 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
                 dg[k] = 0xFFFFFFFFu;
                 wi[k] = 0;
                 if ((uint64_t)k * 64u + lane < NT) {
-                    const uint32_t sd = key_bit(key[k].x, key[k].y, hb);
-                    const uint32_t hs = sd == sf ? hf : hg;
-                    const uint64_t t = hs == 0 ? key[k].x
-                                       : (hs < 64 ? (key[k].x << hs) | (key[k].y >> (64 - hs)) : key[k].y << (hs - 64));
-                    dg[k] = (sd << 8) | (uint32_t)(t >> 56);
+                    dg[k] = dgv[k];
                     wi[k] = atomicAdd(&s_dc[dg[k]], 1u);
                 }
             }
@@ -1499,6 +1535,16 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
                     run += v[x];
                 }
                 for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
+#ifdef MRG_WIDE_PROF
+                uint32_t nz = 0;
+#pragma unroll
+                for (uint32_t x = 0; x < PT; ++x) nz += v[x] != 0u ? 1u : 0u;
+                for (int o = 32; o > 0; o >>= 1) nz += (uint32_t)__shfl_xor(nz, o);
+                if (lane == 0) {
+                    atomicAdd(&L.prof[14], (unsigned long long)nz);
+                    atomicAdd(&L.prof[15], (unsigned long long)mx);
+                }
+#endif
             }
             if (mx > W_VMAXB) {   // many equal (or near-equal) keys: the workgroup kernel
                 if (lane == 0) s_pass[npass] = (uint32_t)lid;
@@ -1510,6 +1556,7 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
                 continue;
             }
             wave_lds_sync();
+            VP(2);
             uint32_t slot[W_VIPL];
 #pragma unroll
             for (uint32_t k = 0; k < W_VIPL; ++k) {
@@ -1520,68 +1567,78 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
                 s_cb[slot[k]] = (uint32_t)cnt[k];
             }
             wave_lds_sync();
+            // rank inside the bucket by comparisons (equal keys by bucket slot); an item with an equal
+            // key in an earlier slot is not its run's head (flag 0x8000 in s_ix); a head with equal
+            // keys after it stores the run's summed count in its own s_cb slot (the other members
+            // never write, and what they read is unused)
+            // every row's bucket walked in one loop (trip q reads position q of all W_VIPL buckets: one
+            // LDS wait per trip instead of one per row and position)
+            // rank: the items of the bucket before this one, equal keys ordered by bucket slot; fq = the
+            // first slot (in the bucket) holding this item's key, so the item heads its run iff fq == wi.
+            // A run's other members add their counts to the head's count slot afterwards (an LDS
+            // atomic, rare).  Per-row state stays in VGPRs: bool arrays here became SGPR lane masks in
+            // a kernel already at the SGPR limit, and their spills cost more than the loop.
+            uint32_t bs[W_VIPL], bn[W_VIPL], rank[W_VIPL], fq[W_VIPL];
+#pragma unroll
+            for (uint32_t k = 0; k < W_VIPL; ++k) {
+                const bool v = dg[k] != 0xFFFFFFFFu;
+                bs[k] = v ? s_ds[dg[k]] : 0u;
+                bn[k] = v ? s_dc[dg[k]] : 0u;
+                rank[k] = 0;
+                fq[k] = wi[k];
+            }
+#pragma unroll
+            for (uint32_t g0 = 0; g0 < W_VIPL; g0 += W_VRG) {
+            uint32_t gmax = 0;
+#pragma unroll
+            for (uint32_t k = g0; k < g0 + W_VRG && k < W_VIPL; ++k) gmax = max(gmax, bn[k]);
+#if MRG_WIDE_ABL & 1   // timing only: no rank loop
+            gmax = 0;
+#endif
+            for (uint32_t q = 0; __any(q < gmax); ++q) {
+                v2 x[W_VRG];
+#pragma unroll
+                for (uint32_t k = g0; k < g0 + W_VRG && k < W_VIPL; ++k) x[k - g0] = s_kb[min(bs[k] + q, W_VC - 1u)];
+#pragma unroll
+                for (uint32_t kk = 0; kk < W_VRG; ++kk) {
+                    const uint32_t k = g0 + kk;
+                    if (k >= W_VIPL || q >= bn[k]) continue;
+                    const bool eq = x[kk].x == key[k].x && x[kk].y == key[k].y;
+                    const bool before = key_lt(x[kk].x, x[kk].y, key[k].x, key[k].y) || (eq && q < wi[k]);
+                    rank[k] += before ? 1u : 0u;
+                    fq[k] = (eq && q < fq[k]) ? q : fq[k];
+                }
+            }
+            }
 #pragma unroll
             for (uint32_t k = 0; k < W_VIPL; ++k) {
                 if (dg[k] == 0xFFFFFFFFu) continue;
-                const uint32_t bs = s_ds[dg[k]], bn = s_dc[dg[k]];
-                uint32_t rank = 0;
-                for (uint32_t q = 0; q < bn; ++q) {
-                    const v2 x = s_kb[bs + q];
-                    rank += (key_lt(x.x, x.y, key[k].x, key[k].y) ||
-                             (x.x == key[k].x && x.y == key[k].y && q < wi[k])) ? 1u : 0u;
-                }
-                s_ix[bs + rank] = (uint16_t)slot[k];
+                const bool member = fq[k] != wi[k];
+                s_ix[bs[k] + rank[k]] = (uint16_t)(slot[k] | (member ? 0x8000u : 0u));
+                if (member) atomicAdd(&s_cb[bs[k] + fq[k]], (uint32_t)cnt[k]);
             }
             wave_lds_sync();
-            // runs of equal keys in sorted order (position p = k * 64 + lane): every position's key
-            // and count in registers first (independent reads); the previous / next position's key
-            // comes from the neighbour lane (lane 0 / 63: the last / first lane of row k - 1 / k + 1)
+            VP(3);
+            // the heads in sorted order (position p = k * 64 + lane): each is one distinct key, stored
+            // at its rank among the heads
+            uint32_t e[W_VIPL];
+#pragma unroll
+            for (uint32_t k = 0; k < W_VIPL; ++k) e[k] = k * 64u + lane < NT ? s_ix[k * 64u + lane] : 0x8000u;
             v2 xs[W_VIPL];
-            uint64_t cs[W_VIPL];
-            {
-                uint32_t sl[W_VIPL];
-#pragma unroll
-                for (uint32_t k = 0; k < W_VIPL; ++k) sl[k] = k * 64u + lane < NT ? s_ix[k * 64u + lane] : 0u;
-#pragma unroll
-                for (uint32_t k = 0; k < W_VIPL; ++k) {
-                    xs[k] = s_kb[sl[k]];
-                    cs[k] = s_cb[sl[k]];
-                }
-            }
-            bool head[W_VIPL];
+            uint32_t cs[W_VIPL];
 #pragma unroll
             for (uint32_t k = 0; k < W_VIPL; ++k) {
-                const uint32_t p = k * 64u + lane;
-                // every lane takes part in every shuffle (a shuffle inside a branch reads inactive lanes)
-                const uint32_t kp = k > 0 ? k - 1 : 0;
-                const uint64_t z0 = __shfl(xs[kp].x, 63), z1 = __shfl(xs[kp].y, 63);
-                uint64_t y0 = __shfl_up(xs[k].x, 1), y1 = __shfl_up(xs[k].y, 1);
-                if (lane == 0) {
-                    y0 = z0;
-                    y1 = z1;
-                }
-                head[k] = p < NT && (p == 0 || y0 != xs[k].x || y1 != xs[k].y);
+                xs[k] = s_kb[e[k] & 0x7FFFu];
+                cs[k] = s_cb[e[k] & 0x7FFFu];
             }
 #pragma unroll
             for (uint32_t k = 0; k < W_VIPL; ++k) {
-                const uint32_t p = k * 64u + lane;
-                // is position p + 1 the start of another run (or the end)?
-                const bool dn = __shfl_down(head[k] ? 1u : 0u, 1) != 0u;
-                const bool nx = k + 1 < W_VIPL ? __shfl(head[k + 1 < W_VIPL ? k + 1 : k] ? 1u : 0u, 0) != 0u : true;
-                const bool nh = (lane == 63 ? nx : dn) || p + 1 >= NT;
-                const uint64_t hm = __ballot(head[k]);
-                if (head[k]) {
+                const bool head = (e[k] & 0x8000u) == 0u;
+                const uint64_t hm = __ballot(head);
+                if (head) {
                     const uint32_t dpos = D + (uint32_t)__popcll(hm & lt);
                     const v2 x = xs[k];
-                    uint64_t n = cs[k];
-                    if (!nh) {   // equal keys follow (rare): sum the run
-                        for (uint32_t q = p + 1; q < NT; ++q) {
-                            const uint32_t s2 = s_ix[q];
-                            const v2 y = s_kb[s2];
-                            if (y.x != x.x || y.y != x.y) break;
-                            n += s_cb[s2];
-                        }
-                    }
+                    const uint64_t n = cs[k];
                     if (pk) {
                         ko[dpos] = v2{x.x, x.y | n};
                     } else {
@@ -1595,6 +1652,7 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
                 D += (uint32_t)__popcll(hm);
             }
         }
+        VP(4);
         if (D && my_last == D - 1) L.leaf_last[lid] = my_ll;
         for (int o = 32; o > 0; o >>= 1) bytes += __shfl_xor(bytes, o);
         if (lane == 0) {
@@ -1607,6 +1665,11 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
         keys += D;
         wave_lds_sync();
     }
+#ifdef MRG_WIDE_PROF
+    if (lane == 0)
+        for (int i = 0; i < 6; ++i) atomicAdd(&L.prof[8 + i], (unsigned long long)vacc[i]);
+#endif
+#undef VP
     // the passed-on leaves, with one device atomic per wave
     if (npass) {
         wave_lds_sync();

@@ -367,7 +367,7 @@ struct WideLeafArgs {
     unsigned long long *ovf_n;
     unsigned long long *nkeys;   // += distinct keys of every finished leaf
     uint64_t *wr;                // [B1 * MRG_WIDE_MAXB2][2] scratch: weighted-key range of each leaf
-    unsigned long long *prof;    // diagnostics (builds with -DMRG_WIDE_PROF): leaf phase clocks [8]
+    unsigned long long *prof;    // diagnostics (builds with -DMRG_WIDE_PROF): leaf phase clocks [16]
     uint32_t *big_list;          // [B1 * MRG_WIDE_MAXB2] leaves passed from the one-wave to the workgroup kernel
     unsigned long long *big_n;   // their count (zeroed by the caller)
     uint32_t *leaf_pk;           // [B1 * MRG_WIDE_MAXB2] 1: the leaf's counts are packed into its key slots (zeroed by the caller)

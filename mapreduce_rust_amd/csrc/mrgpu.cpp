@@ -756,8 +756,8 @@ void wide_finish(mrg_ctx *c, LongItems li, uint64_t n, uint64_t nw, uint32_t B1,
     L.ocnt = w.ocnt; L.leaf_out = w.leaf_out; L.leaf_nd = w.leaf_nd; L.leaf_bytes = w.leaf_bytes;
     L.leaf_last = w.leaf_last; L.ovf_list = ovf_list; L.ovf_n = &c->d_cnt[CNT_OVF2]; L.nkeys = &c->d_cnt[CNT_KEYS];
     L.wr = pget<uint64_t>(p, 2 * NL);
-    L.prof = pget<unsigned long long>(p, 8);
-    HIPCHK(hipMemsetAsync(L.prof, 0, 64, s));
+    L.prof = pget<unsigned long long>(p, 16);
+    HIPCHK(hipMemsetAsync(L.prof, 0, 128, s));
     L.big_list = pget<uint32_t>(p, NL);
     L.big_n = pget<unsigned long long>(p, 1);
     L.leaf_pk = w.leaf_pk;
@@ -784,7 +784,7 @@ void wide_finish(mrg_ctx *c, LongItems li, uint64_t n, uint64_t nw, uint32_t B1,
         }
         fprintf(stderr, "\n");
         for (int i = 0; i < npe; ++i) (void)hipEventDestroy(pe[i]);
-        unsigned long long pr[8], nbig = 0;
+        unsigned long long pr[16], nbig = 0;
         HIPCHK(hipMemcpy(pr, L.prof, sizeof pr, hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(&nbig, L.big_n, 8, hipMemcpyDeviceToHost));
         fprintf(stderr, "[mrgpu] wide: %llu passed to the workgroup kernel (%llu by size, %llu by bucket)\n", nbig,
@@ -812,6 +812,13 @@ void wide_finish(mrg_ctx *c, LongItems li, uint64_t n, uint64_t nw, uint32_t B1,
             fprintf(stderr, "[mrgpu] leaf phase clocks (wave 0, all WGs): clear %.3g insert %.3g list %.3g digits %.3g "
                             "order %.3g write %.3g\n", (double)pr[0], (double)pr[1], (double)pr[2], (double)pr[3],
                     (double)pr[4], (double)pr[5]);
+        if (pr[8] | pr[12])
+            fprintf(stderr, "[mrgpu] one-wave leaf phase clocks (all waves): load %.3g bits %.3g digits %.3g order %.3g "
+                            "runs %.3g stats %.3g\n", (double)pr[8], (double)pr[9], (double)pr[10], (double)pr[11],
+                    (double)pr[12], (double)pr[13]);
+        if (pr[14])
+            fprintf(stderr, "[mrgpu] one-wave leaves: digits used %.3g, largest digit bucket %.3g (sums)\n", (double)pr[14],
+                    (double)pr[15]);
     }
     if (getenv("MRG_DEBUG"))
         fprintf(stderr, "[mrgpu] wide: %llu records, %llu weighted, B1 %u (x%u), %llu distinct, %llu leaves overflowed\n",
