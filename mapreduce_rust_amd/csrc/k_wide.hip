@@ -483,6 +483,12 @@ __device__ __forceinline__ void seg_record(const L2Args &L, uint32_t b, const ui
     seg_load(L, b, lo, i - so[lo], k0, k1);
 }
 
+#ifdef MRG_WIDE_PROF  // diagnostic build: L2 phase clocks of thread 0 of every workgroup
+__device__ unsigned long long g_l2prof[8];
+#define L2P(i) { if (tid == 0) { const uint64_t t_ = clock64(); l2acc[i] += t_ - l2t; l2t = t_; } }
+#else
+#define L2P(i)
+#endif
 template <bool SEG>
 __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     __shared__ uint64_t s_smp[2 * W_S2];            // samples (k0, k1), bitonic-sorted
@@ -495,10 +501,14 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     __shared__ uint32_t s_ws[W_NW];
     __shared__ uint32_t s_cseg[SEG ? W_MAXSEG + 2 : 1];   // SEG: the bucket's segment starts
     const uint32_t tid = threadIdx.x, b = blockIdx.x;
+#ifdef MRG_WIDE_PROF
+    uint64_t l2acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, l2t = clock64();
+#endif
     if (SEG) {
         for (uint32_t w = tid; w <= L.grid + 1u; w += W_WG) s_cseg[w] = L.soff[(uint64_t)b * (L.grid + 2u) + w];
         lds_barrier();
     }
+    L2P(0);
     const uint64_t base = L.bstart[b], nb = L.bstart[b + 1] - base;
     uint32_t B2 = (uint32_t)min<uint64_t>((nb + L.target - 1) / L.target, MRG_WIDE_MAXB2);
     if (B2 < 1) B2 = 1;
@@ -523,6 +533,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
             s_smp[2 * k + 1] = c;
         }
         lds_barrier();
+        L2P(1);
         for (uint32_t size = 2; size <= P; size <<= 1) {
             for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
                 for (uint32_t t = tid; t < P / 2; t += W_WG) {
@@ -538,6 +549,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
                 lds_barrier();
             }
         }
+        L2P(2);
         for (uint32_t q = tid; q + 1 < B2; q += W_WG) {
             const uint32_t k = (uint32_t)(((uint64_t)(q + 1u) * S) / B2);
             s_spl[2 * q] = s_smp[2 * k];
@@ -555,6 +567,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     const LeafIndex si{s_spl, reinterpret_cast<const uint16_t *>(s_smp), B2 - 1u,
                        B2 > 1 ? LeafIndex::prefix_bits(s_spl, B2 - 1u) : 0u};
     auto sub_of = [&](uint64_t k0, uint64_t k1) { return B2 > 1 ? si.upper(k0, k1) : 0u; };
+    L2P(3);
     // ---- histogram (U records per thread in flight)
     constexpr int U = 4;
     typedef uint64_t v2 __attribute__((ext_vector_type(2)));
@@ -596,6 +609,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         }
     }
     lds_barrier();
+    L2P(4);
     {  // exclusive scan of the B2 <= 1024 counts, one per thread
         const uint32_t v = tid < B2 ? s_cnt[tid] : 0u;
         uint32_t tot;
@@ -622,6 +636,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         if (tid == 0) L.nleaf[b] = B2;
     }
     lds_barrier();
+    L2P(5);
     // ---- scatter, staged through LDS: a chunk of W_SC records is counting-sorted by leaf in LDS,
     // then stored so that consecutive threads write consecutive records of one leaf (a run of ~8
     // records per leaf per chunk instead of one 16-byte store per record at a random place: the
@@ -692,7 +707,13 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         lds_barrier();
         if (tid < B2) s_cur[tid] += s_cnt[tid];   // the thread that zeroes s_cnt[tid] next chunk
     }
+    L2P(6);
+#ifdef MRG_WIDE_PROF
+    if (tid == 0)
+        for (int i = 0; i < 7; ++i) atomicAdd(&g_l2prof[i], (unsigned long long)l2acc[i]);
+#endif
 }
+#undef L2P
 
 // ---------------------------------------------------------------- leaves
 struct LeafArgs {
@@ -1313,7 +1334,10 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
 //   runs    the heads in sorted order, each stored at leaf_out + its rank among the heads (stores
 //           coalesced).
 // Leaves with more items, or with a bucket of more than W_VMAXB items, are listed for k_wleaf.
-constexpr uint32_t W_VC = 448;
+#ifndef MRG_WIDE_VC
+#define MRG_WIDE_VC 448
+#endif
+constexpr uint32_t W_VC = MRG_WIDE_VC;
 constexpr uint32_t W_VIPL = W_VC / 64;
 constexpr uint32_t W_VND = 512;         // digits
 #ifndef MRG_WIDE_ABL
@@ -1797,16 +1821,18 @@ __global__ __launch_bounds__(W_WWG) void k_wwrite(const uint64_t *keys, const ui
     struct One {
         uint64_t a, c, n;
     };
+    // leaf l of key i: s_kst[l] <= i < s_kst[l + 1] (the last such l).  A thread's keys only move
+    // forward (by W_WCH per chunk), so its leaf is found by a forward walk from its previous one:
+    // about two LDS reads per chunk for leaves of ~250 keys (a binary search over the bucket's up to
+    // 1024 leaves was ten dependent reads per key)
+    uint32_t lcur = 0;
     auto fetch = [&](uint32_t c0, One &F) {
         const uint32_t i = c0 + tid;
         F.a = F.c = F.n = 0;
         if (i < K) {
-            uint32_t lo = 0, hi = nl;   // leaf l: s_kst[l] <= i < s_kst[l + 1] (last such l)
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_kst[mid] <= i) lo = mid;
-                else hi = mid;
-            }
+            uint32_t lo = lcur;
+            while (lo + 1u < nl && s_kst[lo + 1u] <= i) ++lo;
+            lcur = lo;
             const uint64_t lo_out = s_lout[lo];
             const uint64_t slot = (lo_out & ~(1ull << 63)) + (i - s_kst[lo]);
             F.a = keys[2 * slot];
@@ -2051,6 +2077,14 @@ void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstar
              wm.rin, wm.soff, wm.grid, wm.wcap, wm.w12, wm.wl16cap, wm.wl16};
     if (wm.rin) hipLaunchKernelGGL(k_wl2<true>, dim3(B1), dim3(W_WG), 0, s, L);
     else hipLaunchKernelGGL(k_wl2<false>, dim3(B1), dim3(W_WG), 0, s, L);
+}
+// diagnostic builds (-DMRG_WIDE_PROF): the L2 phase clocks summed so far (else zeros)
+void mrg_wide_l2_prof(unsigned long long out[8]) {
+#ifdef MRG_WIDE_PROF
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_l2prof), 8 * sizeof(unsigned long long));
+#else
+    for (int i = 0; i < 8; ++i) out[i] = 0;
+#endif
 }
 void mrg_wide_launch_weights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *wk0, uint64_t *wk1, uint64_t *wcnt,
                              uint32_t *wpart, hipStream_t s) {

@@ -393,6 +393,7 @@ struct WmapIn {
     uint32_t grid = 0, wcap = 0, w12 = 0, wl16cap = 0;
     const uint64_t *wl16 = nullptr;
 };
+void mrg_wide_l2_prof(unsigned long long out[8]);
 void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstart, const uint64_t *spl1, uint32_t B1,
                         uint32_t B1r, uint32_t target, uint32_t *nleaf, uint64_t *leaf_lo, uint64_t *leaf_lb,
                         uint16_t *sub, hipStream_t s, const WmapIn &wm = WmapIn{});

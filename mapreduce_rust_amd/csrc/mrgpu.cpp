@@ -816,6 +816,14 @@ void wide_finish(mrg_ctx *c, LongItems li, uint64_t n, uint64_t nw, uint32_t B1,
             fprintf(stderr, "[mrgpu] one-wave leaf phase clocks (all waves): load %.3g bits %.3g digits %.3g order %.3g "
                             "runs %.3g stats %.3g\n", (double)pr[8], (double)pr[9], (double)pr[10], (double)pr[11],
                     (double)pr[12], (double)pr[13]);
+        {
+            unsigned long long l2[8];
+            mrg_wide_l2_prof(l2);
+            if (l2[6])
+                fprintf(stderr, "[mrgpu] L2 phase clocks (thread 0, all WGs, cumulative): segs %.3g sample %.3g sort %.3g "
+                                "index %.3g hist %.3g scan %.3g scatter %.3g\n", (double)l2[0], (double)l2[1],
+                        (double)l2[2], (double)l2[3], (double)l2[4], (double)l2[5], (double)l2[6]);
+        }
         if (pr[14])
             fprintf(stderr, "[mrgpu] one-wave leaves: digits used %.3g, largest digit bucket %.3g (sums)\n", (double)pr[14],
                     (double)pr[15]);
