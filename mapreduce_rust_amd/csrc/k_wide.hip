@@ -35,6 +35,9 @@ __device__ __forceinline__ GASW T *gw(T *p) {
 constexpr int W_WG = 1024;
 constexpr int W_NW = W_WG / 64;
 constexpr uint32_t W_S2 = 8192;       // L2 samples per L1 bucket (sorted in LDS)
+#ifndef MRG_WIDE_L2U
+#define MRG_WIDE_L2U 4   // L2 histogram: records per thread in flight
+#endif
 constexpr uint32_t W_SC = 8192;       // L2 scatter chunk (staged in the samples' LDS)
 constexpr int W_LWG = 256;            // leaf workgroup (four per CU: while one waits on memory, others work)
 constexpr int W_LNW = W_LWG / 64;
@@ -569,7 +572,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     auto sub_of = [&](uint64_t k0, uint64_t k1) { return B2 > 1 ? si.upper(k0, k1) : 0u; };
     L2P(3);
     // ---- histogram (U records per thread in flight)
-    constexpr int U = 4;
+    constexpr int U = MRG_WIDE_L2U;
     typedef uint64_t v2 __attribute__((ext_vector_type(2)));
     const GASW v2 *inv = reinterpret_cast<const GASW v2 *>(in);
     if (SEG) {  // segment by segment, one wave each: reads stay inside a segment
@@ -1340,6 +1343,9 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
 constexpr uint32_t W_VC = MRG_WIDE_VC;
 constexpr uint32_t W_VIPL = W_VC / 64;
 constexpr uint32_t W_VND = 512;         // digits
+#ifndef MRG_WIDE_L2U
+#define MRG_WIDE_L2U 4
+#endif
 #ifndef MRG_WIDE_ABL
 #define MRG_WIDE_ABL 0
 #endif
