@@ -401,13 +401,22 @@ __device__ __forceinline__ void wide_store(const MapArgs &A, const TailRegions &
         return;
     }
     const uint32_t pos = atomicAdd(&R.wcur[b], 1u);
+    if ((MRG_MAP_ABL_CONST & 4096u) && pos != 0xFFFFFFFFu) return;   // timing variant only: no record store
     if (pos < A.wcap) {
         const uint64_t i = ((uint64_t)b * gridDim.x + blockIdx.x) * A.wcap + pos;
+#if MRG_MAP_ABL_CONST & 8192u   // timing variant: non-temporal record stores
+        if (A.w12)
+            __builtin_nontemporal_store(u32x3a{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)(k1 >> 32)},
+                                        reinterpret_cast<GAS u32x3a *>(reinterpret_cast<GAS uint8_t *>(gp(A.wrec)) + 12u * i));
+        else
+            __builtin_nontemporal_store(u64x2{k0, k1}, reinterpret_cast<GAS u64x2 *>(gp(A.wrec) + 2u * i));
+#else
         if (A.w12)
             *reinterpret_cast<GAS u32x3a *>(reinterpret_cast<GAS uint8_t *>(gp(A.wrec)) + 12u * i) =
                 u32x3a{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)(k1 >> 32)};
         else
             *reinterpret_cast<GAS u64x2 *>(gp(A.wrec) + 2u * i) = u64x2{k0, k1};
+#endif
     }
 }
 
