@@ -1158,7 +1158,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         // carries its class, so the W / S masks mean the same.  Invalid UTF-8 defers the block's tiles
         // to generic_tile after the main loop (which reports the first bad byte).
         bool defer_blk = false;
-        if (!(abl & 256u) && __any(n0 || n1 || (lane <= 1 && ne))) {
+        if (!(abl & 256u) && !(MRG_MAP_ABL_CONST & 0x20000u) && __any(n0 || n1 || (lane <= 1 && ne))) {
 #ifdef MRG_MAP_NO_UNI
             defer_blk = true;  // A/B builds only: every such block to the exact walker, as in r03
 #else
@@ -1244,7 +1244,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             uint32_t W0 = 0, S0 = 0, C0 = 0, W1 = 0, S1 = 0, C1 = 0;
             // one codepoint per lane and trip, the lane's two segments' leads in one mask (non-ASCII
             // text is sparse: most lanes have none, a few one)
-            for (uint32_t mAB = ld0 | (ld1 << 16); __any(mAB != 0u);) {
+            for (uint32_t mAB = (MRG_MAP_ABL_CONST & 0x10000u) ? 0u : (ld0 | (ld1 << 16)); __any(mAB != 0u);) {
                 if (mAB) {
                     const uint32_t q = (uint32_t)__builtin_ctz(mAB);
                     mAB &= mAB - 1u;
@@ -1301,7 +1301,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 W = (W | ((in >> 4) & 0xFu)) & 0xFFFFu;
                 S = (S | ((in >> 8) & 0xFu)) & 0xFFFFu;
                 C = (C | (in & 0xFu)) & 0xFFFFu;
-                bad |= C != nam;
+                if (!(MRG_MAP_ABL_CONST & 0x10000u)) bad |= C != nam;   // (0x10000: timing only, no decode)
                 return ((m & 0xFFFFu & ~nam) | W) | ((((m >> 16) & ~nam) | S) << 16);
             };
             m0 = fix(m0, nam0, W0, S0, C0, in0);
