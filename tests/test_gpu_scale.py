@@ -523,12 +523,15 @@ def test_two_ranks_library_exchange(tmp_path):
             assert merged[R][str(r)] == GOLDEN["wc"][R][f"mr-{r}.txt"], (R, r)
 
 
+@pytest.mark.parametrize("wmap", ["0", "1"])
 @pytest.mark.parametrize("cap,target", [("0", "1024"), ("8", "1024"), ("0", "16"), ("64", "100000")])
-def test_wide_sample_sort_knobs_vs_oracle(ctx, corpus, knobs, cap, target):
+def test_wide_sample_sort_knobs_vs_oracle(ctx, corpus, knobs, cap, target, wmap):
     """The wide aggregation (k_wide.hip) with its leaf capacity / leaf size knobs: cap 8 sends most
     leaves to the global-sort fallback, target 16 makes thousands of tiny leaves, target 100000 one
     leaf per L1 bucket (its distinct keys overflow a 64-key cap).  Inputs: near-unique keys, Zipf
-    (hot keys come through the flushed map tables as weighted keys), the corpus, long keys."""
+    (hot keys come through the flushed map tables as weighted keys), the corpus, long keys.  wmap=1:
+    the same through the wide map, whose L2 cuts leaves from byte-code digits (hot keys: digits of
+    many equal keys, leaves past the cap)."""
     import torch
     import oracle_lib as O
     from gpu_util import run_wc
@@ -538,10 +541,10 @@ def test_wide_sample_sort_knobs_vs_oracle(ctx, corpus, knobs, cap, target):
     uniq = t[:n].cpu().numpy().tobytes()
     ctx.gen_zipf(t.data_ptr(), n, 0x5EED2026, 3, 1 << 14, 1.1)
     zipf = t[:n].cpu().numpy().tobytes()
-    knobs(MRG_WIDE=1, MRG_TEST_LEAF_CAP=cap, MRG_TEST_LEAF_TARGET=target)
+    knobs(MRG_WIDE=1, MRG_TEST_LEAF_CAP=cap, MRG_TEST_LEAF_TARGET=target, MRG_WIDE_MAP=wmap)
     for docs, R in (([uniq], 16), ([zipf, uniq[:MIB]], 7), (corpus, 10), ([uniq, b"x" * 40 + b" y"], 3)):
         assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST), (len(docs), R)
-    if cap == "8":
+    if cap == "8" and wmap == "0":
         assert ctx.stats()["overflow_keys"] > 0   # leaves finished by the fallback
 
 

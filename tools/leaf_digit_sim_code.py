@@ -1,4 +1,5 @@
-exec(open('leafsim.py').read().split("L = 256")[0])
+import os
+exec(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'leaf_digit_sim.py')).read().split("L = 256")[0])
 L = 256
 def scheme_code(a0, a1):
     f0, f1 = a0[0], a1[0]
