@@ -38,6 +38,11 @@ constexpr uint32_t W_S2 = 8192;       // L2 samples per L1 bucket (sorted in LDS
 #ifndef MRG_WIDE_L2U
 #define MRG_WIDE_L2U 4   // L2 histogram: records per thread in flight
 #endif
+constexpr uint32_t W_L2D = 8192;          // SEG L2: digits
+constexpr uint32_t W_L2DS = 2048;         // SEG L2: sampled records (the digit bytes' values)
+constexpr uint32_t W_SCS = 7168;          // SEG L2: scatter chunk (the stage's top 16 KiB holds the leaf map)
+constexpr uint32_t W_L2D_CNT = 32768;     // SEG L2: byte offset of the digit counts in the sample LDS
+constexpr uint32_t W_L2D_MAP = 16u * W_SCS;   // SEG L2: byte offset of the digit -> leaf map
 constexpr uint32_t W_SC = 8192;       // L2 scatter chunk (staged in the samples' LDS)
 constexpr int W_LWG = 256;            // leaf workgroup (four per CU: while one waits on memory, others work)
 constexpr int W_LNW = W_LWG / 64;
@@ -486,6 +491,10 @@ __device__ __forceinline__ void seg_record(const L2Args &L, uint32_t b, const ui
     seg_load(L, b, lo, i - so[lo], k0, k1);
 }
 
+// byte j (0 = most significant) of a packed key, 0 past byte 15
+__device__ __forceinline__ uint32_t key_byte(uint64_t k0, uint64_t k1, uint32_t j) {
+    return j < 8u ? (uint32_t)(k0 >> (56u - 8u * j)) & 0xFFu : (j < 16u ? (uint32_t)(k1 >> (56u - 8u * (j - 8u))) & 0xFFu : 0u);
+}
 #ifdef MRG_WIDE_PROF  // diagnostic build: L2 phase clocks of thread 0 of every workgroup
 __device__ unsigned long long g_l2prof[8];
 #define L2P(i) { if (tid == 0) { const uint64_t t_ = clock64(); l2acc[i] += t_ - l2t; l2t = t_; } }
@@ -501,8 +510,13 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     __shared__ uint32_t s_bst[MRG_WIDE_MAXB2];      // scatter: a chunk's leaf starts
     static_assert(W_SC * sizeof(uint64_t) * 2 <= sizeof(s_smp) && W_SC * sizeof(uint16_t) <= sizeof(s_spl),
                   "the scatter's stage fits the sample and splitter arrays");
+    static_assert(16 * W_L2DS <= W_L2D_CNT && W_L2D_CNT + 4 * W_L2D <= W_L2D_MAP && W_L2D_MAP + 2 * W_L2D <= sizeof(s_smp) &&
+                  W_SCS * sizeof(uint16_t) <= sizeof(s_spl) && 1536 <= sizeof(s_bst) && W_L2D % W_WG == 0,
+                  "SEG L2: samples, digit counts, leaf map and stage fit the sample LDS");
     __shared__ uint32_t s_ws[W_NW];
     __shared__ uint32_t s_cseg[SEG ? W_MAXSEG + 2 : 1];   // SEG: the bucket's segment starts
+    __shared__ uint32_t s_dor[SEG ? 4 : 1];                // SEG: OR of the samples' bits against the first
+    __shared__ uint32_t s_dnv[SEG ? 4 : 1];                // SEG: values present at the three digit bytes
     const uint32_t tid = threadIdx.x, b = blockIdx.x;
 #ifdef MRG_WIDE_PROF
     uint64_t l2acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, l2t = clock64();
@@ -516,8 +530,100 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     uint32_t B2 = (uint32_t)min<uint64_t>((nb + L.target - 1) / L.target, MRG_WIDE_MAXB2);
     if (B2 < 1) B2 = 1;
     const GASW uint64_t *in = gw(L.in) + 2 * base;
+    // SEG (the wide map's buckets): leaves are runs of DIGITS, not ranges between sampled splitters.
+    // digit = the key bytes P, P + 1, P + 2 from the first byte the bucket's keys may differ on (the
+    // sample's, bounded by the bucket's splitters), each replaced by its rank among the values a
+    // sample shows at that byte, in mixed radix scaled to W_L2D digits (a value the sample lacks:
+    // see the radices below; profiles/r05 and tools/leaf_digit_sim*.py check the order).
+    // The histogram counts digits; a leaf = the digits whose running count falls in one multiple of
+    // the target.  No sample sort, and leaves come out the target size (a digit holds ~31 records
+    // at C5) instead of varying like 8-sample gaps (4 % of them went to the workgroup kernel).
+    uint32_t *dcnt = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(s_smp) + W_L2D_CNT);
+    uint16_t *lmap = reinterpret_cast<uint16_t *>(reinterpret_cast<uint8_t *>(s_smp) + W_L2D_MAP);
+    uint16_t *dcode = reinterpret_cast<uint16_t *>(s_bst);   // [3][256]: 2 x (values present below) + present
+    uint32_t dP = 0, dn1 = 1, dn2 = 1;
+    uint64_t dM = 1ull << 32;
+    uint64_t dtgt = L.target;
+    if (SEG) {
+        dtgt = max<uint64_t>(L.target, (nb + MRG_WIDE_MAXB2 - 1) / MRG_WIDE_MAXB2);
+        B2 = nb ? (uint32_t)((nb - 1) / dtgt + 1) : 1u;
+    }
     // ---- splitters from a sorted sample
-    if (B2 > 1) {
+    if (SEG && B2 > 1) {
+        const uint32_t S = (uint32_t)min<uint64_t>(nb, W_L2DS);
+        if (tid < 4) s_dor[tid] = 0;
+        for (uint32_t i = tid; i < 3u * 128u; i += W_WG) reinterpret_cast<uint32_t *>(dcode)[i] = 0;
+        for (uint32_t i = tid; i < W_L2D; i += W_WG) dcnt[i] = 0;
+        for (uint32_t k = tid; k < S; k += W_WG) {
+            uint64_t a, c;
+            seg_record(L, b, s_cseg, ((2ull * k + 1ull) * nb) / (2ull * S), a, c);
+            s_smp[2 * k] = a;
+            s_smp[2 * k + 1] = c;
+        }
+        lds_barrier();
+        {
+            const uint64_t f0 = s_smp[0], f1 = s_smp[1];
+            uint64_t o0 = 0, o1 = 0;
+            for (uint32_t k = tid; k < S; k += W_WG) {
+                o0 |= s_smp[2 * k] ^ f0;
+                o1 |= s_smp[2 * k + 1] ^ f1;
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                o0 |= __shfl_xor(o0, o);
+                o1 |= __shfl_xor(o1, o);
+            }
+            if ((tid & 63u) == 0) {
+                if (o0) { atomicOr(&s_dor[0], (uint32_t)o0); atomicOr(&s_dor[1], (uint32_t)(o0 >> 32)); }
+                if (o1) { atomicOr(&s_dor[2], (uint32_t)o1); atomicOr(&s_dor[3], (uint32_t)(o1 >> 32)); }
+            }
+        }
+        lds_barrier();
+        {
+            // P: the first byte the sample differs on, but no later than the first byte the bucket's
+            // bounds differ on -- keys outside the sample may differ earlier than it, never earlier
+            // than the bounds (every key lies between them)
+            uint64_t o0 = (uint64_t)s_dor[0] | ((uint64_t)s_dor[1] << 32), o1 = (uint64_t)s_dor[2] | ((uint64_t)s_dor[3] << 32);
+            const uint32_t q = b % L.B1r, r = b / L.B1r;
+            const uint64_t *sp = L.spl1 + 2ull * r * (L.B1r - 1u);
+            const uint64_t l0 = q > 0 ? sp[2 * (q - 1u)] : 0ull, l1 = q > 0 ? sp[2 * (q - 1u) + 1] : 0ull;
+            const uint64_t h0 = q + 1u < L.B1r ? sp[2 * q] : ~0ull, h1 = q + 1u < L.B1r ? sp[2 * q + 1] : ~0ull;
+            o0 |= l0 ^ h0;
+            o1 |= l1 ^ h1;
+            const uint32_t hb = o0 ? (uint32_t)__builtin_clzll(o0) : (o1 ? 64u + (uint32_t)__builtin_clzll(o1) : 0u);
+            dP = hb >> 3;
+        }
+        for (uint32_t k = tid; k < S; k += W_WG) {
+            const uint64_t a = s_smp[2 * k], c = s_smp[2 * k + 1];
+#pragma unroll
+            for (uint32_t t = 0; t < 3; ++t) dcode[256u * t + key_byte(a, c, dP + t)] = 1;
+        }
+        lds_barrier();
+        if (tid < 3u * 64u) {   // presence -> 2 x (present values below v) + (v present)
+            const uint32_t t = tid >> 6, lane = tid & 63u;
+            uint32_t *cw = reinterpret_cast<uint32_t *>(dcode + 256u * t);
+            const uint32_t w0 = cw[2 * lane], w1 = cw[2 * lane + 1];   // values 4 lane .. 4 lane + 3
+            const uint32_t pr[4] = {w0 & 1u, w0 >> 16, w1 & 1u, w1 >> 16};
+            const uint32_t cnt = pr[0] + pr[1] + pr[2] + pr[3];
+            const uint32_t inc = wave_scan_incl(cnt);
+            uint32_t run = inc - cnt, e[4];
+#pragma unroll
+            for (uint32_t x = 0; x < 4; ++x) {
+                e[x] = (run << 1) | pr[x];
+                run += pr[x];
+            }
+            cw[2 * lane] = e[0] | (e[1] << 16);
+            cw[2 * lane + 1] = e[2] | (e[3] << 16);
+            if (lane == 63) s_dnv[t] = inc;
+        }
+        lds_barrier();
+        // radices n + 1: a value the sample lacks takes the code of the next present value (or n)
+        // and zeroes the less significant codes, so the digit never decreases along the key order
+        // (a lacking value collapsed onto a present one, with its lower bytes kept, would reorder)
+        const uint64_t N = (uint64_t)(s_dnv[0] + 1u) * (s_dnv[1] + 1u) * (s_dnv[2] + 1u);
+        dn1 = s_dnv[1] + 1u;
+        dn2 = s_dnv[2] + 1u;
+        dM = N > W_L2D ? ((uint64_t)W_L2D << 32) / N : (1ull << 32);
+    } else if (!SEG && B2 > 1) {
         const uint32_t S = (uint32_t)min<uint64_t>(nb, W_S2);
         uint32_t P = 1;
         while (P < S) P <<= 1;
@@ -568,8 +674,18 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     }
     lds_barrier();
     const LeafIndex si{s_spl, reinterpret_cast<const uint16_t *>(s_smp), B2 - 1u,
-                       B2 > 1 ? LeafIndex::prefix_bits(s_spl, B2 - 1u) : 0u};
-    auto sub_of = [&](uint64_t k0, uint64_t k1) { return B2 > 1 ? si.upper(k0, k1) : 0u; };
+                       (!SEG && B2 > 1) ? LeafIndex::prefix_bits(s_spl, B2 - 1u) : 0u};
+    auto sub_of = [&](uint64_t k0, uint64_t k1) -> uint32_t {
+        if (SEG) {
+            if (B2 <= 1) return 0u;
+            const uint32_t e0 = dcode[key_byte(k0, k1, dP)], e1 = dcode[256u + key_byte(k0, k1, dP + 1u)],
+                           e2 = dcode[512u + key_byte(k0, k1, dP + 2u)];
+            const uint32_t c1 = (e0 & 1u) ? e1 >> 1 : 0u, c2 = (e0 & e1 & 1u) ? e2 >> 1 : 0u;
+            const uint32_t x = ((e0 >> 1) * dn1 + c1) * dn2 + c2;
+            return (uint32_t)(((uint64_t)x * dM) >> 32);
+        }
+        return B2 > 1 ? si.upper(k0, k1) : 0u;
+    };
     L2P(3);
     // ---- histogram (U records per thread in flight)
     constexpr int U = MRG_WIDE_L2U;
@@ -592,7 +708,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
                 for (int u = 0; u < U; ++u)
                     if (j0 + (uint32_t)u * 64u < nw) {
                         const uint32_t j = sub_of(x[u].x, x[u].y);
-                        atomicAdd(&s_cnt[j], 1u);
+                        atomicAdd(B2 > 1 ? &dcnt[j] : &s_cnt[0], 1u);   // SEG: digits
                         gw(L.sub)[base + o + j0 + (uint64_t)u * 64u] = (uint16_t)j;
                     }
             }
@@ -612,6 +728,25 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         }
     }
     lds_barrier();
+    if (SEG && B2 > 1) {   // digit d -> leaf floor(records before d / target); the leaves' counts
+        constexpr uint32_t PT = W_L2D / W_WG;
+        uint32_t v[PT], sum = 0;
+#pragma unroll
+        for (uint32_t x = 0; x < PT; ++x) {
+            v[x] = dcnt[tid * PT + x];
+            sum += v[x];
+        }
+        uint32_t tot;
+        uint32_t run = block_scan_excl(sum, s_ws, &tot);
+#pragma unroll
+        for (uint32_t x = 0; x < PT; ++x) {
+            const uint32_t leaf = min((uint32_t)(run / dtgt), B2 - 1u);
+            lmap[tid * PT + x] = (uint16_t)leaf;
+            if (v[x]) atomicAdd(&s_cnt[leaf], v[x]);
+            run += v[x];
+        }
+        lds_barrier();
+    }
     L2P(4);
     {  // exclusive scan of the B2 <= 1024 counts, one per thread
         const uint32_t v = tid < B2 ? s_cnt[tid] : 0u;
@@ -622,7 +757,10 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         if (tid < B2) {
             L.leaf_lo[lid] = base + ex;
             uint64_t a, c;
-            if (tid > 0) {
+            if (SEG) {   // digit leaves have no key bound (the wide map's job has no weighted keys)
+                a = 0;
+                c = 0;
+            } else if (tid > 0) {
                 a = s_spl[2 * (tid - 1)];
                 c = s_spl[2 * (tid - 1) + 1];
             } else {  // the L1 bucket's own lower bound
@@ -644,12 +782,13 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     // then stored so that consecutive threads write consecutive records of one leaf (a run of ~8
     // records per leaf per chunk instead of one 16-byte store per record at a random place: the
     // unstaged scatter wrote 2x its bytes to HBM and ran at a fifth of the read passes' rate)
-    constexpr uint32_t SU = W_SC / W_WG;
+    constexpr uint32_t WSC = SEG ? W_SCS : W_SC;   // SEG: the top of the stage holds the digit -> leaf map
+    constexpr uint32_t SU = WSC / W_WG;
     v2 *stg = reinterpret_cast<v2 *>(s_smp);              // the chunk in leaf order (the sample's LDS)
     uint16_t *stl = reinterpret_cast<uint16_t *>(s_spl);  // its leaves (the splitters' LDS)
     GASW v2 *outv = reinterpret_cast<GASW v2 *>(gw(L.out) + 2 * base);
-    for (uint64_t c0 = 0; c0 < nb; c0 += W_SC) {
-        const uint32_t nc = (uint32_t)min<uint64_t>(W_SC, nb - c0);
+    for (uint64_t c0 = 0; c0 < nb; c0 += WSC) {
+        const uint32_t nc = (uint32_t)min<uint64_t>(WSC, nb - c0);
         v2 x[SU];
         uint32_t j[SU], r[SU];
         // SEG: each thread finds its first record's segment by a search over the bucket's segment starts
@@ -677,7 +816,8 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
             } else {
                 x[u] = inv[i];
             }
-            j[u] = gw(L.sub)[base + i];   // the histogram pass's leaf: no second splitter search
+            j[u] = gw(L.sub)[base + i];   // the histogram pass's leaf (SEG: digit): no second search
+            if (SEG) j[u] = B2 > 1 ? lmap[j[u]] : 0u;
         }
         if (tid < B2) s_cnt[tid] = 0;
         lds_barrier();
@@ -766,9 +906,6 @@ __device__ __forceinline__ uint32_t w_hash(uint64_t a, uint64_t b) {
 }
 __device__ __forceinline__ uint32_t line_len(uint64_t k0, uint64_t k1, uint64_t c) {
     return mrg_short_len(k0, k1) + 2u + mrg_ndigits(c);
-}
-__device__ __forceinline__ uint32_t key_byte(uint64_t k0, uint64_t k1, uint32_t q) {
-    return q < 8u ? (uint32_t)(k0 >> (56u - 8u * q)) & 0xFFu : (uint32_t)(k1 >> (56u - 8u * (q - 8u))) & 0xFFu;
 }
 
 // weighted-key range [wr[2l], wr[2l+1]) of every leaf l: partition r's keys in [lb_l, lb_{l+1})
