@@ -149,6 +149,37 @@ def test_wide_map_forced_vs_oracle(ctx, corpus, knobs, knob):
     assert run_wc(ctx, docs, 10, flags=M.debug_hash_bits(4)) == O.wc(docs, 10, O.FAST)
 
 
+def _rare_byte_keys_doc(seed, n_words=400_000):
+    """Near-unique 12-letter keys that share their first bytes, with one key in 2000 taking a byte
+    value the rest never use at each of the positions the wide map's L2 digits read: a sample of
+    2048 records mostly misses those values, so their digit codes come from the 'value the sample
+    lacks' rule (a lacking value collapsed onto a present one, lower bytes kept, reordered keys)."""
+    import random
+    rng = random.Random(seed)
+    common, rare = "abcdefghijklmnop", "z9"
+    words = []
+    for i in range(n_words):
+        w = ["k", "q"] + [rng.choice(common) for _ in range(10)]
+        if i % 2000 == 1999:
+            for pos in rng.sample(range(1, 6), 2):
+                w[pos] = rng.choice(rare)
+        words.append("".join(w))
+    return " ".join(words).encode()
+
+
+@pytest.mark.parametrize("b1r", ["1", "4"])
+def test_wide_map_rare_byte_values_vs_oracle(ctx, knobs, b1r):
+    """The wide map's L2 digit leaves on keys whose rare byte values a bucket's sample misses, at one
+    and four quantile buckets per partition, against the oracle (R = 3 and 64)."""
+    import oracle_lib as O
+    from gpu_util import run_wc
+    knobs(MRG_WIDE_MAP=1, MRG_TEST_WMAP_B1R=b1r)
+    docs = [_rare_byte_keys_doc(7), _rare_byte_keys_doc(8, 100_000)]
+    for R in (3, 64):
+        assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST), R
+        assert ctx.stats()["map_kind"] == 1
+
+
 def _mixed_keys_doc(seed, n_words=200_000):
     """Words of 1..16 letters (a few thousand distinct per length) and one word in 100 of 17..20: the
     map's tail records are then a mix of 12-byte records (keys of <= 12 bytes) and 16-byte records
