@@ -1475,7 +1475,7 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
 //           coalesced).
 // Leaves with more items, or with a bucket of more than W_VMAXB items, are listed for k_wleaf.
 #ifndef MRG_WIDE_VC
-#define MRG_WIDE_VC 448
+#define MRG_WIDE_VC 384   // one-wave leaf capacity (r05: 448 -> 384 with digit leaves, v54)
 #endif
 constexpr uint32_t W_VC = MRG_WIDE_VC;
 constexpr uint32_t W_VIPL = W_VC / 64;
