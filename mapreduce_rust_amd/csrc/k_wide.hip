@@ -1491,7 +1491,10 @@ constexpr uint32_t W_VND = 512;         // digits
 #endif
 constexpr uint32_t W_VRG = MRG_WIDE_VRG; // rows whose buckets one trip of the rank loop reads
 constexpr uint32_t W_VMAXB = 64;
-constexpr uint32_t W_VQ = 4;            // waves (one-wave workgroups) per L1 bucket
+#ifndef MRG_WIDE_VQ
+#define MRG_WIDE_VQ 16   // (r05 v55: 4 -> 16, the last round of waves less ragged: C5 +2 %)
+#endif
+constexpr uint32_t W_VQ = MRG_WIDE_VQ;  // waves (one-wave workgroups) per L1 bucket
 constexpr uint32_t W_VPASS = MRG_WIDE_MAXB2 / W_VQ;   // leaves one wave may pass on
 
 __device__ __forceinline__ void wave_lds_sync() {
