@@ -511,12 +511,13 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     static_assert(W_SC * sizeof(uint64_t) * 2 <= sizeof(s_smp) && W_SC * sizeof(uint16_t) <= sizeof(s_spl),
                   "the scatter's stage fits the sample and splitter arrays");
     static_assert(16 * W_L2DS <= W_L2D_CNT && W_L2D_CNT + 4 * W_L2D <= W_L2D_MAP && W_L2D_MAP + 2 * W_L2D <= sizeof(s_smp) &&
-                  W_SCS * sizeof(uint16_t) <= sizeof(s_spl) && 1536 <= sizeof(s_bst) && W_L2D % W_WG == 0,
+                  W_SCS * sizeof(uint16_t) <= sizeof(s_spl) && W_L2D % W_WG == 0,
                   "SEG L2: samples, digit counts, leaf map and stage fit the sample LDS");
     __shared__ uint32_t s_ws[W_NW];
     __shared__ uint32_t s_cseg[SEG ? W_MAXSEG + 2 : 1];   // SEG: the bucket's segment starts
     __shared__ uint32_t s_dor[SEG ? 4 : 1];                // SEG: OR of the samples' bits against the first
     __shared__ uint32_t s_dnv[SEG ? 4 : 1];                // SEG: values present at the three digit bytes
+    __shared__ uint16_t s_dcode[SEG ? 3 * 256 : 1];        // SEG: the digit bytes' codes (live through the scatter)
     const uint32_t tid = threadIdx.x, b = blockIdx.x;
 #ifdef MRG_WIDE_PROF
     uint64_t l2acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, l2t = clock64();
@@ -540,7 +541,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     // at C5) instead of varying like 8-sample gaps (4 % of them went to the workgroup kernel).
     uint32_t *dcnt = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(s_smp) + W_L2D_CNT);
     uint16_t *lmap = reinterpret_cast<uint16_t *>(reinterpret_cast<uint8_t *>(s_smp) + W_L2D_MAP);
-    uint16_t *dcode = reinterpret_cast<uint16_t *>(s_bst);   // [3][256]: 2 x (values present below) + present
+    uint16_t *dcode = s_dcode;   // [3][256]: 2 x (values present below) + present
     uint32_t dP = 0, dn1 = 1, dn2 = 1;
     uint64_t dM = 1ull << 32;
     uint64_t dtgt = L.target;
@@ -709,7 +710,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
                     if (j0 + (uint32_t)u * 64u < nw) {
                         const uint32_t j = sub_of(x[u].x, x[u].y);
                         atomicAdd(B2 > 1 ? &dcnt[j] : &s_cnt[0], 1u);   // SEG: digits
-                        gw(L.sub)[base + o + j0 + (uint64_t)u * 64u] = (uint16_t)j;
+                        if (!SEG) gw(L.sub)[base + o + j0 + (uint64_t)u * 64u] = (uint16_t)j;   // SEG: recomputed
                     }
             }
         }
@@ -816,8 +817,10 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
             } else {
                 x[u] = inv[i];
             }
-            j[u] = gw(L.sub)[base + i];   // the histogram pass's leaf (SEG: digit): no second search
-            if (SEG) j[u] = B2 > 1 ? lmap[j[u]] : 0u;
+            // the histogram pass's leaf (no second splitter search); SEG: the digit again from the
+            // record (three LDS code reads: cheaper than storing and re-reading a digit per record)
+            if (SEG) j[u] = B2 > 1 ? lmap[sub_of(x[u].x, x[u].y)] : 0u;
+            else j[u] = gw(L.sub)[base + i];
         }
         if (tid < B2) s_cnt[tid] = 0;
         lds_barrier();
