@@ -1519,6 +1519,7 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
     __shared__ v2 s_kb[W_VC];            // items in digit-bucket order
     __shared__ uint32_t s_cb[W_VC];      // their counts (a leaf with a larger weighted count is passed on)
     __shared__ __attribute__((aligned(16))) uint16_t s_ix[W_VC];   // sorted position -> bucket slot (and the digit code tables)
+    static_assert(sizeof(s_ix) >= 3 * 256, "the leaf digit's three 256-byte code tables live in s_ix");
     __shared__ uint32_t s_dc[W_VND];     // digit counts
     __shared__ uint16_t s_ds[W_VND];     // digit starts
     __shared__ uint32_t s_pass[W_VPASS]; // leaves passed on to k_wleaf
