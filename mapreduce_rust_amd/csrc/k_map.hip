@@ -25,8 +25,9 @@
 //      table gives the big-endian packed key (k0, k1); further interior deletions are squeezed out
 //      by 128-bit shifts; tokens that run past the 2-segment window or the staged halo are deferred
 //      to the exact per-codepoint walker.
-// Blocks with a non-ASCII byte take the same path with UTF-8-exact byte classes (codepoint leads
-// compacted into the wave's queue and decoded one per lane, see the block step); only blocks holding
+// Blocks with a non-ASCII byte take the same path with UTF-8-exact byte classes (each lane decodes
+// the codepoints whose leads lie in its segments, in registers; when a lane holds two or more, the
+// block's leads are first compacted one per lane through the wave's queue, see the block step); only blocks holding
 // invalid UTF-8 are listed by the main loop and walked afterwards by all 16 waves with the exact
 // per-codepoint walker, which reports the first bad byte.
 // Keys of <= 16 bytes go to the workgroup's LDS hash table (exact: the packed key IS the identity):
@@ -178,6 +179,9 @@ __device__ __forceinline__ TileInfo sub_tile(const BlkInfo &b, uint32_t j) {
 // timing variants only: an ablation compiled in as a constant (the product build: 0)
 #ifndef MRG_MAP_ABL_CONST
 #define MRG_MAP_ABL_CONST 0u
+#endif
+#ifndef MRG_MAP_CMPT  // compacted codepoint decode for blocks with a lane of 2+ leads (A/B switch)
+#define MRG_MAP_CMPT 1
 #endif
 // per-wave dedup of a round's repeated keys (timing variant, MRG_MAP_DEDUP = leader rounds; 0 = off):
 // see emit_fastN
@@ -1164,9 +1168,10 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
 #else
             // UTF-8-exact classes in registers (r05): every lane decodes the codepoints whose leads lie
             // in its own segments, straight from the segment's four dwords and the next segment's first
-            // (DPP) -- no LDS window, no queue, no compaction.  One loop over the lane's leads, both
-            // segments per trip (the trip count is the busiest lane's lead count: about 2 per block on
-            // English text, whose non-ASCII codepoints are sparse).  A lead's bytes are checked by the
+            // (DPP) -- no LDS window.  One loop over the lane's leads, both segments per trip (the trip
+            // count is the busiest lane's lead count: about 1.6 per block on English text, whose
+            // non-ASCII codepoints are sparse), unless a lane holds two or more: then the compacted
+            // decode below takes one trip (MRG_MAP_CMPT).  A lead's bytes are checked by the
             // decode (continuation bytes, overlongs, surrogates, range); a codepoint's last bytes may lie in
             // the next segment (spilled by DPP).  Every non-ASCII byte must be covered by a decoded
             // codepoint, else the block holds invalid UTF-8 and is deferred.  (r04 compacted the leads
@@ -1242,9 +1247,70 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                 S |= cl == MRG_CLS_S ? span : 0u;
             };
             uint32_t W0 = 0, S0 = 0, C0 = 0, W1 = 0, S1 = 0, C1 = 0;
+            uint32_t mAB0 = (MRG_MAP_ABL_CONST & 0x10000u) ? 0u : (ld0 | (ld1 << 16));
+#if MRG_MAP_CMPT
+            // a lane with two or more leads (about 6 blocks in 10 of English text: one codepoint per
+            // ~190 bytes, 32 bytes per lane) would cost the whole wave a second decode trip.  Instead
+            // the block's leads are compacted, one per lane (a wave prefix sum of the lead counts):
+            // the owner writes each lead's 4 bytes and its byte budget to the wave's token queue (free
+            // between tiles), lanes 0..T-1 decode one codepoint each, and the owners read the results
+            // back (length | W << 3 | S << 4; length 0 = invalid).
+            {
+                const uint32_t c = (uint32_t)__builtin_popcount(mAB0);
+                if (__any(c >= 2u)) {
+                    const uint32_t incl = wave_incl_scan(c);
+                    const uint32_t T = lane_u32(incl, 63);
+                    if (T <= 64u) {
+                        LDS uint64_t *slot = (LDS uint64_t *)queue;
+                        wave_sync_lds();
+                        uint32_t pos = incl - c;
+                        for (uint32_t m = mAB0; m;) {
+                            const uint32_t q = (uint32_t)__builtin_ctz(m);
+                            m &= m - 1u;
+                            const bool sb = q >= 16u;
+                            const uint32_t p = q & 15u, k = p >> 2;
+                            const uint32_t d0 = sb ? X.v1.x : X.v0.x, d1 = sb ? X.v1.y : X.v0.y,
+                                           d2 = sb ? X.v1.z : X.v0.z, d3 = sb ? X.v1.w : X.v0.w, d4 = sb ? nB : nA;
+                            const uint32_t a = (k & 2u) ? ((k & 1u) ? d3 : d2) : ((k & 1u) ? d1 : d0);
+                            const uint32_t b = (k & 2u) ? ((k & 1u) ? d4 : d3) : ((k & 1u) ? d2 : d1);
+                            const int so = (sb ? 1024 : 0) + (int)l16 + (int)p;
+                            slot[pos++] = (uint64_t)__builtin_amdgcn_alignbyte(b, a, p & 3u) | ((uint64_t)(uint32_t)min(hi - so, 4) << 32);
+                        }
+                        wave_sync_lds();
+                        if ((uint32_t)lane < T) {
+                            const uint64_t s = slot[lane];
+                            const uint32_t sw = (uint32_t)s;
+                            auto rd = [&](uint64_t x) -> uint32_t { return (sw >> (8u * (uint32_t)x)) & 0xFFu; };
+                            uint32_t cp = 0, raw;
+                            const uint32_t n = (uint32_t)mrg_utf8_decode(rd, 0ull, s >> 32, &cp, &raw);
+                            const uint32_t cl = uni_class(uc, cp);
+                            ((LDS uint32_t *)slot)[2 * lane] =
+                                n | (cl == MRG_CLS_W ? 8u : 0u) | (cl == MRG_CLS_S ? 16u : 0u);
+                        }
+                        wave_sync_lds();
+                        pos = incl - c;
+                        for (uint32_t m = mAB0; m;) {
+                            const uint32_t q = (uint32_t)__builtin_ctz(m);
+                            m &= m - 1u;
+                            const uint32_t r = ((const LDS uint32_t *)slot)[2 * pos++];
+                            const uint32_t n = r & 7u;
+                            bad |= n == 0u;
+                            const uint32_t span = ((1u << n) - 1u) << (q & 15u);
+                            const uint32_t w = (r & 8u) ? span : 0u, sm = (r & 16u) ? span : 0u;
+                            if (q >= 16u) {
+                                W1 |= w; S1 |= sm; C1 |= span;
+                            } else {
+                                W0 |= w; S0 |= sm; C0 |= span;
+                            }
+                        }
+                        mAB0 = 0u;
+                    }
+                }
+            }
+#endif
             // one codepoint per lane and trip, the lane's two segments' leads in one mask (non-ASCII
             // text is sparse: most lanes have none, a few one)
-            for (uint32_t mAB = (MRG_MAP_ABL_CONST & 0x10000u) ? 0u : (ld0 | (ld1 << 16)); __any(mAB != 0u);) {
+            for (uint32_t mAB = mAB0; __any(mAB != 0u);) {
                 if (mAB) {
                     const uint32_t q = (uint32_t)__builtin_ctz(mAB);
                     mAB &= mAB - 1u;

@@ -133,6 +133,40 @@ def test_random_unicode_vs_oracle(ctx, seed):
         assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST)
 
 
+@pytest.mark.parametrize("gap", [7, 24, 31, 32, 33, 48, 120])
+def test_codepoint_density_sweep_vs_oracle(ctx, gap):
+    """One non-ASCII codepoint every ~`gap` bytes: a 2 KiB block holds ~2048/gap codepoint leads, so
+    the sweep crosses k_map's compacted decode (a lane with 2+ leads, at most 64 leads per block, one
+    per lane) and the per-lane loop it falls back to above 64.  Codepoints of 2, 3 and 4 bytes, word
+    and White_Space classes, leads placed at every offset of a 16-byte lane segment; then one
+    invalid sequence per document at a few densities (MRG_EUTF8)."""
+    import oracle_lib as O
+    import mapreduce_rust_amd as M
+    from gpu_util import run_wc
+    rng = random.Random(gap)
+    cps = ["é", "ж", "’", "—", "“", "中", "😀", " ", "　", "ſ", "ß"]
+    def doc(n):
+        out, L = [], 0
+        while L < n:
+            w = "".join(rng.choice("abcdefgh") for _ in range(rng.randint(1, gap)))
+            c = rng.choice(cps)
+            s = w + c + rng.choice([" ", "", "\n"])
+            out.append(s)
+            L += len(s.encode())
+        return "".join(out).encode()
+    docs = [doc(rng.randint(3000, 40000)) for _ in range(4)]
+    for R in (1, 7):
+        assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST)
+    if gap in (24, 32, 48):
+        d = bytearray(docs[1])
+        d[len(d) // 2] = 0xE2  # a lead without its continuations (or a broken one) mid-document
+        d[len(d) // 2 + 1] = 0x41
+        with pytest.raises(M.MrgError) as ei:
+            run_wc(ctx, [docs[0], bytes(d)], 3)
+        assert ei.value.code == -2
+        assert run_wc(ctx, docs, 3) == O.wc(docs, 3, O.FAST)
+
+
 def test_tile_boundaries_and_long_tokens(ctx):
     """Tokens straddling 4 KiB tiles / 16 B lane segments / the 256 B halo, and > 16 B keys."""
     import oracle_lib as O
