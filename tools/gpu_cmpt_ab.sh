@@ -1,6 +1,7 @@
 #!/bin/bash
-# r05 v64: compacted codepoint decode (MRG_MAP_CMPT=1, lib_variants/cmpt) -- parity tests through the
-# variant, then alternated zipf_u and C3 timings against the main build.
+# r05 v63/v64: compacted codepoint decode variants (built with tools/build_variant.sh, EXTRA=-DMRG_MAP_CMPT=1:
+# lib_variants/cmpt, and cmpt2 = cmpt + the edge codepoints folded in) -- parity tests through the
+# variant, then alternated zipf_u and C3 timings against the main build (v63 ran cmpt alone).
 set -o pipefail
 mkdir -p gpurun_out/v64
 MRG_LIB=$PWD/mapreduce_rust_amd/lib_variants/cmpt2/libmrgpu.so timeout -k 10 400 python -u -m pytest -x -q \
