@@ -788,7 +788,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // per wave: staged window, 2-segment mask windows, token queue (waves work on their own tiles)
     __shared__ __attribute__((aligned(16))) uint8_t s_win[NW][WIN];
     __shared__ __attribute__((aligned(8))) uint64_t s_mp[NW][NMP];  // W(g)|W(g+1)<<16 | (S(g)|S(g+1)<<16)<<32
-    __shared__ uint16_t s_q[NW][QCAP];
+    // 8-byte aligned rows: the class fix's compacted decode uses a row as 64 u64 slots between tiles
+    __shared__ __attribute__((aligned(8))) uint16_t s_q[NW][QCAP];
+    static_assert((QCAP * sizeof(uint16_t)) % 8 == 0 && QCAP * sizeof(uint16_t) >= 64 * 8, "queue rows hold 64 u64 slots");
     // LUT and length masks first in LDS (highest alignment): their base then fits the 16-bit
     // offset field of ds_read, so a lookup needs no separate address add
     // Byte class per byte position p of a dword: s_lut[p][c] = (W | S << 4) << p, one byte per byte
