@@ -61,6 +61,19 @@ constexpr int QCAP = TILE / 2 + 16;  // token starts of a tile (a start needs a 
 constexpr int NMP = 64;         // mask pairs per wave (one per segment of the tile)
 static_assert(TILE == 64 * SEG, "one segment per lane");
 static_assert(WIN % 16 == 0, "16-byte window rows");
+// Every tunable-sized LDS array against the largest index the code forms into it (the r05 fault in
+// k_wleafw was a tunable outgrowing a fixed array: these fail the build instead).
+//   mask pairs: mp[s >> 4] for a tile offset s < TILE, and mp[nseg - 1] with nseg <= TILE / SEG
+static_assert(NMP == TILE / SEG, "one mask pair per segment of the tile");
+//   window: the staged 16-byte vectors 0 .. 1 + TILE/16 + HALO/16 - 1 (the byte before, the tile,
+//   the halo), and the key read's five dwords from BEHIND + s + first (s < TILE, first < 32)
+static_assert(16 * (1 + TILE / 16 + HALO / 16) <= WIN, "staged vectors fit the window row");
+static_assert(BEHIND + (TILE - 1) + 31 + 20 <= WIN, "the 5-dword key read stays in the window row");
+static_assert(BEHIND == 16 && HALO % 16 == 0 && HALO >= 64, "one 16-byte vector behind, whole halo vectors");
+//   queue: at most one token start per two bytes of the tile (a start follows a space), plus the
+//   tile's first byte; reads are also clamped to QCAP - 1
+static_assert(QCAP >= TILE / 2 + 1, "the token queue holds every start of a tile");
+static_assert(BLK == 2 * TILE && NSUB == 2, "A/B register sets hold two tiles per lane (v0, v1)");
 
 // ---------------------------------------------------------------- wave primitives (DPP, wave64)
 __device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {  // lane l <- lane l+1 (lane 63 <- 0)
@@ -247,6 +260,8 @@ struct alignas(16) KeyPair {
 #ifndef MRG_MAP_DOOR_LEVELS
 #define MRG_MAP_DOOR_LEVELS 1
 #endif
+static_assert(MRG_MAP_DOOR_WORDS >= 32 && (MRG_MAP_DOOR_WORDS & (MRG_MAP_DOOR_WORDS - 1)) == 0,
+              "doorkeeper bit index is masked with DW * 32 - 1");
 template <int CAP, bool IDX>
 struct LdsTable {
     static constexpr uint32_t NS = CAP / 2;
@@ -826,6 +841,18 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ unsigned int s_lcnt;                      // long-token records (region cursor)
     __shared__ unsigned int s_door[(MRG_MAP_DOOR && !WIDE) ? LdsTable<CAP, IDX>::DW : 1];  // admission bitmap
     static_assert(WIDE || sizeof(s_q) >= CAP * sizeof(uint16_t), "flush ranks reuse the queues");
+    static_assert((CAP & (CAP - 1)) == 0 && CAP >= 64 && CAP <= 65536, "2-way sets: NS = CAP / 2 a power of two, ranks in u16");
+    static_assert(sizeof(s_door) / sizeof(s_door[0]) >= ((MRG_MAP_DOOR && !WIDE) ? LdsTable<CAP, IDX>::DW : 1u), "doorkeeper words");
+    static_assert(!WIDE || (sizeof(s_wcur) / sizeof(s_wcur[0]) == MRG_WMAP_MAXB1 && sizeof(s_wspl) / sizeof(s_wspl[0]) == 2 * MRG_WMAP_MAXB1 &&
+                            sizeof(s_wix) == MRG_WMAP_IXR * MRG_WIDE_IX1 && MRG_WIDE_IX1 % 4 == 0),
+                  "wide map: cursors, splitters and index rows as the host plan sizes them");
+    // the wide map's run-time sizes against those arrays (the host plan keeps R * B1r <= MRG_WMAP_MAXB1
+    // and passes an index only when R <= MRG_WMAP_IXR, mrgpu.cpp wide_map_plan; job_map_wide refuses
+    // a plan that breaks them before the launch): a launch that still did would return here, uniformly,
+    // instead of indexing past LDS
+    if constexpr (WIDE) {
+        if (A.wR * A.wB1r > (uint32_t)MRG_WMAP_MAXB1 || A.wB1r == 0u || (A.wix && A.wR > (uint32_t)MRG_WMAP_IXR)) return;
+    }
 
     const int tid = threadIdx.x;
     // wave index through readfirstlane: the compiler then knows everything derived from it (tile

@@ -1499,6 +1499,11 @@ constexpr uint32_t W_VMAXB = 64;
 #endif
 constexpr uint32_t W_VQ = MRG_WIDE_VQ;  // waves (one-wave workgroups) per L1 bucket
 constexpr uint32_t W_VPASS = MRG_WIDE_MAXB2 / W_VQ;   // leaves one wave may pass on
+// tunables against the arrays they size (r06; the v59 fault was W_VC outgrowing s_ix's code tables):
+static_assert(W_VC % 64 == 0 && W_VIPL * 64 == W_VC, "items per lane: W_VC a whole number of wave rows");
+static_assert(W_VC <= 0x8000u, "s_ix holds sorted positions below the 0x8000 padding marker");
+static_assert(W_VQ * W_VPASS == MRG_WIDE_MAXB2, "the waves of an L1 bucket pass on at most MAXB2 leaves together");
+static_assert(W_VRG >= 1 && W_VRG <= W_VIPL, "rank-loop row groups within the lane's rows");
 
 __device__ __forceinline__ void wave_lds_sync() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

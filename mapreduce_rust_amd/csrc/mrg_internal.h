@@ -4,7 +4,9 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#ifndef MRG_MAP_WAVES  // (timing variants override it: the r06 occupancy sweep)
 #define MRG_MAP_WAVES 16        // waves per map workgroup (one workgroup per CU, one shared LDS table)
+#endif
 #define MRG_MAP_WG (64 * MRG_MAP_WAVES)
 #define MRG_MAP_SEG 16          // input bytes per lane per tile
 #define MRG_MAP_TILE (64 * MRG_MAP_SEG)  // 1 KiB tile per WAVE iteration (waves never synchronise)

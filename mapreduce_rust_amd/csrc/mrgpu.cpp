@@ -1129,6 +1129,9 @@ void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_
         A.wrec = wrec; A.wcnt = wcnt; A.wspl = wp.spl1; A.wix = wp.ix1;
         A.wR = c->R; A.wB1r = wp.B1r; A.wcap = (uint32_t)wcap;
         A.w12 = w12 ? 1u : 0u; A.wl16cap = (uint32_t)wl16cap; A.wl16 = wl16; A.wl16n = wl16n;
+        // the kernel's LDS cursors, splitters and index rows are sized by these bounds (k_map.hip)
+        if (A.wB1r == 0 || (uint64_t)A.wR * A.wB1r > MRG_WMAP_MAXB1 || (A.wix && A.wR > MRG_WMAP_IXR))
+            raise(MRG_EINVAL, "wide map plan exceeds the kernel's LDS bounds");
         HIPCHK(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long) * CNT_N, s));
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_ERRPOS], 0xFF, sizeof(unsigned long long), s));
         ev_rec(c, 0);
