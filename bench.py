@@ -175,8 +175,8 @@ def end_to_end(buf, files, fbytes, n_reduce):
             M.native.run_job(c1p, 10, M.APP_WC, out)
             lat.append((time.perf_counter() - t0) * 1e3)
         res = {"end_to_end_gbs": round(n / wall / 1e9, 3), "ms": round(wall * 1e3, 1),
-               "phases_ms": {k: round(st[k], 1) for k in ("ms_open", "ms_read", "ms_map", "ms_shuffle", "ms_reduce",
-                                                          "ms_write")},
+               "phases_ms": {k: round(st[k], 1) for k in ("ms_open", "ms_read", "ms_map", "ms_map_alloc", "ms_shuffle",
+                                                          "ms_reduce", "ms_write")},
                "input_bytes": n, "output_bytes": st["output_bytes"],
                "read_gbs": round(n / (st["ms_read"] / 1e3) / 1e9, 2) if st["ms_read"] > 0 else None,
                "c1_latency_ms": round(statistics.median(lat), 2),
@@ -291,6 +291,45 @@ def stage_roofline(stats, shard, out_bytes):
     return stages, ratio, note
 
 
+def cold_job(dev, buf, doc_off, n_reduce, steady):
+    """The FIRST job on a fresh Context over the same resident input: what mrg_run_job and every
+    one-shot worker call run (the reference runs each task once per call, src/bin/mrworker.rs:95,145).
+    Reports its wall time, its kernel time (sum of the HIP-event stages) against the steady steps'
+    median, the pool's device allocations (hipMalloc calls, bytes, host ms: paid once per context, so
+    reported apart from the kernels) and the paths it took.  `steady` = the warm legs' per-step stats."""
+    ctx = M.Context(dev.index)
+    try:
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        ctx.set_timing(True)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ctx.job_begin(M.APP_WC, n_reduce)
+        ctx.set_input(buf.data_ptr(), doc_off)
+        ctx.map()
+        ctx.reduce()
+        torch.cuda.synchronize(dev)
+        wall = (time.perf_counter() - t0) * 1e3
+        st = ctx.stats()
+        n_alloc, alloc_bytes, alloc_ms = ctx.pool_alloc_stats()
+    finally:
+        ctx.close()
+    keys = ("ms_map", "ms_aggregate", "ms_sort", "ms_format")
+    kern = sum(st[k] for k in keys)
+    warm = statistics.median(sum(s[k] for k in keys) for s in steady)
+    res = {"ms_wall": round(wall, 3), "ms_kernels": round(kern, 3), "steady_ms_kernels": round(warm, 3),
+           "kernels_vs_steady": round(kern / warm, 3) if warm > 0 else None,
+           "stages_ms": {k: round(st[k], 3) for k in keys},
+           "pool_allocs": n_alloc, "pool_alloc_bytes": alloc_bytes, "pool_alloc_ms": round(alloc_ms, 3),
+           "ms_wall_minus_alloc": round(wall - alloc_ms, 3),
+           "map_launches": st["map_launches"], "map_kind": st["map_kind"], "agg_path": st["agg_path"],
+           "note": "first job on a fresh Context (same resident input, same process): wall = job_begin .. reduce; "
+                   "kernels = sum of the HIP-event stages; pool_alloc_ms = host time inside the pool's hipMalloc calls"}
+    log(f"cold job: wall {res['ms_wall']} ms (alloc {res['pool_alloc_ms']} ms in {n_alloc} hipMalloc), kernels "
+        f"{res['ms_kernels']} ms vs steady {res['steady_ms_kernels']}, map launches {res['map_launches']}, "
+        f"map kind {res['map_kind']}")
+    return res
+
+
 def leg(ctx, dev, a, workload, files, steps, warmup):
     """An extra single-GPU workload (zipf_u, C5) on its own buffer, timed like the headline line."""
     fbytes = a.file_mib * MIB
@@ -306,6 +345,7 @@ def leg(ctx, dev, a, workload, files, steps, warmup):
         return ctx.reduce()
 
     dt, step_max, stats = time_steps(ctx, step, steps, warmup, dev, 1, 0, workload)
+    cold = cold_job(dev, buf, doc_off, a.reduce, stats) if workload == "unique" else None
     del buf
     torch.cuda.empty_cache()
     m = statistics.median(step_max)
@@ -319,7 +359,8 @@ def leg(ctx, dev, a, workload, files, steps, warmup):
             "stages_ms": {k: round(med(stats, k), 3) for k in ("ms_map", "ms_aggregate", "ms_sort", "ms_format")},
             "tokens": st["tokens"], "long_tokens": st["long_tokens"], "map_records": st["map_records"],
             "distinct_keys": st["distinct_keys"], "nonascii_tiles": st["nonascii_tiles"],
-            "nonascii_tile_frac": round(st["nonascii_tiles"] / tiles, 4), "agg_path": st["agg_path"]}
+            "nonascii_tile_frac": round(st["nonascii_tiles"] / tiles, 4), "agg_path": st["agg_path"],
+            **({"cold": cold} if cold else {})}
 
 
 def c2_latency(ctx, dev):
@@ -560,6 +601,8 @@ def main():
                 "agg_path": st["agg_path"]},
     }
     single = world == 1 and a.workload == "zipf" and not a.shuffle_1
+    if world == 1 and not a.shuffle_1 and not a.quick:
+        line["cold"] = cold_job(dev, buf, doc_off, a.reduce, stats)
     if single and not a.no_e2e:
         line["end_to_end"] = end_to_end(buf, files, fbytes, a.reduce)
     cpu = None

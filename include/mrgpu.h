@@ -104,9 +104,9 @@ typedef struct {
 
 /* ABI history: 1 = round-1 layout; 2 = mrg_run_job's last argument is n_gpus (was a device index);
  * 3 = 24-byte exchange records (were 40), mrg_run_get_stats; 4 = mrg_stats gains nonascii_tiles,
- * tail_records_16, spec_agg, agg_path; 5 = mrg_stats gains map_kind, mrg_comm_count, mrg_pool_stats.
- * mrg_version() names the ABI it implements. */
-#define MRG_ABI_VERSION 5
+ * tail_records_16, spec_agg, agg_path; 5 = mrg_stats gains map_kind, mrg_comm_count, mrg_pool_stats;
+ * 6 = mrg_pool_alloc_stats.  mrg_version() names the ABI it implements. */
+#define MRG_ABI_VERSION 6
 
 const char *mrg_last_error(void);
 const char *mrg_version(void);
@@ -184,6 +184,10 @@ int mrg_comm_count(const mrg_comm *comm, int *n_ranks);
 /* The context's device buffer pool: blocks handed out and not yet returned (between calls this is
  * the job state the context keeps), and all bytes it holds (handed out + cached).  Either may be NULL. */
 int mrg_pool_stats(mrg_ctx *ctx, uint64_t *outstanding, uint64_t *held_bytes);
+/* Device allocations the pool has made since mrg_open (cumulative): hipMalloc calls, their bytes and
+ * the host milliseconds spent inside them.  A fresh context's first job pays these; later jobs reuse
+ * cached blocks.  Either pointer may be NULL.  (ABI 6.) */
+int mrg_pool_alloc_stats(mrg_ctx *ctx, uint64_t *n_allocs, uint64_t *alloc_bytes, double *alloc_ms);
 
 /* ---- plugin-surface equivalents, host buffers (one map task / one reduce task) ---- */
 
@@ -240,6 +244,8 @@ typedef struct {
     uint64_t input_bytes;
     uint64_t output_bytes;  /* bytes of all mr-{r}.txt */
     int n_gpus;
+    double ms_map_alloc;    /* of ms_map: host time inside the fresh contexts' device allocations (slowest
+                               GPU; every mrg_run_job opens fresh contexts, ABI 6) */
 } mrg_run_stats;
 int mrg_run_get_stats(mrg_run_stats *out);
 

@@ -119,6 +119,7 @@ class Pool : public DevPool {
         }
         void *p = nullptr;
         if (debug_) fprintf(stderr, "[mrgpu] pool: allocating %zu bytes\n", c);
+        const auto t0 = std::chrono::steady_clock::now();
         if (hipMalloc(&p, c) != hipSuccess) {
             (void)hipGetLastError();
             if (debug_) fprintf(stderr, "[mrgpu] pool: device full, trimming %zu free blocks\n", free_.size());
@@ -128,6 +129,9 @@ class Pool : public DevPool {
                 raise(MRG_ENOMEM, "device allocation of %zu bytes failed", c);
             }
         }
+        alloc_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        ++allocs_;
+        alloc_bytes_ += c;
         size_[p] = c;
         return p;
     }
@@ -151,6 +155,13 @@ class Pool : public DevPool {
         for (auto &kv : size_) b += kv.second;
         return b;
     }
+    // device allocations made so far (hipMalloc calls, bytes, host milliseconds inside them): a fresh
+    // context's first job pays them, later jobs reuse the cached blocks
+    void alloc_stats(uint64_t *n, uint64_t *bytes, double *ms) const {
+        if (n) *n = allocs_;
+        if (bytes) *bytes = alloc_bytes_;
+        if (ms) *ms = alloc_ms_;
+    }
     ~Pool() override {
         (void)hipDeviceSynchronize();
         for (auto &kv : size_) (void)hipFree(kv.first);
@@ -167,6 +178,8 @@ class Pool : public DevPool {
     std::multimap<size_t, void *> free_;
     std::unordered_map<void *, size_t> size_;
     bool debug_ = getenv("MRG_DEBUG") != nullptr;
+    uint64_t allocs_ = 0, alloc_bytes_ = 0;
+    double alloc_ms_ = 0.0;
 };
 
 template <class T>
@@ -223,6 +236,7 @@ struct mrg_ctx {
     uint64_t ocap_hint = 0;         // records per bucket overflow list
     bool spec_agg = false, spec_c32 = false;  // last wc job took the bucket path (with 32-bit counts)
     bool wide_hint = false;   // last wc job took the wide aggregation (the next one may take the wide map)
+    bool wc_sized = false;    // a wc job of >= 64 MiB has run on this context (its path is a measured hint)
     uint64_t wcap_hint = 0;   // wide map: records per (L1 bucket, workgroup) region the last run needed
     bool w12_off = false;     // wide map: a job overflowed the 16-byte lists of the 12-byte regions
     // job
@@ -1009,14 +1023,18 @@ struct WideMapPlan {
     uint8_t *ix1 = nullptr;
 };
 
-// Taken when the context's last wc job went the wide way (or MRG_WIDE_MAP=1) and a sample of the
-// input is near-unique: fewer than 1 in 16 sampled tokens repeat a sampled neighbour in key order.
+// Sampled (k_wsample_text + k_wsample_dups, ~0.1 ms and one host wait) on every wc job of >= 64 MiB
+// whose context has no measured path yet -- the first job of a fresh context, so every mrg_run_job and
+// every one-shot worker call -- and when the context's last such job went the wide way (or
+// MRG_WIDE_MAP=1).  Taken when the sample is near-unique: fewer than 1 in 16 sampled tokens repeat a
+// sampled neighbour in key order.  (Until r05 only the hint sampled: a cold near-unique job ran the
+// LDS-combine map, overflowed its tail regions, reran it and took the L1 count + scatter passes.)
 WideMapPlan wide_map_plan(mrg_ctx *c, const uint64_t *d_doc_off, uint32_t nd, uint64_t total, int grid) {
     WideMapPlan P;
     const char *env = getenv("MRG_WIDE_MAP");
     P.forced = env && atoi(env) != 0;
     if (is_idx(c) || (env && atoi(env) == 0) || total == 0 || wide_forced_off()) return P;
-    if (!P.forced && (!c->wide_hint || total < (64ull << 20))) return P;
+    if (!P.forced && (total < (64ull << 20) || (c->wc_sized && !c->wide_hint))) return P;
     const uint32_t R = c->R;
     if (R > MRG_WMAP_MAXB1 || grid > 512) return P;
     uint32_t B1r = std::min<uint32_t>(64, std::max<uint32_t>(1, MRG_WMAP_MAXB1 / R));
@@ -1239,6 +1257,7 @@ void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_
     c->st.ms_aggregate = ev_ms(c, 2, 3);
     // the hint holds while the input stays near-unique
     c->wide_hint = 2 * c->st.distinct_keys > c->st.tokens;
+    c->wc_sized = true;
     c->mapped = true;
 }
 
@@ -1538,6 +1557,7 @@ void job_map(mrg_ctx *c) {
     ev_rec(c, 3);
     release_map();
     c->st.ms_aggregate = ev_ms(c, 2, 3);
+    if (!idx && total >= (64ull << 20)) c->wc_sized = true;
     c->mapped = true;
 }
 
@@ -2273,7 +2293,7 @@ void text_reduce(mrg_ctx *c, const uint8_t *const *files, const uint64_t *sizes,
 extern "C" {
 
 const char *mrg_last_error(void) { return g_err.c_str(); }
-const char *mrg_version(void) { return "mrgpu 0.5 (gfx950, abi 5)"; }
+const char *mrg_version(void) { return "mrgpu 0.6 (gfx950, abi 6)"; }
 
 int mrg_open(int device, mrg_ctx **out) {
     return guard([&] {
@@ -2635,6 +2655,13 @@ int mrg_pool_stats(mrg_ctx *c, uint64_t *outstanding, uint64_t *held_bytes) {
     });
 }
 
+int mrg_pool_alloc_stats(mrg_ctx *c, uint64_t *n_allocs, uint64_t *alloc_bytes, double *alloc_ms) {
+    return guard([&] {
+        if (!c) raise(MRG_EINVAL, "null context");
+        c->pool.alloc_stats(n_allocs, alloc_bytes, alloc_ms);
+    });
+}
+
 }  // extern "C"
 
 namespace {
@@ -2904,7 +2931,7 @@ void run_job(const char *const *files, size_t n_files, uint32_t R, int app, cons
     g_run.ms_open = ms_since(t0);
     // ---- map phase: GPU g reads and maps files m with m % G == g (coordinator.rs:137-176)
     const int readers = (int)std::max<uint64_t>(1, env_u64("MRG_READ_THREADS", std::max(1, std::min(16, 32 / G))));
-    std::vector<double> t_read(G, 0.0);
+    std::vector<double> t_read(G, 0.0), t_alloc(G, 0.0);
     t0 = Clock::now();
     run_ranks(rs, false, [&](RankState &r) {
         mrg_ctx *c = r.c;
@@ -2929,11 +2956,16 @@ void run_job(const char *const *files, size_t n_files, uint32_t R, int app, cons
         c->d_in = r.d;
         c->doc_off = off;
         c->doc_ids = ids;
+        double a0 = 0.0, a1 = 0.0;
+        c->pool.alloc_stats(nullptr, nullptr, &a0);
         job_map(c);
+        c->pool.alloc_stats(nullptr, nullptr, &a1);
+        t_alloc[r.g] = a1 - a0;
     }, rc, msg);
     raise_first(rc, msg, rs);
     g_run.ms_map = ms_since(t0);
     for (int g = 0; g < G; ++g) {
+        g_run.ms_map_alloc = std::max(g_run.ms_map_alloc, t_alloc[g]);
         g_run.ms_read = std::max(g_run.ms_read, t_read[g]);
         g_run.input_bytes += rs[g].in_bytes;
     }

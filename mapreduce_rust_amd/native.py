@@ -14,7 +14,7 @@ APP_INDEXER = 1
 FLAG_NO_COMPAT_DROP_LAST = 0x1
 FLAG_FINAL_TXT = 0x2
 XREC_BYTES = 24  # include/mrgpu.h MRG_XREC_BYTES (ABI 3)
-ABI_VERSION = 5  # include/mrgpu.h MRG_ABI_VERSION
+ABI_VERSION = 6  # include/mrgpu.h MRG_ABI_VERSION
 
 OK, EINVAL, EUTF8, EHIP, ENOMEM, EIO, ECOMM = 0, -1, -2, -3, -4, -5, -6
 _CODES = {EINVAL: "EINVAL", EUTF8: "EUTF8", EHIP: "EHIP", ENOMEM: "ENOMEM", EIO: "EIO", ECOMM: "ECOMM"}
@@ -67,7 +67,8 @@ class RunStats(C.Structure):
     """mrg_run_stats: wall-clock phases of the last mrg_run_job on this thread."""
     _fields_ = [("ms_total", C.c_double), ("ms_open", C.c_double), ("ms_read", C.c_double), ("ms_map", C.c_double),
                 ("ms_shuffle", C.c_double), ("ms_reduce", C.c_double), ("ms_write", C.c_double),
-                ("input_bytes", C.c_uint64), ("output_bytes", C.c_uint64), ("n_gpus", C.c_int)]
+                ("input_bytes", C.c_uint64), ("output_bytes", C.c_uint64), ("n_gpus", C.c_int),
+                ("ms_map_alloc", C.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -117,6 +118,7 @@ _SIGS = {
     "mrg_job_shuffle": (C.c_int, [_vp, _vp]),
     "mrg_comm_count": (C.c_int, [_vp, C.POINTER(C.c_int)]),
     "mrg_pool_stats": (C.c_int, [_vp, _u64p, _u64p]),
+    "mrg_pool_alloc_stats": (C.c_int, [_vp, _u64p, _u64p, C.POINTER(C.c_double)]),
     "mrg_free": (None, [_vp]),
     "mrg_gen_zipf": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_double]),
     "mrg_gen_unique": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64]),
@@ -217,6 +219,12 @@ class Context:
         n, b = C.c_uint64(), C.c_uint64()
         _check(load().mrg_pool_stats(self.h, C.byref(n), C.byref(b)))
         return n.value, b.value
+
+    def pool_alloc_stats(self):
+        """mrg_pool_alloc_stats: (hipMalloc calls, bytes, host ms spent in them) since the context opened."""
+        n, b, ms = C.c_uint64(), C.c_uint64(), C.c_double()
+        _check(load().mrg_pool_alloc_stats(self.h, C.byref(n), C.byref(b), C.byref(ms)))
+        return n.value, b.value, ms.value
 
     def set_timing(self, on=True):
         _check(load().mrg_set_timing(self.h, 1 if on else 0))

@@ -26,7 +26,7 @@ pub const fn mrg_flag_debug_hash_bits(n: u32) -> u32 {
     (n & 0xFF) << 8
 }
 pub const MRG_XREC_BYTES: usize = 24;
-pub const MRG_ABI_VERSION: u32 = 5;
+pub const MRG_ABI_VERSION: u32 = 6;
 pub const MRG_COMM_ID_BYTES: usize = 128;
 
 #[repr(C)]
@@ -83,6 +83,7 @@ pub struct mrg_run_stats {
     pub input_bytes: u64,
     pub output_bytes: u64,
     pub n_gpus: c_int,
+    pub ms_map_alloc: f64,
 }
 
 extern "C" {
@@ -118,6 +119,7 @@ extern "C" {
     pub fn mrg_comm_count(comm: *const mrg_comm, n_ranks: *mut c_int) -> c_int;
 
     pub fn mrg_pool_stats(ctx: *mut mrg_ctx, outstanding: *mut u64, held_bytes: *mut u64) -> c_int;
+    pub fn mrg_pool_alloc_stats(ctx: *mut mrg_ctx, n_allocs: *mut u64, alloc_bytes: *mut u64, alloc_ms: *mut f64) -> c_int;
 
     pub fn mrg_map(ctx: *mut mrg_ctx, app: c_int, h_bytes: *const u8, n: usize, doc: *const c_char, doc_id: u32,
                    n_reduce: u32, flags: u32, out: *mut *mut mrg_parts) -> c_int;

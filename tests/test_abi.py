@@ -48,12 +48,12 @@ def test_no_gpu_is_a_clean_error():
 
 def test_record_layout_constant():
     src = open(os.path.join(ROOT, "include", "mrgpu.h")).read()
-    assert "#define MRG_XREC_BYTES 24" in src and "#define MRG_ABI_VERSION 5" in src
+    assert "#define MRG_XREC_BYTES 24" in src and "#define MRG_ABI_VERSION 6" in src
     from mapreduce_rust_amd import native, shuffle
-    assert native.XREC_BYTES == shuffle.XREC == 24 and native.ABI_VERSION == 5
-    assert b"abi 5" in native.load().mrg_version()
+    assert native.XREC_BYTES == shuffle.XREC == 24 and native.ABI_VERSION == 6
+    assert b"abi 6" in native.load().mrg_version()
     rs = open(os.path.join(ROOT, "mrgpu-sys", "src", "lib.rs")).read()
-    assert "pub const MRG_XREC_BYTES: usize = 24;" in rs and "pub const MRG_ABI_VERSION: u32 = 5;" in rs
+    assert "pub const MRG_XREC_BYTES: usize = 24;" in rs and "pub const MRG_ABI_VERSION: u32 = 6;" in rs
 
 
 def test_merge_sorted_lines_host():

@@ -89,27 +89,60 @@ def test_c3_full_size_vs_oracle(ctx):
     assert [sha(g) for g in got] == [sha(e) for e in exp]
 
 
-def test_c5_slice_vs_oracle(ctx):
-    """configs[4] (1e9 near-unique keys), a 1 GiB slice: 4 x 256 MiB, ~8e7 distinct 12-byte keys.  The
-    first job takes the LDS-combine map and the wide (sort-based) aggregation; the second, on the same
-    context, the wide map (the sample of the input is near-unique: keys straight to their sort
-    buckets).  Both byte-identical to the oracle."""
+def test_c5_slice_vs_oracle(ctx, knobs):
+    """configs[4] (1e9 near-unique keys), a 1 GiB slice: 4 x 256 MiB, ~8e7 distinct 12-byte keys.
+    (1) The FIRST job of a fresh context -- what every mrg_run_job / one-shot worker call is -- samples
+    the input, finds it near-unique and takes the wide map in ONE launch (r06; until r05 the cold job
+    ran the LDS-combine map, overflowed and reran it).  (2) A second job on that context: the wide map
+    again.  (3) The LDS-combine map with the wide (sort-based) aggregation behind it (MRG_WIDE_MAP=0
+    rules the wide map out; the aggregation switches to the wide path by the map's counters).  All
+    byte-identical to the oracle."""
+    import mapreduce_rust_amd as M
     import oracle_lib as O
     nf, fb = 4, 256 * MIB
     buf = _generate(ctx, "unique", nf, fb, 0xC5C5)
-    got = _run_job(ctx, buf, nf, fb, 64)
-    st = ctx.stats()
-    got2 = _run_job(ctx, buf, nf, fb, 64)
-    st2 = ctx.stats()
+    knobs()
+    with M.Context(0) as fresh:
+        got = _run_job(fresh, buf, nf, fb, 64)
+        st = fresh.stats()
+        got2 = _run_job(fresh, buf, nf, fb, 64)
+        st2 = fresh.stats()
+    knobs(MRG_WIDE_MAP=0)
+    got3 = _run_job(ctx, buf, nf, fb, 64)
+    st3 = ctx.stats()
+    knobs()
     files = _host_files(buf, nf, fb)
     del buf
-    assert st["distinct_keys"] > 70_000_000 and st["agg_path"] == 2 and st["map_kind"] == 0
-    assert st2["map_kind"] == 1 and st2["distinct_keys"] == st["distinct_keys"]
+    assert st["distinct_keys"] > 70_000_000
+    assert st["map_kind"] == 1 and st["map_launches"] == 1 and st["agg_path"] == 2, st
+    assert st2["map_kind"] == 1 and st2["map_launches"] == 1 and st2["distinct_keys"] == st["distinct_keys"]
+    assert st3["map_kind"] == 0 and st3["agg_path"] == 2 and st3["distinct_keys"] == st["distinct_keys"], st3
     exp = O.wc_mt(files, 64, threads=THREADS)
-    assert len(got) == len(exp) == len(got2)
+    assert len(got) == len(exp) == len(got2) == len(got3)
     for r in range(64):
         assert got[r] == exp[r], r
         assert got2[r] == exp[r], r
+        assert got3[r] == exp[r], r
+
+
+def test_cold_context_zipf_takes_bucket_path_vs_oracle(ctx):
+    """The cold-context sample on text with repeats (a 512 MiB Zipf slice of C3): the FIRST job of a
+    fresh context samples, finds repeats, and takes the LDS-combine map + bucket aggregation in one map
+    launch; byte-identical to the oracle."""
+    import mapreduce_rust_amd as M
+    import oracle_lib as O
+    nf, fb = 2, 256 * MIB
+    buf = _generate(ctx, "zipf", nf, fb, 0x5EED2026)
+    with M.Context(0) as fresh:
+        got = _run_job(fresh, buf, nf, fb, 64)
+        st = fresh.stats()
+        n_alloc, alloc_bytes, alloc_ms = fresh.pool_alloc_stats()
+    files = _host_files(buf, nf, fb)
+    del buf
+    assert st["map_kind"] == 0 and st["agg_path"] == 1 and st["map_launches"] == 1, st
+    assert n_alloc > 0 and alloc_bytes > 0 and alloc_ms >= 0.0
+    exp = O.wc_mt(files, 64, threads=THREADS)
+    assert [sha(g) for g in got] == [sha(e) for e in exp]
 
 
 @pytest.mark.parametrize("knob", [{}, {"MRG_TEST_WMAP_CAP": 2}, {"MRG_TEST_WMAP_B1R": 1}, {"MRG_TEST_WMAP_B1R": 3},
