@@ -895,14 +895,15 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         s_fill = 0;
         s_lcnt = 0;
     }
-    if (tid < 9 * 64) {
-        const uint32_t blk = tid < 512 ? (uint32_t)tid >> 6 : 0x20u;
-        s_uc[tid] = c_uclass_stage2[c_uclass_stage1[blk] * 64u + ((uint32_t)tid & 63u)];
+    // (strided: a workgroup of fewer than 1024 threads -- the occupancy-sweep builds -- fills them too)
+    for (int i = tid; i < 9 * 64; i += WG) {
+        const uint32_t blk = i < 512 ? (uint32_t)i >> 6 : 0x20u;
+        s_uc[i] = c_uclass_stage2[c_uclass_stage1[blk] * 64u + ((uint32_t)i & 63u)];
     }
-    if (tid < 1024) {
-        const uint32_t v = (uint32_t)tid & 255u, c = mrg_uclass(v & 127u);
+    for (int i = tid; i < 1024; i += WG) {
+        const uint32_t v = (uint32_t)i & 255u, c = mrg_uclass(v & 127u);
         const uint32_t ws = v >= 128u ? 0x11u : ((c == MRG_CLS_W ? 1u : 0u) | (c == MRG_CLS_S ? 0x10u : 0u));
-        s_lut[tid >> 8][v] = (uint8_t)(ws << (tid >> 8));
+        s_lut[i >> 8][v] = (uint8_t)(ws << (i >> 8));
     }
     auto zmask = [](uint32_t L, uint32_t j) {  // word j, byte p (p = 0 least significant) holds key byte 4j + 3 - p
         uint32_t m = 0;

@@ -1886,6 +1886,12 @@ __global__ void k_wdrop(const uint32_t *nleaf, uint32_t B1r, uint32_t R, const u
 // lengths (whole dwords: the first and last are shared with the neighbour lines), then the stage
 // is stored as aligned dwords (byte stores only at the two ends of a chunk) and zeroed on the way.
 // 512-thread workgroups, several per CU: while one formats, the others load and store.
+#ifndef MRG_WIDE_WWAVE
+#define MRG_WIDE_WWAVE 0   // 1: one wave per leaf (k_wwritew), 0: one workgroup per L1 bucket (k_wwrite)
+#endif
+#ifndef MRG_WIDE_WST
+#define MRG_WIDE_WST 1   // r06: the stage stored as 16-byte vectors (was dwords)
+#endif
 constexpr uint32_t W_WWG = 512;
 constexpr uint32_t W_WCH = W_WWG;             // keys per chunk
 constexpr uint32_t W_STAGE = 40 * W_WCH;      // >= W_WCH lines of <= 16 + 1 + 20 + 1 bytes (+ 3 of shift)
@@ -1941,7 +1947,8 @@ __global__ __launch_bounds__(W_WWG) void k_wwrite(const uint64_t *keys, const ui
                                                     const uint32_t *nleaf, const uint64_t *leaf_out,
                                                     const uint32_t *leaf_nd, const uint32_t *leaf_drop,
                                                     const uint64_t *leaf_off, uint8_t *out) {
-    __shared__ uint32_t s_buf[W_STAGE / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t s_buf[W_STAGE / 4];
+    static_assert(W_STAGE >= 15 + 38 * W_WCH + 4 * 11, "a chunk's lines (<= 38 bytes each) at a 0..15-byte stage shift");
     __shared__ uint32_t s_kst[MRG_WIDE_MAXB2 + 1];   // keys before leaf l (this bucket)
     __shared__ uint64_t s_lout[MRG_WIDE_MAXB2];      // first key slot of leaf l; bit 63: counts packed
     __shared__ uint32_t s_ws[W_WWG / 64];
@@ -2008,7 +2015,8 @@ __global__ __launch_bounds__(W_WWG) void k_wwrite(const uint64_t *keys, const ui
         const uint32_t ll = c0 + tid < K ? line_words(cur.a, cur.c, cur.n, w) : 0u;
         uint32_t tot;
         const uint32_t at = block_scan_excl<W_WWG / 64>(ll, s_ws, &tot);
-        const uint32_t sh = (uint32_t)(dst & 3u);   // stage at (dst & 3): output dwords align in LDS
+        // stage at the output's offset in its 16-byte (MRG_WIDE_WST; else 4-byte) unit: output vectors align in LDS
+        const uint32_t sh = (uint32_t)(dst & (MRG_WIDE_WST ? 15u : 3u));
         if (ll) {
             const uint32_t o = sh + at, base = o >> 2, bs = 8u * (o & 3u);
             const uint32_t ndw = ((o & 3u) + ll + 3u) >> 2;
@@ -2024,6 +2032,16 @@ __global__ __launch_bounds__(W_WWG) void k_wwrite(const uint64_t *keys, const ui
         }
         lds_barrier();
         const uint64_t end = dst + tot;
+#if MRG_WIDE_WST
+        // whole 16-byte vectors (one dwordx4 store per lane: a 1 KiB wave store), bytes at the two ends
+        const uint64_t a16 = (dst + 15u) & ~15ull, e16 = end & ~15ull;
+        for (uint64_t x = dst + tid; x < min(a16, end); x += W_WWG) out[x] = sb[sh + (x - dst)];
+        for (uint64_t x = max(e16, a16) + tid; x < end; x += W_WWG) out[x] = sb[sh + (x - dst)];
+        for (uint64_t v = a16 / 16 + tid; v < e16 / 16; v += W_WWG) {
+            const uint32_t i = (sh + (uint32_t)(v * 16 - dst)) / 16;
+            reinterpret_cast<uint4 *>(out)[v] = reinterpret_cast<const uint4 *>(s_buf)[i];
+        }
+#else
         const uint64_t a4 = (dst + 3u) & ~3ull, e4 = end & ~3ull;
         for (uint64_t x = dst + tid; x < min(a4, end); x += W_WWG) out[x] = sb[sh + (x - dst)];
         for (uint64_t x = max(e4, a4) + tid; x < end; x += W_WWG) out[x] = sb[sh + (x - dst)];
@@ -2031,12 +2049,110 @@ __global__ __launch_bounds__(W_WWG) void k_wwrite(const uint64_t *keys, const ui
             const uint32_t i = (sh + (uint32_t)(w4 * 4 - dst)) / 4;
             reinterpret_cast<uint32_t *>(out)[w4] = s_buf[i];
         }
+#endif
         lds_barrier();
         // zero what this chunk used (its byte-stored ends included) for the next chunk's ORs
         for (uint32_t i = tid; i < (sh + tot + 3u) / 4u; i += W_WWG) s_buf[i] = 0;
         dst = end;
         lds_barrier();
         cur = nxt;
+    }
+}
+
+// r06: the same lines, one WAVE per leaf and no workgroup barrier.  A leaf's text starts at
+// leaf_off[leaf] (the scan of the leaves' line bytes after the drop), so waves write their leaves
+// independently: 64 keys per step, line lengths by a wave scan, the lines OR-ed into the wave's own LDS
+// stage, whole 16-byte vectors stored, the partial last vector carried to the next step at the
+// stage's start; bytes only at the leaf's two ends (the vectors it shares with its neighbours).
+constexpr uint32_t WW_WG = 256, WW_NW = WW_WG / 64;
+constexpr uint32_t WW_PER = 16;                          // workgroups per L1 bucket (64 waves stride its leaves)
+constexpr uint32_t WW_STGW = (16 + 64 * 38 + 64) / 4;   // stage dwords per wave: carried vector + 64 lines + slack
+__device__ __forceinline__ void ww_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__global__ __launch_bounds__(WW_WG) void k_wwritew(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *leaf_pk,
+                                                  const uint32_t *nleaf, const uint64_t *leaf_out,
+                                                  const uint32_t *leaf_nd, const uint32_t *leaf_drop,
+                                                  const uint64_t *leaf_off, uint8_t *out) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_stg[WW_NW][WW_STGW];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t b = blockIdx.x / WW_PER, g = (blockIdx.x % WW_PER) * WW_NW + wv;
+    const uint32_t nl = nleaf[b];
+    uint32_t *stg = s_stg[wv];
+    const uint8_t *sb = reinterpret_cast<const uint8_t *>(stg);
+    for (uint32_t i = lane; i < WW_STGW; i += 64u) stg[i] = 0;
+    ww_sync();
+    typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+    const v2 *kv = reinterpret_cast<const v2 *>(keys);
+    for (uint32_t j = g; j < nl; j += WW_PER * WW_NW) {
+        const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + j;
+        const uint32_t K = leaf_nd[lid] - (leaf_drop[lid] ? 1u : 0u);
+        if (K == 0u) continue;
+        const uint64_t o0 = leaf_out[lid];
+        const bool pk = leaf_pk[lid] != 0u;
+        const uint64_t lstart = leaf_off[lid];
+        uint64_t dst = lstart;                 // next output byte; the stage holds [dst - sh, ...)
+        uint32_t sh = (uint32_t)(dst & 15u);
+        for (uint32_t c0 = 0; c0 < K; c0 += 64u) {
+            const uint32_t i = c0 + lane;
+            uint64_t w[5];
+            uint32_t ll = 0;
+            if (i < K) {
+                const v2 kk = kv[o0 + i];
+                uint64_t c = kk.y, n;
+                if (pk) {
+                    n = c & 0xFFFFFFFFull;
+                    c &= ~0xFFFFFFFFull;
+                } else {
+                    n = ocnt[o0 + i];
+                }
+                ll = line_words(kk.x, c, n, w);
+            }
+            const uint32_t incl = wave_scan_incl(ll), tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            if (ll) {
+                const uint32_t o = sh + incl - ll, base = o >> 2, bs = 8u * (o & 3u);
+                const uint32_t ndw = ((o & 3u) + ll + 3u) >> 2;
+                uint32_t prev = 0;
+#pragma unroll
+                for (uint32_t x = 0; x < 10; ++x) {
+                    const uint32_t d = (uint32_t)(w[x >> 1] >> (32u * (x & 1u)));
+                    const uint32_t e = (d << bs) | (bs ? prev >> (32u - bs) : 0u);
+                    prev = d;
+                    if (x < ndw) atomicOr(&stg[base + x], e);
+                }
+                if (10u < ndw) atomicOr(&stg[base + 10u], prev >> (32u - bs));
+            }
+            ww_sync();
+            const uint64_t end = dst + tot, vb = dst - sh;   // stage byte 0 = output byte vb (16-aligned)
+            const bool last = c0 + 64u >= K;
+            const uint32_t nfull = (uint32_t)((end - vb) >> 4);   // whole vectors of the stage
+            // vector 0 of the leaf's first step holds the previous leaf's last bytes: bytes from lstart on
+            if (c0 == 0u && sh != 0u) {
+                const uint32_t e0 = (uint32_t)min<uint64_t>(16u, end - vb);
+                if (lane >= sh && lane < e0) out[vb + lane] = sb[lane];
+            }
+            for (uint32_t v = lane; v < nfull; v += 64u)
+                if (v != 0u || c0 != 0u || sh == 0u)
+                    reinterpret_cast<uint4 *>(out + vb)[v] = reinterpret_cast<const uint4 *>(stg)[v];
+            const uint32_t rem = (uint32_t)(end - vb) & 15u;   // bytes of the partial last vector
+            if (last) {   // the leaf's last bytes (shared with the next leaf's first vector)
+                if (lane < rem && !(nfull == 0u && c0 == 0u && vb + lane < lstart)) out[vb + 16u * nfull + lane] = sb[16u * nfull + lane];
+            }
+            ww_sync();
+            // carry the partial vector to the stage's start (or clear it after the leaf) and zero the rest
+            uint32_t cv = 0;
+            if (lane < 4u) cv = stg[4u * nfull + lane];
+            const uint32_t used = (16u * nfull + rem + 3u) >> 2;
+            ww_sync();
+            for (uint32_t x = lane; x < used; x += 64u) stg[x] = 0;
+            ww_sync();
+            if (!last && lane < 4u) stg[lane] = cv;
+            ww_sync();
+            dst = end;
+            sh = rem;
+        }
     }
 }
 
@@ -2309,8 +2425,13 @@ void mrg_wide_launch_drop(const uint32_t *nleaf, uint32_t B1r, uint32_t R, const
 void mrg_wide_launch_write(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *leaf_pk, const uint32_t *nleaf,
                            const uint64_t *leaf_out, const uint32_t *leaf_nd, const uint32_t *leaf_drop,
                            const uint64_t *leaf_off, uint32_t B1, uint8_t *out, hipStream_t s) {
+#if MRG_WIDE_WWAVE
+    hipLaunchKernelGGL(k_wwritew, dim3(B1 * WW_PER), dim3(WW_WG), 0, s, keys, ocnt, leaf_pk, nleaf, leaf_out, leaf_nd,
+                       leaf_drop, leaf_off, out);
+#else
     hipLaunchKernelGGL(k_wwrite, dim3(B1), dim3(W_WWG), 0, s, keys, ocnt, leaf_pk, nleaf, leaf_out, leaf_nd, leaf_drop,
                        leaf_off, out);
+#endif
 }
 void mrg_wide_launch_part_off(const uint64_t *leaf_off, uint32_t B1r, uint32_t R, uint64_t total, uint64_t *part_off,
                               hipStream_t s) {

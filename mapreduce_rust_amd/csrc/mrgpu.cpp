@@ -104,8 +104,66 @@ int guard(F &&f) {
 }
 
 // ---------------------------------------------------------------- caching device allocator
+// Process-wide cache of the device blocks of closed contexts, per device (r06).  A worker process runs
+// one task after another (src/bin/mrworker.rs:43-149); every mrg_run_job opens fresh contexts, and
+// without this each call re-allocated -- and the GPU re-touched -- its multi-GiB workspaces (the first
+// job's map ran 1.2x its steady time).  Capped at MRG_POOL_KEEP_GIB per device (default 64; 0 = off);
+// blocks beyond the cap are freed.  Never destroyed: no hipFree may run after the HIP runtime's own
+// teardown at process exit.
+class DeviceCache {
+   public:
+    static DeviceCache &get() {
+        static DeviceCache *c = new DeviceCache();
+        return *c;
+    }
+    // a cached block of `dev` of at least c bytes and at most c + c / 4 (its size in *got), else null
+    void *take(int dev, size_t c, size_t *got) {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto &f = free_[dev];
+        auto it = f.lower_bound(c);
+        if (it == f.end() || it->first > c + (c >> 2)) return nullptr;
+        void *p = it->second;
+        *got = it->first;
+        bytes_[dev] -= it->first;
+        f.erase(it);
+        return p;
+    }
+    // a block of a closing context (its work on the device finished); the current device is `dev`
+    void give(int dev, void *p, size_t c) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (bytes_[dev] + c <= keep_) {
+                free_[dev].insert({c, p});
+                bytes_[dev] += c;
+                return;
+            }
+        }
+        (void)hipFree(p);
+    }
+    void trim(int dev) {  // the device is full: give the cached blocks back to the driver
+        std::multimap<size_t, void *> f;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            f.swap(free_[dev]);
+            bytes_[dev] = 0;
+        }
+        for (auto &kv : f) (void)hipFree(kv.second);
+    }
+
+   private:
+    DeviceCache() {
+        const char *v = getenv("MRG_POOL_KEEP_GIB");
+        keep_ = (size_t)((v ? atof(v) : 64.0) * (double)((size_t)1 << 30));
+    }
+    std::mutex mu_;
+    std::map<int, std::multimap<size_t, void *>> free_;
+    std::map<int, size_t> bytes_;
+    size_t keep_ = 0;
+};
+
 class Pool : public DevPool {
    public:
+    void set_device(int dev) { dev_ = dev; }
     void *get(size_t bytes) override {
         const size_t c = cls(bytes ? bytes : 1);
         // smallest free block of this class or up to two classes above (record counts drift by a few
@@ -116,6 +174,14 @@ class Pool : public DevPool {
             void *p = it->second;
             free_.erase(it);
             return p;
+        }
+        if (dev_ >= 0) {  // a block a closed context of this device left behind
+            size_t got = 0;
+            if (void *q = DeviceCache::get().take(dev_, c, &got)) {
+                size_[q] = got;
+                ++reused_;
+                return q;
+            }
         }
         void *p = nullptr;
         if (debug_) fprintf(stderr, "[mrgpu] pool: allocating %zu bytes\n", c);
@@ -147,6 +213,7 @@ class Pool : public DevPool {
             size_.erase(kv.second);
         }
         free_.clear();
+        if (dev_ >= 0) DeviceCache::get().trim(dev_);
     }
     // blocks handed out and not returned; bytes held by the pool (handed out or cached)
     uint64_t outstanding() const { return size_.size() - free_.size(); }
@@ -162,9 +229,13 @@ class Pool : public DevPool {
         if (bytes) *bytes = alloc_bytes_;
         if (ms) *ms = alloc_ms_;
     }
-    ~Pool() override {
+    uint64_t reused() const { return reused_; }  // blocks taken from the process-wide device cache
+    ~Pool() override {  // (the caller has made dev_ current)
         (void)hipDeviceSynchronize();
-        for (auto &kv : size_) (void)hipFree(kv.first);
+        for (auto &kv : size_) {
+            if (dev_ >= 0) DeviceCache::get().give(dev_, kv.first, kv.second);
+            else (void)hipFree(kv.first);
+        }
     }
 
    private:
@@ -178,7 +249,8 @@ class Pool : public DevPool {
     std::multimap<size_t, void *> free_;
     std::unordered_map<void *, size_t> size_;
     bool debug_ = getenv("MRG_DEBUG") != nullptr;
-    uint64_t allocs_ = 0, alloc_bytes_ = 0;
+    uint64_t allocs_ = 0, alloc_bytes_ = 0, reused_ = 0;
+    int dev_ = -1;
     double alloc_ms_ = 0.0;
 };
 
@@ -2304,6 +2376,7 @@ int mrg_open(int device, mrg_ctx **out) {
         HIPCHK(hipSetDevice(device));
         mrg_ctx *c = new mrg_ctx();
         c->device = device;
+        c->pool.set_device(device);
         HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
         c->stream = c->own;
         HIPCHK(hipMalloc(&c->d_cnt, sizeof(unsigned long long) * CNT_N));
