@@ -1887,7 +1887,7 @@ __global__ void k_wdrop(const uint32_t *nleaf, uint32_t B1r, uint32_t R, const u
 // is stored as aligned dwords (byte stores only at the two ends of a chunk) and zeroed on the way.
 // 512-thread workgroups, several per CU: while one formats, the others load and store.
 #ifndef MRG_WIDE_WWAVE
-#define MRG_WIDE_WWAVE 0   // 1: one wave per leaf (k_wwritew), 0: one workgroup per L1 bucket (k_wwrite)
+#define MRG_WIDE_WWAVE 1   // 1: one wave per leaf (k_wwritew, r06: C5 format -23 %), 0: one workgroup per L1 bucket (k_wwrite)
 #endif
 #ifndef MRG_WIDE_WST
 #define MRG_WIDE_WST 1   // r06: the stage stored as 16-byte vectors (was dwords)
@@ -2067,10 +2067,9 @@ __global__ __launch_bounds__(W_WWG) void k_wwrite(const uint64_t *keys, const ui
 constexpr uint32_t WW_WG = 256, WW_NW = WW_WG / 64;
 constexpr uint32_t WW_PER = 16;                          // workgroups per L1 bucket (64 waves stride its leaves)
 constexpr uint32_t WW_STGW = (16 + 64 * 38 + 64) / 4;   // stage dwords per wave: carried vector + 64 lines + slack
-__device__ __forceinline__ void ww_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+__device__ __forceinline__ void ww_sync() {   // the wave's LDS ops so far have completed (atomics included)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 __global__ __launch_bounds__(WW_WG) void k_wwritew(const uint64_t *keys, const uint64_t *ocnt, const uint32_t *leaf_pk,
                                                   const uint32_t *nleaf, const uint64_t *leaf_out,
@@ -2096,20 +2095,18 @@ __global__ __launch_bounds__(WW_WG) void k_wwritew(const uint64_t *keys, const u
         uint64_t dst = lstart;                 // next output byte; the stage holds [dst - sh, ...)
         uint32_t sh = (uint32_t)(dst & 15u);
         for (uint32_t c0 = 0; c0 < K; c0 += 64u) {
+            // every lane formats a line (inactive lanes the leaf's first key, then ll = 0): an earlier
+            // version with the load and format inside `if (i < K)` wrote a stray 0x83 into 1 % of the
+            // lines (the compiled divergent block; found by byte comparison with k_wwrite, tools/dbg_ww.py)
             const uint32_t i = c0 + lane;
-            uint64_t w[5];
-            uint32_t ll = 0;
-            if (i < K) {
-                const v2 kk = kv[o0 + i];
-                uint64_t c = kk.y, n;
-                if (pk) {
-                    n = c & 0xFFFFFFFFull;
-                    c &= ~0xFFFFFFFFull;
-                } else {
-                    n = ocnt[o0 + i];
-                }
-                ll = line_words(kk.x, c, n, w);
-            }
+            const bool act = i < K;
+            const uint64_t slot = o0 + (act ? i : 0u);
+            const v2 kk = kv[slot];
+            const uint64_t nw = pk ? (kk.y & 0xFFFFFFFFull) : ocnt[slot];
+            const uint64_t c = pk ? (kk.y & ~0xFFFFFFFFull) : kk.y;
+            uint64_t w[5] = {0, 0, 0, 0, 0};
+            const uint32_t lw = line_words(kk.x, c, nw, w);
+            const uint32_t ll = act ? lw : 0u;
             const uint32_t incl = wave_scan_incl(ll), tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
             if (ll) {
                 const uint32_t o = sh + incl - ll, base = o >> 2, bs = 8u * (o & 3u);

@@ -1747,6 +1747,7 @@ void wide_reduce(mrg_ctx *c) {
         c->out_cap = total + 16;
         c->d_out = pget<uint8_t>(p, c->out_cap);
     }
+    if (getenv("MRG_DEBUG_FILL_OUT")) HIPCHK(hipMemsetAsync(c->d_out, 0xEE, total, s));  // diagnostics: unwritten bytes show
     mrg_wide_launch_write(w.kout, w.ocnt, w.leaf_pk, w.nleaf, w.leaf_out, w.leaf_nd, drop, off, w.B1, c->d_out, s);
     uint64_t *poff = pget<uint64_t>(p, c->R + 1);
     mrg_wide_launch_part_off(off, w.B1r, c->R, total, poff, s);
