@@ -175,8 +175,8 @@ def end_to_end(buf, files, fbytes, n_reduce):
             M.native.run_job(c1p, 10, M.APP_WC, out)
             lat.append((time.perf_counter() - t0) * 1e3)
         res = {"end_to_end_gbs": round(n / wall / 1e9, 3), "ms": round(wall * 1e3, 1),
-               "phases_ms": {k: round(st[k], 1) for k in ("ms_open", "ms_read", "ms_map", "ms_map_alloc", "ms_shuffle",
-                                                          "ms_reduce", "ms_write")},
+               "phases_ms": {k: round(st[k], 2) for k in ("ms_open", "ms_read", "ms_map", "ms_map_alloc", "ms_map_kernel",
+                                                          "ms_aggregate_kernel", "ms_shuffle", "ms_reduce", "ms_write")},
                "input_bytes": n, "output_bytes": st["output_bytes"],
                "read_gbs": round(n / (st["ms_read"] / 1e3) / 1e9, 2) if st["ms_read"] > 0 else None,
                "c1_latency_ms": round(statistics.median(lat), 2),

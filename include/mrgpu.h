@@ -246,6 +246,8 @@ typedef struct {
     int n_gpus;
     double ms_map_alloc;    /* of ms_map: host time inside the fresh contexts' device allocations (slowest
                                GPU; every mrg_run_job opens fresh contexts, ABI 6) */
+    double ms_map_kernel;       /* of ms_map: the map kernel (HIP events, slowest GPU; ABI 6) */
+    double ms_aggregate_kernel; /* of ms_map: the aggregation after it (HIP events, slowest GPU; ABI 6) */
 } mrg_run_stats;
 int mrg_run_get_stats(mrg_run_stats *out);
 

@@ -259,6 +259,40 @@ __global__ void k_wsample_dups(const SortRec *r, uint32_t S, unsigned long long 
     if ((threadIdx.x & 63u) == 0 && m16) atomicAdd(dups + 1, (unsigned long long)__popcll(m16));
 }
 
+// The cold-context decision (r06): S <= W_UQ / 2 unsorted samples, one workgroup, an LDS set of 64-bit
+// fingerprints of (part, key): dups[0] = samples whose fingerprint an earlier sample already holds (= S -
+// distinct, the sorted test's adjacent-equal count up to fingerprint collisions: a heuristic either way),
+// dups[1] = keys of 13..16 bytes.  One launch and no sort, so a job on text with repeats pays ~20 us for
+// the test instead of the full sample's radix sort.
+constexpr uint32_t W_UQ = 16384;
+__global__ __launch_bounds__(1024) void k_wsample_uniq(const SortRec *r, uint32_t S, unsigned long long *dups) {
+    __shared__ unsigned long long s_fp[W_UQ];
+    __shared__ unsigned int s_n[2];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < W_UQ; i += 1024u) s_fp[i] = 0ull;
+    if (tid < 2u) s_n[tid] = 0u;
+    __syncthreads();
+    uint32_t nd = 0, n16 = 0;
+    for (uint32_t j = tid; j < S; j += 1024u) {
+        const SortRec x = r[j];
+        const uint64_t fp = mrg_fmix64(x.k0 ^ mrg_fmix64(x.k1 ^ ((uint64_t)x.part << 32))) | 1ull;   // never 0 (= empty)
+        n16 += (uint32_t)x.k1 != 0u ? 1u : 0u;
+        uint32_t h = (uint32_t)(fp >> 40) & (W_UQ - 1u);
+        for (uint32_t k = 0; k < W_UQ; ++k, h = (h + 1u) & (W_UQ - 1u)) {
+            const unsigned long long old = atomicCAS(&s_fp[h], 0ull, (unsigned long long)fp);
+            if (old == 0ull) break;
+            if (old == fp) { ++nd; break; }
+        }
+    }
+    if (nd) atomicAdd(&s_n[0], nd);
+    if (n16) atomicAdd(&s_n[1], n16);
+    __syncthreads();
+    if (tid == 0) {
+        dups[0] = s_n[0];
+        dups[1] = s_n[1];
+    }
+}
+
 struct L1Args {
     BucketArgs A;
     const uint64_t *off;     // main segment offsets [nseg + 1]
@@ -2445,6 +2479,10 @@ void mrg_wide_launch_sample_text(const uint8_t *in, const uint64_t *doc_off, uin
                                  uint32_t S, uint32_t R, SortRec *out, hipStream_t s) {
     if (S) hipLaunchKernelGGL(k_wsample_text, dim3((S + 255) / 256), dim3(256), 0, s, in, doc_off, n_docs, total, S, R,
                               out);
+}
+void mrg_wide_launch_sample_uniq(const SortRec *r, uint32_t S, unsigned long long *dups, hipStream_t s) {
+    if (S > W_UQ / 2) S = W_UQ / 2;
+    hipLaunchKernelGGL(k_wsample_uniq, dim3(1), dim3(1024), 0, s, r, S, dups);
 }
 void mrg_wide_launch_sample_dups(const SortRec *r, uint32_t S, unsigned long long *dups, hipStream_t s) {
     if (S) hipLaunchKernelGGL(k_wsample_dups, dim3((S + 255) / 256), dim3(256), 0, s, r, S, dups);

@@ -404,6 +404,8 @@ void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstar
 void mrg_wide_launch_sample_text(const uint8_t *in, const uint64_t *doc_off, uint32_t n_docs, uint64_t total,
                                  uint32_t S, uint32_t R, SortRec *out, hipStream_t s);
 void mrg_wide_launch_sample_dups(const SortRec *r, uint32_t S, unsigned long long *dups, hipStream_t s);
+// the cold-context near-unique test: S (<= 8192) unsorted samples, dups[0] = repeats, dups[1] = 13..16-byte keys
+void mrg_wide_launch_sample_uniq(const SortRec *r, uint32_t S, unsigned long long *dups, hipStream_t s);
 void mrg_wide_launch_l1ix(const uint64_t *spl1, uint32_t R, uint32_t B1r, uint8_t *ix1, hipStream_t s);
 // segment starts of bucket b: soff[b * (grid + 2) + w], w < grid the regions, w = grid the 16-byte list
 // (wl16n null: empty), [grid + 1] the bucket's total, also in nb[b]

@@ -1089,6 +1089,7 @@ void job_begin(mrg_ctx *c, int app, uint32_t R, uint32_t flags) {
 // and scatter passes over the map's records (wide_aggregate) disappear; L2 reads the regions.
 struct WideMapPlan {
     bool on = false, forced = false, w12 = false;
+    bool repeats = false;     // a cold context's sample found repeats: the bucket path is the likely one
     uint64_t n16 = 0, S = 0;  // sampled keys of 13..16 bytes, samples
     uint32_t B1 = 0, B1r = 0;
     uint64_t *spl1 = nullptr;
@@ -1115,6 +1116,22 @@ WideMapPlan wide_map_plan(mrg_ctx *c, const uint64_t *d_doc_off, uint32_t nd, ui
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     const uint32_t S = (uint32_t)std::min<uint64_t>(64ull * B1, 1u << 20);
+    if (!P.forced && !c->wide_hint) {  // no hint (a cold context): the one-launch test on 8192 samples first
+        const uint32_t S0 = std::min<uint32_t>(S, 8192);
+        SortRec *s0 = pget<SortRec>(p, S0);
+        unsigned long long *d0 = pget<unsigned long long>(p, 2);
+        mrg_wide_launch_sample_text(c->d_in, d_doc_off, nd, total, S0, R, s0, s);
+        mrg_wide_launch_sample_uniq(s0, S0, d0, s);
+        unsigned long long *h0 = &c->h_cnt[CNT_N];  // pinned scratch
+        HIPCHK(hipMemcpyAsync(h0, d0, 16, hipMemcpyDeviceToHost, s));
+        sync(c);
+        const unsigned long long rep = h0[0];
+        p.put(s0); p.put(d0);
+        if (rep * 16 >= S0) {  // repeats: the LDS combine pays
+            P.repeats = true;
+            return P;
+        }
+    }
     SortRec *sa = pget<SortRec>(p, S), *sb = pget<SortRec>(p, S);
     void *stmp = p.get(mrg_sort_tmp_bytes(S));
     unsigned long long *dups = pget<unsigned long long>(p, 2);
@@ -1357,12 +1374,14 @@ void job_map(mrg_ctx *c) {
 
     if (!c->map_grid) c->map_grid = mrg_map_max_grid(c->app, c->lds_cap, c->device);
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->map_grid, n_chunks));
+    bool cold_repeats = false;  // a cold context whose sample found repeats: queue the aggregation too
     {  // near-unique input: the wide map (every key straight to its L1 bucket)
         WideMapPlan wp = wide_map_plan(c, d_doc_off, nd, total, grid);
         if (wp.on) {
             job_map_wide(c, wp, d_doc_off, d_cb, d_ids, nd, n_chunks, total, grid, ids);
             return;
         }
+        cold_repeats = wp.repeats;
     }
     const uint32_t cap = (uint32_t)mrg_map_cap(c->app, c->lds_cap);
     const bool idx = is_idx(c);
@@ -1488,12 +1507,16 @@ void job_map(mrg_ctx *c) {
         // when the map reruns, goes wide or the 32-bit-count guess was wrong
         // (MRG_WIDE=1 forces the wide path, so nothing is queued; MRG_WIDE=0 and MRG_TEST_AGG_NSUB still
         // queue it: their tests run through this path)
-        if (launches == 1 && !idx && c->spec_agg && !M.prof && !wide_forced() && !getenv("MRG_NO_SPEC_AGG") &&
-            grid <= 2048) {
+        // (r06: also on a cold context's first job when its sample found repeats; the 32-bit-count guess
+        // is then "fewer than 2^32 tokens" -- true unless the input holds billions of one-letter words --
+        // and bucket_aggregate checks it like every guess: a wrong one only drops the queued launch)
+        if (launches == 1 && !idx && (c->spec_agg || cold_repeats) && !M.prof && !wide_forced() &&
+            !getenv("MRG_NO_SPEC_AGG") && grid <= 2048) {
             ev_rec(c, 2);
             uint32_t nsub = c->agg_nsub;
             if (const uint64_t t = env_u64("MRG_TEST_AGG_NSUB", 0)) nsub = (uint32_t)t;
-            spec = agg_launch(c, A, (uint32_t)grid, cap, agg_ocap(c), nsub, lslots, c->spec_c32 && grid <= 512, false);
+            const bool c32 = c->spec_agg ? c->spec_c32 : true;
+            spec = agg_launch(c, A, (uint32_t)grid, cap, agg_ocap(c), nsub, lslots, c32 && grid <= 512, false);
         }
         // overflow-list fill into pinned scratch, then the counters: one host wait for both
         uint32_t *onext = (uint32_t *)&c->h_cnt[CNT_N + 8];
@@ -3005,7 +3028,7 @@ void run_job(const char *const *files, size_t n_files, uint32_t R, int app, cons
     g_run.ms_open = ms_since(t0);
     // ---- map phase: GPU g reads and maps files m with m % G == g (coordinator.rs:137-176)
     const int readers = (int)std::max<uint64_t>(1, env_u64("MRG_READ_THREADS", std::max(1, std::min(16, 32 / G))));
-    std::vector<double> t_read(G, 0.0), t_alloc(G, 0.0);
+    std::vector<double> t_read(G, 0.0), t_alloc(G, 0.0), t_mapk(G, 0.0), t_aggk(G, 0.0);
     t0 = Clock::now();
     run_ranks(rs, false, [&](RankState &r) {
         mrg_ctx *c = r.c;
@@ -3032,14 +3055,19 @@ void run_job(const char *const *files, size_t n_files, uint32_t R, int app, cons
         c->doc_ids = ids;
         double a0 = 0.0, a1 = 0.0;
         c->pool.alloc_stats(nullptr, nullptr, &a0);
+        c->timing = true;  // HIP events around the map and aggregation kernels (mrg_run_stats)
         job_map(c);
         c->pool.alloc_stats(nullptr, nullptr, &a1);
         t_alloc[r.g] = a1 - a0;
+        t_mapk[r.g] = c->st.ms_map;
+        t_aggk[r.g] = c->st.ms_aggregate;
     }, rc, msg);
     raise_first(rc, msg, rs);
     g_run.ms_map = ms_since(t0);
     for (int g = 0; g < G; ++g) {
         g_run.ms_map_alloc = std::max(g_run.ms_map_alloc, t_alloc[g]);
+        g_run.ms_map_kernel = std::max(g_run.ms_map_kernel, t_mapk[g]);
+        g_run.ms_aggregate_kernel = std::max(g_run.ms_aggregate_kernel, t_aggk[g]);
         g_run.ms_read = std::max(g_run.ms_read, t_read[g]);
         g_run.input_bytes += rs[g].in_bytes;
     }

@@ -68,7 +68,7 @@ class RunStats(C.Structure):
     _fields_ = [("ms_total", C.c_double), ("ms_open", C.c_double), ("ms_read", C.c_double), ("ms_map", C.c_double),
                 ("ms_shuffle", C.c_double), ("ms_reduce", C.c_double), ("ms_write", C.c_double),
                 ("input_bytes", C.c_uint64), ("output_bytes", C.c_uint64), ("n_gpus", C.c_int),
-                ("ms_map_alloc", C.c_double)]
+                ("ms_map_alloc", C.c_double), ("ms_map_kernel", C.c_double), ("ms_aggregate_kernel", C.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -84,6 +84,8 @@ pub struct mrg_run_stats {
     pub output_bytes: u64,
     pub n_gpus: c_int,
     pub ms_map_alloc: f64,
+    pub ms_map_kernel: f64,
+    pub ms_aggregate_kernel: f64,
 }
 
 extern "C" {

@@ -140,6 +140,7 @@ def test_cold_context_zipf_takes_bucket_path_vs_oracle(ctx):
     files = _host_files(buf, nf, fb)
     del buf
     assert st["map_kind"] == 0 and st["agg_path"] == 1 and st["map_launches"] == 1, st
+    assert st["spec_agg"] == 1, st   # the aggregation was queued behind the cold job's map and used
     assert n_alloc > 0 and alloc_bytes > 0 and alloc_ms >= 0.0
     exp = O.wc_mt(files, 64, threads=THREADS)
     assert [sha(g) for g in got] == [sha(e) for e in exp]
