@@ -9,10 +9,12 @@ exchange over xGMI (mrg_job_shuffle; torch.distributed only hands out the commun
 Weak scaling: per-GPU work is fixed.  --workload unique: configs[4] (C5), near-unique 12-char keys;
 --workload zipf_u: the C3 text with Gutenberg-like Unicode (the reference corpus's kind of text).
 
-The default N = 1 run adds, beside the C3 line: the end-to-end leg (files on disk -> mrg_run_job), a
+The default N = 1 run adds, beside the C3 line: a `cold` object (the first job on a fresh Context over
+the same resident input -- what mrg_run_job and every one-shot worker call run -- with the pool's device
+allocations reported apart from the kernels), the end-to-end leg (files on disk -> mrg_run_job), a
 zipf_u sub-object (k_map GB/s on Unicode text against the ASCII rate), a c5 sub-object (configs[4] at
-50 x 256 MiB, 3 timed steps), a c2 sub-object (the indexer's latency on the bundled corpus,
-configs[1]) and the CPU baseline; --quick leaves all of them out.
+50 x 256 MiB, 3 timed steps, with its own `cold` object), a c2 sub-object (the indexer's latency on the
+bundled corpus, configs[1]) and the CPU baseline; --quick leaves all of them out.
 
 A step = one whole job over the resident input: map (tokenize + combine) -> aggregate + SipHash
 partition -> [shuffle] -> sort -> format; the output bytes of every mr-{r}.txt are in HBM at the end

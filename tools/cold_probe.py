@@ -18,10 +18,12 @@ torch.cuda.synchronize()
 off = [i * fb for i in range(nf + 1)]
 
 
-def jobs(tag, n):
+def jobs(tag, n, idle=0.0):
     c = M.Context(0)
     c.set_timing(True)
     for j in range(n):
+        if idle:
+            time.sleep(idle)   # the GPU idles (as through mrg_run_job's file read)
         a0 = c.pool_alloc_stats()
         torch.cuda.synchronize()
         t = time.perf_counter()
@@ -39,8 +41,21 @@ def jobs(tag, n):
     c.close()
 
 
-jobs("A", 3)
-jobs("B", 2)
+if os.environ.get("PROBE_DONLY"):
+    jobs("A", 1)
+else:
+    jobs("A", 3)
+    jobs("B", 2)
+# D: the same bytes copied back in by DMA (as mrg_run_job's read path does) into the same buffer
+host = torch.empty(nf * fb, dtype=torch.uint8, pin_memory=True)
+host.copy_(buf[:nf * fb])
+torch.cuda.synchronize()
+buf[:nf * fb].copy_(host, non_blocking=True)
+torch.cuda.synchronize()
+jobs("D (input just DMA-written)", 3)
+jobs("E (no rewrite, 0.3 s idle before each job)", 3, idle=0.3)
+if os.environ.get("PROBE_DONLY"):
+    sys.exit(0)
 os.environ["MRG_WIDE_MAP"] = "0"      # no cold-context sample
 jobs("C (no sample)", 2)
 del os.environ["MRG_WIDE_MAP"]
