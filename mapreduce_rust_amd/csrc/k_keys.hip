@@ -144,6 +144,10 @@ __device__ __forceinline__ bool ba_add(BaKey *key, CT *cnt, unsigned int *doc, u
     return ba_add_from<IDX, C32>(key, cnt, doc, a, b, d, c, h, key[ba_slot<IDX, C32>(h)]);
 }
 
+#ifndef MRG_AGG_XCD
+#define MRG_AGG_XCD 1
+#endif
+static_assert(MRG_NBUCKET % 8 == 0, "buckets spread over the 8 XCDs");
 template <bool IDX, bool C32>
 __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
     constexpr uint32_t BA_CAP = ba_cap<IDX, C32>();
@@ -163,7 +167,17 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
     }
     // workgroup (b, j): bucket b, hash sub-range j of A.nsub (a bucket with more distinct keys than one
     // table holds is summed by nsub workgroups, each reading all of its records and keeping its range)
-    const uint32_t b = blockIdx.x % MRG_NBUCKET, jsub = blockIdx.x / MRG_NBUCKET, nsub = A.nsub;
+    // With sub-ranges, the nsub workgroups of a bucket run side by side on ONE XCD (workgroups go to the
+    // XCDs round-robin by blockIdx), so the second and third reads of the bucket's records come from
+    // that XCD's L2 instead of HBM (MRG_AGG_XCD; 0 = bucket-major, the r05 order)
+    const uint32_t nsub = A.nsub;
+#if MRG_AGG_XCD
+    const uint32_t g = blockIdx.x, slot = g / 8u;
+    const uint32_t b = nsub > 1u ? (slot / nsub) * 8u + g % 8u : g % MRG_NBUCKET;
+    const uint32_t jsub = nsub > 1u ? slot % nsub : g / MRG_NBUCKET;
+#else
+    const uint32_t b = blockIdx.x % MRG_NBUCKET, jsub = blockIdx.x / MRG_NBUCKET;
+#endif
     auto mine = [&](uint32_t h) { return nsub <= 1u || (((h & 0xFFu) * nsub) >> 8) == jsub; };
     constexpr uint32_t RW = IDX ? 3u : 2u;
     const uint32_t cap = gk(A.bcap)[b];

@@ -146,6 +146,27 @@ def test_cold_context_zipf_takes_bucket_path_vs_oracle(ctx):
     assert [sha(g) for g in got] == [sha(e) for e in exp]
 
 
+def test_closed_context_blocks_reused_by_the_next(ctx):
+    """The process-wide device cache (mrgpu.cpp DeviceCache): a context closed after a 256 MiB Zipf job
+    leaves its device blocks behind, and the next context's first job over the same input allocates
+    fewer of them (hipMalloc calls counted by mrg_pool_alloc_stats) and writes the same bytes; every
+    job's output against the oracle."""
+    import mapreduce_rust_amd as M
+    import oracle_lib as O
+    nf, fb = 1, 256 * MIB
+    buf = _generate(ctx, "zipf", nf, fb, 0x5EED2026)
+    with M.Context(0) as a:
+        got_a = _run_job(a, buf, nf, fb, 16)
+        na = a.pool_alloc_stats()[0]
+    with M.Context(0) as b:
+        got_b = _run_job(b, buf, nf, fb, 16)
+        nb = b.pool_alloc_stats()[0]
+    files = _host_files(buf, nf, fb)
+    del buf
+    assert na > 0 and nb < na, (na, nb)
+    assert got_a == got_b == O.wc_mt(files, 16, threads=THREADS)
+
+
 @pytest.mark.parametrize("knob", [{}, {"MRG_TEST_WMAP_CAP": 2}, {"MRG_TEST_WMAP_B1R": 1}, {"MRG_TEST_WMAP_B1R": 3},
                                   {"MRG_TEST_WMAP_W12": 0}, {"MRG_TEST_WMAP_W12": 1, "MRG_TEST_WMAP_L16": 1}])
 def test_wide_map_forced_vs_oracle(ctx, corpus, knobs, knob):
