@@ -40,9 +40,10 @@ constexpr uint32_t W_S2 = 8192;       // L2 samples per L1 bucket (sorted in LDS
 #endif
 constexpr uint32_t W_L2D = 8192;          // SEG L2: digits
 constexpr uint32_t W_L2DS = 2048;         // SEG L2: sampled records (the digit bytes' values)
-constexpr uint32_t W_SCS = 7168;          // SEG L2: scatter chunk (the stage's top 16 KiB holds the leaf map)
+constexpr uint32_t W_SCS = 6144;          // SEG L2: scatter chunk (above the stage: the leaf map, the leaves' ends)
 constexpr uint32_t W_L2D_CNT = 32768;     // SEG L2: byte offset of the digit counts in the sample LDS
 constexpr uint32_t W_L2D_MAP = 16u * W_SCS;   // SEG L2: byte offset of the digit -> leaf map
+constexpr uint32_t W_L2D_END = W_L2D_MAP + 2u * W_L2D;   // SEG L2: byte offset of the leaves' region ends (u32)
 constexpr uint32_t W_SC = 8192;       // L2 scatter chunk (staged in the samples' LDS)
 constexpr int W_LWG = 256;            // leaf workgroup (four per CU: while one waits on memory, others work)
 constexpr int W_LNW = W_LWG / 64;
@@ -478,7 +479,9 @@ struct L2Args {
     const uint64_t *spl1;
     uint32_t B1r, target;
     uint32_t *nleaf;         // [B1]
-    uint64_t *leaf_lo;       // [B1 * MAXB2 + 1] first record of each leaf (absolute)
+    uint64_t *leaf_lo;       // [B1 * MAXB2 + 1] first record of each leaf in `out` (absolute)
+    uint64_t *leaf_hi;       // [B1 * MAXB2] one past its last record in `out`
+    uint64_t *leaf_dlo;      // [B1 * MAXB2] its first record in the dense order (bstart-based): output slots
     uint64_t *leaf_lb;       // [B1 * MAXB2][2] lower key bound of each leaf
     uint16_t *sub;           // [n] leaf (inside its L1 bucket) of each record: histogram pass -> scatter
     // segmented input (the wide map's regions): L1 bucket b's records are segments w <= grid at
@@ -489,6 +492,13 @@ struct L2Args {
     const uint32_t *soff;
     uint32_t grid, wcap, w12, wl16cap;
     const uint64_t *wl16;
+    // sparse leaves (SEG only, r06): bucket b's leaves live in out [9 bstart[b] / 4, 9 bstart[b + 1] / 4);
+    // the histogram counts a quarter of each segment, leaf j gets capmul * (its sampled records) +
+    // capadd slots, and a bucket whose leaf overflows is redone with the exact histogram
+    uint32_t sparse, capmul, capadd;
+    uint32_t sample_min;      // buckets of fewer records take the exact histogram at once
+    uint32_t redo;            // the redo launch: only buckets with redo_flags[b] set, exact histogram
+    uint32_t *redo_flags;     // [B1] buckets whose sampled leaves overflowed (zeroed by the host)
 };
 
 // record r of segment w of bucket b (segmented input), as (k0, k1)
@@ -544,7 +554,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     __shared__ uint32_t s_bst[MRG_WIDE_MAXB2];      // scatter: a chunk's leaf starts
     static_assert(W_SC * sizeof(uint64_t) * 2 <= sizeof(s_smp) && W_SC * sizeof(uint16_t) <= sizeof(s_spl),
                   "the scatter's stage fits the sample and splitter arrays");
-    static_assert(16 * W_L2DS <= W_L2D_CNT && W_L2D_CNT + 4 * W_L2D <= W_L2D_MAP && W_L2D_MAP + 2 * W_L2D <= sizeof(s_smp) &&
+    static_assert(16 * W_L2DS <= W_L2D_CNT && W_L2D_CNT + 4 * W_L2D <= W_L2D_MAP && W_L2D_END + 4 * MRG_WIDE_MAXB2 <= sizeof(s_smp) &&
                   W_SCS * sizeof(uint16_t) <= sizeof(s_spl) && W_L2D % W_WG == 0,
                   "SEG L2: samples, digit counts, leaf map and stage fit the sample LDS");
     __shared__ uint32_t s_ws[W_NW];
@@ -553,6 +563,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     __shared__ uint32_t s_dnv[SEG ? 4 : 1];                // SEG: values present at the three digit bytes
     __shared__ uint16_t s_dcode[SEG ? 3 * 256 : 1];        // SEG: the digit bytes' codes (live through the scatter)
     const uint32_t tid = threadIdx.x, b = blockIdx.x;
+    if (SEG && L.redo && L.redo_flags[b] == 0u) return;   // (uniform) only flagged buckets are redone
 #ifdef MRG_WIDE_PROF
     uint64_t l2acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, l2t = clock64();
 #endif
@@ -703,11 +714,6 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         // the sample is dead now: its LDS holds the splitter index
         LeafIndex::build(s_spl, B2 - 1u, reinterpret_cast<uint16_t *>(s_smp), tid, W_WG);
     }
-    for (uint32_t j = tid; j < MRG_WIDE_MAXB2; j += W_WG) {
-        s_cnt[j] = 0;
-        s_cur[j] = 0;
-    }
-    lds_barrier();
     const LeafIndex si{s_spl, reinterpret_cast<const uint16_t *>(s_smp), B2 - 1u,
                        (!SEG && B2 > 1) ? LeafIndex::prefix_bits(s_spl, B2 - 1u) : 0u};
     auto sub_of = [&](uint64_t k0, uint64_t k1) -> uint32_t {
@@ -722,6 +728,23 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         return B2 > 1 ? si.upper(k0, k1) : 0u;
     };
     L2P(3);
+    // sparse leaves (SEG, large buckets): the histogram counts a quarter of every segment and each leaf
+    // gets a region of capmul x its sampled records + capadd; a bucket whose leaf overflows its region
+    // (or whose capacities pass the bucket's budget) is flagged and redone with the exact histogram by
+    // a second launch (L.redo: the other buckets' workgroups return at once)
+    uint32_t *s_end = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(s_smp) + W_L2D_END);
+    __shared__ uint32_t s_ovf;
+    const bool sparse = SEG && L.sparse != 0u;
+    const uint64_t obase = sparse ? 9u * base / 4u : base;
+    const uint64_t obud = sparse ? 9u * (base + nb) / 4u - obase : nb;   // slots of this bucket in `out`
+    const bool samp = sparse && !L.redo && B2 > 1 && nb >= L.sample_min;
+    const uint64_t dtg = samp ? max<uint64_t>(1u, dtgt / 4u) : dtgt;
+    for (uint32_t j = tid; j < MRG_WIDE_MAXB2; j += W_WG) {
+        s_cnt[j] = 0;
+        s_cur[j] = 0;
+    }
+    if (tid == 0) s_ovf = 0u;
+    lds_barrier();
     // ---- histogram (U records per thread in flight)
     constexpr int U = MRG_WIDE_L2U;
     typedef uint64_t v2 __attribute__((ext_vector_type(2)));
@@ -730,7 +753,8 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         const uint32_t *so = s_cseg;
         const uint32_t lane = tid & 63u;
         for (uint32_t w = tid >> 6; w <= L.grid; w += W_NW) {
-            const uint32_t o = so[w], nw = so[w + 1] - o;
+            const uint32_t o = so[w], nwa = so[w + 1] - o;
+            const uint32_t nw = samp ? (nwa + 3u) / 4u : nwa;   // sampled: the segment's first quarter
             for (uint32_t j0 = lane; j0 < nw; j0 += (uint32_t)U * 64u) {
                 v2 x[U];
 #pragma unroll
@@ -775,7 +799,7 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         uint32_t run = block_scan_excl(sum, s_ws, &tot);
 #pragma unroll
         for (uint32_t x = 0; x < PT; ++x) {
-            const uint32_t leaf = min((uint32_t)(run / dtgt), B2 - 1u);
+            const uint32_t leaf = min((uint32_t)(run / dtg), B2 - 1u);
             lmap[tid * PT + x] = (uint16_t)leaf;
             if (v[x]) atomicAdd(&s_cnt[leaf], v[x]);
             run += v[x];
@@ -783,14 +807,18 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
         lds_barrier();
     }
     L2P(4);
-    {  // exclusive scan of the B2 <= 1024 counts, one per thread
-        const uint32_t v = tid < B2 ? s_cnt[tid] : 0u;
+    {  // exclusive scan of the B2 <= 1024 counts (sampled: region capacities), one per thread
+        const uint32_t v = tid < B2 ? (samp ? L.capmul * s_cnt[tid] + L.capadd : s_cnt[tid]) : 0u;
         uint32_t tot;
         const uint32_t ex = block_scan_excl(v, s_ws, &tot);
-        if (tid < B2) s_cur[tid] = ex;
+        if (tid < B2) {
+            s_cur[tid] = ex;
+            if (SEG) s_end[tid] = ex + v;
+        }
+        if (tid == 0) s_ovf = samp && (uint64_t)tot > obud ? 1u : 0u;   // capacities past the budget: exact
         const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + tid;
         if (tid < B2) {
-            L.leaf_lo[lid] = base + ex;
+            L.leaf_lo[lid] = obase + ex;
             uint64_t a, c;
             if (SEG) {   // digit leaves have no key bound (the wide map's job has no weighted keys)
                 a = 0;
@@ -819,9 +847,14 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
     // unstaged scatter wrote 2x its bytes to HBM and ran at a fifth of the read passes' rate)
     constexpr uint32_t WSC = SEG ? W_SCS : W_SC;   // SEG: the top of the stage holds the digit -> leaf map
     constexpr uint32_t SU = WSC / W_WG;
+    static_assert(WSC % W_WG == 0, "a chunk is whole records per thread");
     v2 *stg = reinterpret_cast<v2 *>(s_smp);              // the chunk in leaf order (the sample's LDS)
     uint16_t *stl = reinterpret_cast<uint16_t *>(s_spl);  // its leaves (the splitters' LDS)
-    GASW v2 *outv = reinterpret_cast<GASW v2 *>(gw(L.out) + 2 * base);
+    GASW v2 *outv = reinterpret_cast<GASW v2 *>(gw(L.out) + 2 * obase);
+    if (samp && s_ovf) {   // (uniform: read after the barrier above) capacities past the budget
+        if (tid == 0) L.redo_flags[b] = 1u;
+        return;
+    }
     for (uint64_t c0 = 0; c0 < nb; c0 += WSC) {
         const uint32_t nc = (uint32_t)min<uint64_t>(WSC, nb - c0);
         v2 x[SU];
@@ -881,11 +914,28 @@ __global__ __launch_bounds__(W_WG, 1) void k_wl2(L2Args L) {
             const uint32_t p = tid + u * W_WG;
             if (p < nc) {
                 const uint32_t q = stl[p];
-                outv[s_cur[q] + (p - s_bst[q])] = stg[p];
+                const uint32_t d = s_cur[q] + (p - s_bst[q]);
+                if (!SEG || d < s_end[q]) outv[d] = stg[p];
+                else s_ovf = 1u;   // a sampled leaf past its region: the bucket is redone exactly
             }
         }
         lds_barrier();
         if (tid < B2) s_cur[tid] += s_cnt[tid];   // the thread that zeroes s_cnt[tid] next chunk
+    }
+    lds_barrier();
+    if (samp && s_ovf) {   // a leaf overflowed its region: the bucket is redone exactly
+        if (tid == 0) L.redo_flags[b] = 1u;
+        return;
+    }
+    {   // where each leaf ends in `out`, and its first slot in the dense order (exact counts, scanned)
+        const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + tid;
+        const uint32_t cnt = tid < B2 ? s_cur[tid] - (uint32_t)(L.leaf_lo[lid] - obase) : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_scan_excl(cnt, s_ws, &tot);
+        if (tid < B2) {
+            L.leaf_hi[lid] = obase + s_cur[tid];
+            L.leaf_dlo[lid] = base + ex;
+        }
     }
     L2P(6);
 #ifdef MRG_WIDE_PROF
@@ -923,6 +973,8 @@ struct LeafArgs {
     unsigned long long *big_n;
     uint32_t *leaf_pk;       // 1: the leaf's counts sit in the low word of its key slots (no ocnt entry)
     uint32_t pack;           // packing allowed (every count fits 32 bits)
+    const uint64_t *leaf_hi;   // one past each leaf's last record in kin (L2 may leave gaps between leaves)
+    const uint64_t *leaf_dlo;  // each leaf's first record in the dense order: its output slots start there
 };
 
 // first weighted key >= (p, a, b)
@@ -1016,8 +1068,9 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
     auto leaf_at = [&](uint32_t i, uint64_t &lid, uint64_t &lo, uint64_t &hi) {
         lid = L.big_list[i];
         const uint32_t b = (uint32_t)(lid / MRG_WIDE_MAXB2), j = (uint32_t)(lid % MRG_WIDE_MAXB2);
+        (void)b; (void)j;
         lo = L.leaf_lo[lid];
-        hi = j + 1 < L.nleaf[b] ? L.leaf_lo[lid + 1] : L.bstart[b + 1];
+        hi = L.leaf_hi[lid];
     };
     // first W_PF * W_LWG records of leaf j into registers (a record past the leaf: a repeat, unused)
     v2 pf[W_PF], pff = v2{0, 0};   // pff: the leaf's first record (the same in every thread)
@@ -1046,7 +1099,7 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
         leaf_at(i, lid, mlo, mhi);
         const uint64_t wlo = L.wr[2 * lid], whi = L.wr[2 * lid + 1];
         const uint64_t nm = mhi - mlo, nwk = whi - wlo;
-        const uint64_t out0 = mlo + wlo;
+        const uint64_t out0 = L.leaf_dlo[lid] + wlo;
         v2 cur[W_PF];
 #pragma unroll
         for (int u = 0; u < W_PF; ++u) cur[u] = pf[u];
@@ -1516,7 +1569,11 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
 #endif
 constexpr uint32_t W_VC = MRG_WIDE_VC;
 constexpr uint32_t W_VIPL = W_VC / 64;
-constexpr uint32_t W_VND = 512;         // digits
+#ifndef MRG_WIDE_VND
+#define MRG_WIDE_VND 512
+#endif
+constexpr uint32_t W_VND = MRG_WIDE_VND;   // digits
+static_assert(W_VND % 64 == 0 && W_VND <= 0x10000u, "digit counts: whole wave rows; starts fit the LDS words");
 #ifndef MRG_WIDE_L2U
 #define MRG_WIDE_L2U 4
 #endif
@@ -1553,26 +1610,31 @@ __device__ __forceinline__ uint64_t wave_or(uint64_t v) {
     return v;
 }
 
-__global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
+#ifndef MRG_WIDE_VWPE
+#define MRG_WIDE_VWPE 1
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MRG_WIDE_VWPE))) void k_wleafw(LeafArgs L) {
     typedef uint64_t v2 __attribute__((ext_vector_type(2)));
     __shared__ v2 s_kb[W_VC];            // items in digit-bucket order
     __shared__ uint32_t s_cb[W_VC];      // their counts (a leaf with a larger weighted count is passed on)
     __shared__ __attribute__((aligned(16))) uint16_t s_ix[W_VC];   // sorted position -> bucket slot (and the digit code tables)
     static_assert(sizeof(s_ix) >= 3 * 256, "the leaf digit's three 256-byte code tables live in s_ix");
-    __shared__ uint32_t s_dc[W_VND];     // digit counts
-    __shared__ uint16_t s_ds[W_VND];     // digit starts
-    __shared__ uint32_t s_pass[W_VPASS]; // leaves passed on to k_wleaf
+    __shared__ uint32_t s_dc[W_VND + 1]; // digit counts, then (the scan, in place) digit starts + the end
+    uint32_t *const s_ds = s_dc;
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x / W_VQ, q0 = blockIdx.x % W_VQ;
     const uint32_t nl = L.nleaf[b];
-    const uint64_t bend = L.bstart[b + 1];
     const uint32_t cap = min(L.maxd, W_VC);
     const uint64_t lt = mrg_lanemask_lt();
     const GASW v2 *kin = reinterpret_cast<const GASW v2 *>(gw(L.kin));
     GASW v2 *kout = reinterpret_cast<GASW v2 *>(gw(L.kout));
     GASW uint64_t *cout = gw(L.ocnt);
     unsigned long long keys = 0;
-    uint32_t npass = 0;
+    // a leaf for the workgroup kernel (rare: one device atomic each; an LDS list of them cost the
+    // LDS that a fourth wave per SIMD needs)
+    auto pass_on = [&](uint64_t lid) {
+        if (lane == 0) L.big_list[atomicAdd(L.big_n, 1ull)] = (uint32_t)lid;
+    };
 #ifdef MRG_WIDE_PROF  // diagnostic build: phase clocks of every wave, summed into L.prof[8..13]
     uint64_t vacc[6] = {0, 0, 0, 0, 0, 0}, vtl = clock64();
 #define VP(i) { const uint64_t t_ = clock64(); vacc[i] += t_ - vtl; vtl = t_; }
@@ -1582,18 +1644,17 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
     for (uint32_t j = q0; j < nl; j += W_VQ) {
         VP(5);
         const uint64_t lid = (uint64_t)b * MRG_WIDE_MAXB2 + j;
-        const uint64_t mlo = L.leaf_lo[lid], mhi = j + 1 < nl ? L.leaf_lo[lid + 1] : bend;
+        const uint64_t mlo = L.leaf_lo[lid], mhi = L.leaf_hi[lid];
         const uint64_t wlo = L.wr[2 * lid], whi = L.wr[2 * lid + 1];
         const uint64_t nm = mhi - mlo, NT = nm + (whi - wlo);
         if (NT > cap) {
-            if (lane == 0) s_pass[npass] = (uint32_t)lid;
-            ++npass;
+            pass_on(lid);
 #ifdef MRG_WIDE_PROF
             if (lane == 0) atomicAdd(&L.prof[6], 1ull);
 #endif
             continue;
         }
-        const uint64_t out0 = mlo + wlo;
+        const uint64_t out0 = L.leaf_dlo[lid] + wlo;
         GASW v2 *ko = kout + out0;
         GASW uint64_t *co = cout + out0;
         v2 key[W_VIPL];
@@ -1620,8 +1681,7 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
         bool big = csum > 0xFFFFFFFFull;
         VP(0);
         if (__any(big)) {   // a count beyond the LDS count width: the workgroup kernel
-            if (lane == 0) s_pass[npass] = (uint32_t)lid;
-            ++npass;
+            pass_on(lid);
             continue;
         }
         // Packed leaf: when every key of the leaf is at most 12 bytes (the low word of k1 is zero
@@ -1744,9 +1804,10 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
                 uint32_t run = wave_scan_incl(sum) - sum;
 #pragma unroll
                 for (uint32_t x = 0; x < PT; ++x) {
-                    s_ds[lane * PT + x] = (uint16_t)run;
+                    s_ds[lane * PT + x] = run;   // (in place: this lane read its counts above)
                     run += v[x];
                 }
+                if (lane == 63) s_ds[W_VND] = run;
                 for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
 #ifdef MRG_WIDE_PROF
                 uint32_t nz = 0;
@@ -1760,8 +1821,7 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
 #endif
             }
             if (mx > W_VMAXB) {   // many equal (or near-equal) keys: the workgroup kernel
-                if (lane == 0) s_pass[npass] = (uint32_t)lid;
-                ++npass;
+                pass_on(lid);
 #ifdef MRG_WIDE_PROF
                 if (lane == 0) atomicAdd(&L.prof[7], 1ull);
 #endif
@@ -1796,7 +1856,7 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
             for (uint32_t k = 0; k < W_VIPL; ++k) {
                 const bool v = dg[k] != 0xFFFFFFFFu;
                 bs[k] = v ? s_ds[dg[k]] : 0u;
-                bn[k] = v ? s_dc[dg[k]] : 0u;
+                bn[k] = v ? s_ds[dg[k] + 1u] - bs[k] : 0u;
                 rank[k] = 0;
                 fq[k] = wi[k];
             }
@@ -1883,14 +1943,6 @@ __global__ __launch_bounds__(64) void k_wleafw(LeafArgs L) {
         for (int i = 0; i < 6; ++i) atomicAdd(&L.prof[8 + i], (unsigned long long)vacc[i]);
 #endif
 #undef VP
-    // the passed-on leaves, with one device atomic per wave
-    if (npass) {
-        wave_lds_sync();
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(L.big_n, (unsigned long long)npass);
-        base = __shfl(base, 0);
-        for (uint32_t i = lane; i < npass; i += 64) L.big_list[base + i] = s_pass[i];
-    }
     if (lane == 0 && keys) atomicAdd(L.nkeys, keys);
 }
 
@@ -2218,22 +2270,20 @@ __global__ __launch_bounds__(256) void k_wdense(const uint64_t *keys, const uint
 
 // ---------------------------------------------------------------- overflowed leaves: global sort
 // records of the listed leaves -> SortRec{key, part = list position, idx = count slot}, counts apart
-__global__ void k_wfb_count(const uint32_t *list, uint32_t nlist, const uint64_t *leaf_lo, const uint32_t *nleaf,
-                            const uint64_t *bstart, const uint64_t *wrange, uint64_t *cnt) {
+__global__ void k_wfb_count(const uint32_t *list, uint32_t nlist, const uint64_t *leaf_lo, const uint64_t *leaf_hi,
+                            const uint64_t *wrange, uint64_t *cnt) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nlist) return;
     const uint64_t lid = list[k];
-    const uint32_t b = (uint32_t)(lid / MRG_WIDE_MAXB2), j = (uint32_t)(lid % MRG_WIDE_MAXB2);
-    const uint64_t mlo = leaf_lo[lid], mhi = j + 1 < nleaf[b] ? leaf_lo[lid + 1] : bstart[b + 1];
+    const uint64_t mlo = leaf_lo[lid], mhi = leaf_hi[lid];
     cnt[k] = (mhi - mlo) + (wrange[2 * k + 1] - wrange[2 * k]);
 }
-__global__ void k_wfb_gather(const uint32_t *list, const uint64_t *off, const uint64_t *leaf_lo, const uint32_t *nleaf,
-                             const uint64_t *bstart, const uint64_t *wrange, const uint64_t *kin, const uint64_t *wk0,
+__global__ void k_wfb_gather(const uint32_t *list, const uint64_t *off, const uint64_t *leaf_lo, const uint64_t *leaf_hi,
+                             const uint64_t *wrange, const uint64_t *kin, const uint64_t *wk0,
                              const uint64_t *wk1, const uint64_t *wcnt, SortRec *recs, uint64_t *rcnt) {
     const uint32_t k = blockIdx.x;
     const uint64_t lid = list[k];
-    const uint32_t b = (uint32_t)(lid / MRG_WIDE_MAXB2), j = (uint32_t)(lid % MRG_WIDE_MAXB2);
-    const uint64_t mlo = leaf_lo[lid], mhi = j + 1 < nleaf[b] ? leaf_lo[lid + 1] : bstart[b + 1];
+    const uint64_t mlo = leaf_lo[lid], mhi = leaf_hi[lid];
     const uint64_t wlo = wrange[2 * k], whi = wrange[2 * k + 1];
     const uint64_t nm = mhi - mlo, n = nm + (whi - wlo), o = off[k];
     for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
@@ -2373,12 +2423,21 @@ void mrg_wide_launch_bstart(const uint32_t *cnt, uint32_t B1, uint32_t ntiles, u
     hipLaunchKernelGGL(k_wbstart, gridw(B1 + 1), dim3(256), 0, s, cnt, B1, ntiles, n, bstart);
 }
 void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstart, const uint64_t *spl1, uint32_t B1,
-                        uint32_t B1r, uint32_t target, uint32_t *nleaf, uint64_t *leaf_lo, uint64_t *leaf_lb,
-                        uint16_t *sub, hipStream_t s, const WmapIn &wm) {
-    L2Args L{in, out, bstart, spl1, B1r, target, nleaf, leaf_lo, leaf_lb, sub,
-             wm.rin, wm.soff, wm.grid, wm.wcap, wm.w12, wm.wl16cap, wm.wl16};
-    if (wm.rin) hipLaunchKernelGGL(k_wl2<true>, dim3(B1), dim3(W_WG), 0, s, L);
-    else hipLaunchKernelGGL(k_wl2<false>, dim3(B1), dim3(W_WG), 0, s, L);
+                        uint32_t B1r, uint32_t target, uint32_t *nleaf, uint64_t *leaf_lo, uint64_t *leaf_hi,
+                        uint64_t *leaf_dlo, uint64_t *leaf_lb, uint16_t *sub, hipStream_t s, const WmapIn &wm,
+                        const L2Sparse &sp) {
+    L2Args L{in, out, bstart, spl1, B1r, target, nleaf, leaf_lo, leaf_hi, leaf_dlo, leaf_lb, sub,
+             wm.rin, wm.soff, wm.grid, wm.wcap, wm.w12, wm.wl16cap, wm.wl16,
+             wm.rin && sp.on ? 1u : 0u, sp.capmul, sp.capadd, sp.sample_min, 0u, sp.redo_flags};
+    if (wm.rin) {
+        hipLaunchKernelGGL(k_wl2<true>, dim3(B1), dim3(W_WG), 0, s, L);
+        if (L.sparse) {  // the buckets whose sampled leaves overflowed, with the exact histogram
+            L.redo = 1u;
+            hipLaunchKernelGGL(k_wl2<true>, dim3(B1), dim3(W_WG), 0, s, L);
+        }
+    } else {
+        hipLaunchKernelGGL(k_wl2<false>, dim3(B1), dim3(W_WG), 0, s, L);
+    }
 }
 // diagnostic builds (-DMRG_WIDE_PROF): the L2 phase clocks summed so far (else zeros)
 void mrg_wide_l2_prof(unsigned long long out[8]) {
@@ -2395,7 +2454,7 @@ void mrg_wide_launch_weights(const SortRec *r, uint64_t n, KeySet ks, uint64_t *
 void mrg_wide_launch_leaf(const WideLeafArgs &w, uint32_t B1, hipStream_t s) {
     LeafArgs L{w.kin, w.kout, w.bstart, w.nleaf, w.leaf_lo, w.leaf_lb, w.B1r, w.R, w.wk0, w.wk1, w.wcnt, w.wpart, w.nw,
                w.maxd ? min(w.maxd, W_MAXD) : W_MAXD, w.ocnt, w.leaf_out, w.leaf_nd, w.leaf_bytes, w.leaf_last, w.ovf_list,
-               w.ovf_n, w.nkeys, w.wr, w.prof, w.big_list, w.big_n, w.leaf_pk, w.pack};
+               w.ovf_n, w.nkeys, w.wr, w.prof, w.big_list, w.big_n, w.leaf_pk, w.pack, w.leaf_hi, w.leaf_dlo};
     hipLaunchKernelGGL(k_wranges, gridw((uint64_t)B1 * MRG_WIDE_MAXB2), dim3(256), 0, s, L, B1);
     hipLaunchKernelGGL(k_wleafw, dim3(B1 * W_VQ), dim3(64), 0, s, L);
     // the passed-on leaves: a fixed grid loops over the list (its length is read on the device)
@@ -2405,21 +2464,20 @@ void mrg_wide_launch_fallback(const WideLeafArgs &w, const uint32_t *list, uint3
                               hipStream_t s) {
     LeafArgs L{w.kin, w.kout, w.bstart, w.nleaf, w.leaf_lo, w.leaf_lb, w.B1r, w.R, w.wk0, w.wk1, w.wcnt, w.wpart, w.nw,
                w.maxd ? min(w.maxd, W_MAXD) : W_MAXD, w.ocnt, w.leaf_out, w.leaf_nd, w.leaf_bytes, w.leaf_last, w.ovf_list,
-               w.ovf_n, w.nkeys, w.wr, w.prof, w.big_list, w.big_n, w.leaf_pk, w.pack};
+               w.ovf_n, w.nkeys, w.wr, w.prof, w.big_list, w.big_n, w.leaf_pk, w.pack, w.leaf_hi, w.leaf_dlo};
     uint64_t *wrange = (uint64_t *)pool.get(16ull * nlist);
     uint64_t *cnt = (uint64_t *)pool.get(8ull * (nlist + 1)), *off = (uint64_t *)pool.get(8ull * (nlist + 1));
     uint64_t *scantmp = (uint64_t *)pool.get(8ull * mrg_scan_tmp_elems(nlist + 1));
     hipLaunchKernelGGL(k_wfb_wrange, gridw(nlist), dim3(256), 0, s, L, list, nlist, wrange);
     hipMemsetAsync(cnt + nlist, 0, 8, s);
-    hipLaunchKernelGGL(k_wfb_count, gridw(nlist), dim3(256), 0, s, list, nlist, w.leaf_lo, w.nleaf, w.bstart, wrange,
-                       cnt);
+    hipLaunchKernelGGL(k_wfb_count, gridw(nlist), dim3(256), 0, s, list, nlist, w.leaf_lo, w.leaf_hi, wrange, cnt);
     mrg_scan_u64(cnt, off, nlist + 1, scantmp, s);
     uint64_t n = 0;
     hipMemcpyAsync(&n, off + nlist, 8, hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
     SortRec *a = (SortRec *)pool.get(sizeof(SortRec) * (n + 1)), *b = (SortRec *)pool.get(sizeof(SortRec) * (n + 1));
     uint64_t *rcnt = (uint64_t *)pool.get(8ull * (n + 1));
-    hipLaunchKernelGGL(k_wfb_gather, dim3(nlist), dim3(256), 0, s, list, off, w.leaf_lo, w.nleaf, w.bstart, wrange,
+    hipLaunchKernelGGL(k_wfb_gather, dim3(nlist), dim3(256), 0, s, list, off, w.leaf_lo, w.leaf_hi, wrange,
                        w.kin, w.wk0, w.wk1, w.wcnt, a, rcnt);
     SortPlan plan{};
     plan.use_part = nlist > 1;

@@ -374,6 +374,8 @@ struct WideLeafArgs {
     unsigned long long *big_n;   // their count (zeroed by the caller)
     uint32_t *leaf_pk;           // [B1 * MRG_WIDE_MAXB2] 1: the leaf's counts are packed into its key slots (zeroed by the caller)
     uint32_t pack;               // packing allowed: every count fits 32 bits (fewer than 2^32 tokens)
+    const uint64_t *leaf_hi;     // [B1 * MAXB2] one past each leaf's last record in kin (L2 may leave gaps)
+    const uint64_t *leaf_dlo;    // [B1 * MAXB2] each leaf's first record in the dense order (its output slots)
 };
 void mrg_wide_launch_counts(const BucketArgs &a, uint64_t *cnt_main, uint64_t *segptr, uint64_t *cnt_flush,
                             hipStream_t s);
@@ -396,9 +398,18 @@ struct WmapIn {
     const uint64_t *wl16 = nullptr;
 };
 void mrg_wide_l2_prof(unsigned long long out[8]);
+// sparse L2 leaves (the wide map's buckets only): out must hold 9 n / 4 + 16 records (bucket b's leaves in
+// [9 bstart[b] / 4, 9 bstart[b + 1] / 4)); capacities capmul x sampled records + capadd (test knobs)
+struct L2Sparse {
+    bool on = false;
+    uint32_t capmul = 8, capadd = 64;
+    uint32_t sample_min = 65536;      // records: smaller buckets histogram exactly
+    uint32_t *redo_flags = nullptr;   // [B1], zeroed: buckets the exact second launch redoes
+};
 void mrg_wide_launch_l2(const uint64_t *in, uint64_t *out, const uint64_t *bstart, const uint64_t *spl1, uint32_t B1,
-                        uint32_t B1r, uint32_t target, uint32_t *nleaf, uint64_t *leaf_lo, uint64_t *leaf_lb,
-                        uint16_t *sub, hipStream_t s, const WmapIn &wm = WmapIn{});
+                        uint32_t B1r, uint32_t target, uint32_t *nleaf, uint64_t *leaf_lo, uint64_t *leaf_hi,
+                        uint64_t *leaf_dlo, uint64_t *leaf_lb, uint16_t *sub, hipStream_t s,
+                        const WmapIn &wm = WmapIn{}, const L2Sparse &sp = L2Sparse{});
 // wide map (near-unique input): a sample of the input text's tokens (k_wsample_text), adjacent
 // duplicates of the sorted sample, the L1 splitter index, the regions' per-bucket segment starts
 void mrg_wide_launch_sample_text(const uint8_t *in, const uint64_t *doc_off, uint32_t n_docs, uint64_t total,

@@ -809,13 +809,32 @@ void wide_finish(mrg_ctx *c, LongItems li, uint64_t n, uint64_t nw, uint32_t B1,
     };
     // ---- L2: leaves inside every L1 bucket
     const uint64_t NL = (uint64_t)B1 * MRG_WIDE_MAXB2;
-    uint64_t *K2 = pget<uint64_t>(p, 2 * n + 2);
+    // the wide map's buckets: sparse leaves in K2 from a sampled histogram
+    // unless MRG_WIDE_L2_EXACT=1; MRG_TEST_L2_CAP=<mul>,<add> sets the leaf capacities (small ones force
+    // the exact redo), MRG_TEST_L2_MIN the smallest bucket that samples
+    L2Sparse sp;
+    sp.on = wm.rin != nullptr && !env_u64("MRG_WIDE_L2_EXACT", 0);
+    if (const char *e = getenv("MRG_TEST_L2_CAP")) {
+        unsigned a = 8, d = 64;
+        if (sscanf(e, "%u,%u", &a, &d) >= 1) { sp.capmul = a; sp.capadd = d; }
+    }
+    sp.sample_min = (uint32_t)env_u64("MRG_TEST_L2_MIN", sp.sample_min);  // (tests: sample small buckets)
+    if (sp.on) {
+        sp.redo_flags = pget<uint32_t>(p, B1);
+        HIPCHK(hipMemsetAsync(sp.redo_flags, 0, 4ull * B1, s));
+    }
+    const uint64_t nrec2 = sp.on ? 9 * n / 4 + 16 : n + 1;  // K2 records
+    uint64_t *K2 = pget<uint64_t>(p, 2 * nrec2 + 2);
     uint32_t *nleaf = pget<uint32_t>(p, B1);
     uint64_t *leaf_lo = pget<uint64_t>(p, NL + 1), *leaf_lb = pget<uint64_t>(p, 2 * NL + 2);
-    // records per leaf: the wide map's digit leaves come out near the target (320: r05 v61), the
-    // sampled splitters' leaves vary like 8-sample gaps (256 keeps most under the one-wave capacity)
-    const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", wm.rin ? 320 : 256);
-    mrg_wide_launch_l2(wm.rin ? nullptr : K1, K2, bstart, spl1, B1, B1r, target, nleaf, leaf_lo, leaf_lb, bid, s, wm);
+    uint64_t *leaf_hi = pget<uint64_t>(p, NL + 1), *leaf_dlo = pget<uint64_t>(p, NL + 1);
+    // records per leaf: the wide map's digit leaves come out near the target (320: r05 v61; 288 when cut
+    // from the sampled histogram, whose leaves vary more: r06 v09), the sampled splitters' leaves vary
+    // like 8-sample gaps (256 keeps most under the one-wave capacity)
+    const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", wm.rin ? (sp.on ? 288 : 320) : 256);
+    mrg_wide_launch_l2(wm.rin ? nullptr : K1, K2, bstart, spl1, B1, B1r, target, nleaf, leaf_lo, leaf_hi, leaf_dlo, leaf_lb,
+                       bid, s, wm, sp);
+    p.put(sp.redo_flags);
     p.put(bid);
     mark();  // 4: L2
     // ---- leaves: aggregate + sort + line bytes (K1 becomes the output key array)
@@ -839,6 +858,7 @@ void wide_finish(mrg_ctx *c, LongItems li, uint64_t n, uint64_t nw, uint32_t B1,
     HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_OVF2], 0, 8, s));
     WideLeafArgs L{};
     L.kin = K2; L.kout = K1; L.bstart = bstart; L.nleaf = nleaf; L.leaf_lo = leaf_lo; L.leaf_lb = leaf_lb;
+    L.leaf_hi = leaf_hi; L.leaf_dlo = leaf_dlo;
     L.B1r = B1r; L.R = R; L.wk0 = wk0; L.wk1 = wk1; L.wcnt = wcnt; L.wpart = wpart; L.nw = nw;
     L.maxd = (uint32_t)env_u64("MRG_TEST_LEAF_CAP", 0);
     L.ocnt = w.ocnt; L.leaf_out = w.leaf_out; L.leaf_nd = w.leaf_nd; L.leaf_bytes = w.leaf_bytes;
@@ -879,15 +899,15 @@ void wide_finish(mrg_ctx *c, LongItems li, uint64_t n, uint64_t nw, uint32_t B1,
                 pr[6], pr[7]);
         {  // leaf sizes (records)
             std::vector<uint32_t> hn(B1);
-            std::vector<uint64_t> hlo(NL), hbs(B1 + 1);
+            std::vector<uint64_t> hlo(NL), hhi(NL);
             HIPCHK(hipMemcpy(hn.data(), nleaf, 4ull * B1, hipMemcpyDeviceToHost));
             HIPCHK(hipMemcpy(hlo.data(), leaf_lo, 8ull * NL, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(hbs.data(), bstart, 8ull * (B1 + 1), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hhi.data(), leaf_hi, 8ull * NL, hipMemcpyDeviceToHost));
             std::vector<uint64_t> sz;
             for (uint32_t bb = 0; bb < B1; ++bb)
                 for (uint32_t j = 0; j < hn[bb]; ++j) {
                     const uint64_t lid = (uint64_t)bb * MRG_WIDE_MAXB2 + j;
-                    sz.push_back((j + 1 < hn[bb] ? hlo[lid + 1] : hbs[bb + 1]) - hlo[lid]);
+                    sz.push_back(hhi[lid] - hlo[lid]);
                 }
             std::sort(sz.begin(), sz.end());
             if (!sz.empty())
@@ -920,7 +940,8 @@ void wide_finish(mrg_ctx *c, LongItems li, uint64_t n, uint64_t nw, uint32_t B1,
         fprintf(stderr, "[mrgpu] wide: %llu records, %llu weighted, B1 %u (x%u), %llu distinct, %llu leaves overflowed\n",
                 (unsigned long long)n, (unsigned long long)nw, B1, B1r, (unsigned long long)w.distinct,
                 (unsigned long long)novf);
-    p.put(K2); p.put(leaf_lo); p.put(leaf_lb); p.put(ovf_list); p.put(spl1); p.put(bstart); p.put(L.wr);
+    p.put(K2); p.put(leaf_lo); p.put(leaf_lb); p.put(leaf_hi); p.put(leaf_dlo); p.put(ovf_list); p.put(spl1); p.put(bstart);
+    p.put(L.wr);
     p.put(L.prof); p.put(L.big_list); p.put(L.big_n);
     p.put(wk0); p.put(wk1); p.put(wcnt); p.put(wpart);
     c->st.overflow_keys = novf;

@@ -252,7 +252,8 @@ def knobs():
     keys = ["MRG_TEST_TAIL_CAP", "MRG_TEST_OVF_CAP", "MRG_TEST_AGG_OCAP", "MRG_WIDE", "MRG_TEST_LEAF_CAP",
             "MRG_TEST_LEAF_TARGET", "MRG_TEST_SORT_LCAP", "MRG_TEST_AGG_WIDE_OVF", "MRG_TEST_AGG_NSUB",
             "MRG_TEST_NO_PACK", "MRG_TEST_LONG_PER", "MRG_TEST_LONG_LIST", "MRG_WIDE_MAP", "MRG_TEST_WMAP_CAP",
-            "MRG_TEST_WMAP_B1R", "MRG_TEST_WMAP_W12", "MRG_TEST_WMAP_L16"]
+            "MRG_TEST_WMAP_B1R", "MRG_TEST_WMAP_W12", "MRG_TEST_WMAP_L16", "MRG_TEST_L2_CAP",
+            "MRG_TEST_L2_MIN", "MRG_WIDE_L2_EXACT"]
     saved = {k: os.environ.get(k) for k in keys}
 
     def set_(**kw):
@@ -673,6 +674,34 @@ def test_wide_many_partitions_vs_oracle(ctx, knobs):
     knobs(MRG_WIDE=1)
     for R in (5000, 4096):
         assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST), R
+
+
+def test_wide_l2_sampled_leaves_vs_oracle(ctx, knobs):
+    """The wide map's L2 (k_wide.hip k_wl2): a bucket's digit histogram from a
+    quarter of its records, fixed-capacity leaf regions, and the exact second launch for every bucket
+    whose leaf overflowed.  256 MiB of near-unique keys at R = 16 (every bucket sampled: the size floor
+    lowered to 1024 records), then mixed lengths and repeated keys at R = 7; default capacities, regions
+    of 1 x the sampled count (every bucket overflows: all redone), 3 x (some redone), and the exact
+    histogram -- all byte-identical to the oracle."""
+    import torch
+    import oracle_lib as O
+    from gpu_util import run_wc
+    nf, fb = 1, 256 * MIB
+    buf = _generate(ctx, "unique", nf, fb, 0x15A3)
+    files = _host_files(buf, nf, fb)
+    exp = O.wc_mt(files, 16, threads=THREADS)
+    docs = [_mixed_keys_doc(13, 300_000), b" ".join([b"repeated"] * 40000 + [b"twelvecharsx"] * 30000)]
+    exp2 = O.wc(docs, 7, O.FAST)
+    for knob in ({}, {"MRG_TEST_L2_CAP": "1,0"}, {"MRG_TEST_L2_CAP": "3,0"}, {"MRG_WIDE_L2_EXACT": 1}):
+        knobs(MRG_WIDE_MAP=1, MRG_TEST_L2_MIN=1024, **knob)
+        got = _run_job(ctx, buf, nf, fb, 16)
+        st = ctx.stats()
+        assert st["map_kind"] == 1 and st["agg_path"] == 2, (knob, st)
+        assert [sha(g) for g in got] == [sha(e) for e in exp], knob
+        knobs(MRG_WIDE_MAP=1, MRG_TEST_L2_MIN=64, **knob)
+        assert run_wc(ctx, docs, 7) == exp2, knob
+    knobs()
+    del buf
 
 
 def test_zipf_unicode_256mib_vs_oracle(ctx):
