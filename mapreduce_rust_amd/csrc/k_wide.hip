@@ -1570,7 +1570,7 @@ __global__ __launch_bounds__(W_LWG, 3) void k_wleaf(LeafArgs L) {
 constexpr uint32_t W_VC = MRG_WIDE_VC;
 constexpr uint32_t W_VIPL = W_VC / 64;
 #ifndef MRG_WIDE_VND
-#define MRG_WIDE_VND 512
+#define MRG_WIDE_VND 384   // (r06 v08, v10: 512 -> 384 digits, the leaf kernel at 4 waves per SIMD: C5 aggregation -1.5 %)
 #endif
 constexpr uint32_t W_VND = MRG_WIDE_VND;   // digits
 static_assert(W_VND % 64 == 0 && W_VND <= 0x10000u, "digit counts: whole wave rows; starts fit the LDS words");
@@ -1611,7 +1611,7 @@ __device__ __forceinline__ uint64_t wave_or(uint64_t v) {
 }
 
 #ifndef MRG_WIDE_VWPE
-#define MRG_WIDE_VWPE 1
+#define MRG_WIDE_VWPE 4   // waves per SIMD the register budget is held to (117 VGPRs, no spill)
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MRG_WIDE_VWPE))) void k_wleafw(LeafArgs L) {
     typedef uint64_t v2 __attribute__((ext_vector_type(2)));
@@ -1621,6 +1621,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MRG_WIDE_VWP
     static_assert(sizeof(s_ix) >= 3 * 256, "the leaf digit's three 256-byte code tables live in s_ix");
     __shared__ uint32_t s_dc[W_VND + 1]; // digit counts, then (the scan, in place) digit starts + the end
     uint32_t *const s_ds = s_dc;
+    static_assert(MRG_WIDE_VWPE < 4 || sizeof(s_kb) + sizeof(s_cb) + sizeof(s_ix) + sizeof(s_dc) <= 160u * 1024u / 16u,
+                  "4 one-wave workgroups per SIMD: 16 per CU share its 160 KiB of LDS");
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x / W_VQ, q0 = blockIdx.x % W_VQ;
     const uint32_t nl = L.nleaf[b];
