@@ -402,7 +402,7 @@ void mrg_wide_l2_prof(unsigned long long out[8]);
 // [9 bstart[b] / 4, 9 bstart[b + 1] / 4)); capacities capmul x sampled records + capadd (test knobs)
 struct L2Sparse {
     bool on = false;
-    uint32_t capmul = 8, capadd = 64;
+    uint32_t capmul = 6, capadd = 64;   // (r06 v11: 6 x the sampled records + 64, leaf target 256)
     uint32_t sample_min = 65536;      // records: smaller buckets histogram exactly
     uint32_t *redo_flags = nullptr;   // [B1], zeroed: buckets the exact second launch redoes
 };

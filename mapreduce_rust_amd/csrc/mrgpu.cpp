@@ -828,10 +828,10 @@ void wide_finish(mrg_ctx *c, LongItems li, uint64_t n, uint64_t nw, uint32_t B1,
     uint32_t *nleaf = pget<uint32_t>(p, B1);
     uint64_t *leaf_lo = pget<uint64_t>(p, NL + 1), *leaf_lb = pget<uint64_t>(p, 2 * NL + 2);
     uint64_t *leaf_hi = pget<uint64_t>(p, NL + 1), *leaf_dlo = pget<uint64_t>(p, NL + 1);
-    // records per leaf: the wide map's digit leaves come out near the target (320: r05 v61; 288 when cut
-    // from the sampled histogram, whose leaves vary more: r06 v09), the sampled splitters' leaves vary
-    // like 8-sample gaps (256 keeps most under the one-wave capacity)
-    const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", wm.rin ? (sp.on ? 288 : 320) : 256);
+    // records per leaf: the wide map's digit leaves come out near the target (320: r05 v61; 256 when cut
+    // from the sampled histogram, whose leaves vary more: r06 v09, v11), the sampled splitters' leaves
+    // vary like 8-sample gaps (256 keeps most under the one-wave capacity)
+    const uint32_t target = (uint32_t)env_u64("MRG_TEST_LEAF_TARGET", wm.rin ? (sp.on ? 256 : 320) : 256);
     mrg_wide_launch_l2(wm.rin ? nullptr : K1, K2, bstart, spl1, B1, B1r, target, nleaf, leaf_lo, leaf_hi, leaf_dlo, leaf_lb,
                        bid, s, wm, sp);
     p.put(sp.redo_flags);
