@@ -107,9 +107,9 @@ int guard(F &&f) {
 // Process-wide cache of the device blocks of closed contexts, per device (r06).  A worker process runs
 // one task after another (src/bin/mrworker.rs:43-149); every mrg_run_job opens fresh contexts, and
 // without this each call re-allocated -- and the GPU re-touched -- its multi-GiB workspaces (the first
-// job's map ran 1.2x its steady time).  Capped at MRG_POOL_KEEP_GIB per device (default 64; 0 = off);
-// blocks beyond the cap are freed.  Never destroyed: no hipFree may run after the HIP runtime's own
-// teardown at process exit.
+// job's map ran 1.2x its steady time).  Capped at MRG_POOL_KEEP_GIB per device (default: half the
+// device's memory; 0 = off); blocks beyond the cap are freed.  Never destroyed: no hipFree may run
+// after the HIP runtime's own teardown at process exit.
 class DeviceCache {
    public:
     static DeviceCache &get() {
@@ -132,7 +132,7 @@ class DeviceCache {
     void give(int dev, void *p, size_t c) {
         {
             std::lock_guard<std::mutex> lk(mu_);
-            if (bytes_[dev] + c <= keep_) {
+            if (bytes_[dev] + c <= keep(dev)) {
                 free_[dev].insert({c, p});
                 bytes_[dev] += c;
                 return;
@@ -152,13 +152,28 @@ class DeviceCache {
 
    private:
     DeviceCache() {
-        const char *v = getenv("MRG_POOL_KEEP_GIB");
-        keep_ = (size_t)((v ? atof(v) : 64.0) * (double)((size_t)1 << 30));
+        if (const char *v = getenv("MRG_POOL_KEEP_GIB")) keep_env_ = (long long)(atof(v) * (double)((size_t)1 << 30));
+    }
+    // bytes of `dev` (the current device) kept: MRG_POOL_KEEP_GIB, else half the device's memory.  A
+    // block handed back to the driver is wiped before any allocation can reuse it (a fresh context
+    // after one that freed ~100 GiB waited 4.6 s in hipMalloc: profiles/r06/v13), so one C5-sized
+    // job's blocks (67-83 GiB at 13.4 GB of input) are worth keeping
+    size_t keep(int dev) {
+        if (keep_env_ >= 0) return (size_t)keep_env_;
+        auto it = keep_dev_.find(dev);
+        if (it != keep_dev_.end()) return it->second;
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+            (void)hipGetLastError();
+            tot = (size_t)128 << 30;
+        }
+        return keep_dev_[dev] = tot / 2;
     }
     std::mutex mu_;
     std::map<int, std::multimap<size_t, void *>> free_;
     std::map<int, size_t> bytes_;
-    size_t keep_ = 0;
+    std::map<int, size_t> keep_dev_;
+    long long keep_env_ = -1;
 };
 
 class Pool : public DevPool {
@@ -809,11 +824,12 @@ void wide_finish(mrg_ctx *c, LongItems li, uint64_t n, uint64_t nw, uint32_t B1,
     };
     // ---- L2: leaves inside every L1 bucket
     const uint64_t NL = (uint64_t)B1 * MRG_WIDE_MAXB2;
-    // the wide map's buckets: sparse leaves in K2 from a sampled histogram
-    // unless MRG_WIDE_L2_EXACT=1; MRG_TEST_L2_CAP=<mul>,<add> sets the leaf capacities (small ones force
-    // the exact redo), MRG_TEST_L2_MIN the smallest bucket that samples
+    // the wide map's buckets: with MRG_WIDE_L2_SAMPLED=1, sparse leaves in K2 from a sampled histogram
+    // (-1 % of C5's step for 1.6x its device memory, so not the default);
+    // MRG_TEST_L2_CAP=<mul>,<add> sets the leaf capacities (small ones force the exact redo),
+    // MRG_TEST_L2_MIN the smallest bucket that samples
     L2Sparse sp;
-    sp.on = wm.rin != nullptr && !env_u64("MRG_WIDE_L2_EXACT", 0);
+    sp.on = wm.rin != nullptr && env_u64("MRG_WIDE_L2_SAMPLED", 0) != 0;
     if (const char *e = getenv("MRG_TEST_L2_CAP")) {
         unsigned a = 8, d = 64;
         if (sscanf(e, "%u,%u", &a, &d) >= 1) { sp.capmul = a; sp.capadd = d; }

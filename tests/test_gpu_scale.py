@@ -253,7 +253,7 @@ def knobs():
             "MRG_TEST_LEAF_TARGET", "MRG_TEST_SORT_LCAP", "MRG_TEST_AGG_WIDE_OVF", "MRG_TEST_AGG_NSUB",
             "MRG_TEST_NO_PACK", "MRG_TEST_LONG_PER", "MRG_TEST_LONG_LIST", "MRG_WIDE_MAP", "MRG_TEST_WMAP_CAP",
             "MRG_TEST_WMAP_B1R", "MRG_TEST_WMAP_W12", "MRG_TEST_WMAP_L16", "MRG_TEST_L2_CAP",
-            "MRG_TEST_L2_MIN", "MRG_WIDE_L2_EXACT"]
+            "MRG_TEST_L2_MIN", "MRG_WIDE_L2_SAMPLED"]
     saved = {k: os.environ.get(k) for k in keys}
 
     def set_(**kw):
@@ -677,12 +677,12 @@ def test_wide_many_partitions_vs_oracle(ctx, knobs):
 
 
 def test_wide_l2_sampled_leaves_vs_oracle(ctx, knobs):
-    """The wide map's L2 (k_wide.hip k_wl2): a bucket's digit histogram from a
-    quarter of its records, fixed-capacity leaf regions, and the exact second launch for every bucket
-    whose leaf overflowed.  256 MiB of near-unique keys at R = 16 (every bucket sampled: the size floor
+    """The wide map's sampled L2 (MRG_WIDE_L2_SAMPLED; k_wide.hip k_wl2): a
+    bucket's digit histogram from a quarter of its records, fixed-capacity leaf regions, and the exact
+    second launch for every bucket whose leaf overflowed.  256 MiB of near-unique keys at R = 16 (every bucket sampled: the size floor
     lowered to 1024 records), then mixed lengths and repeated keys at R = 7; default capacities, regions
     of 1 x the sampled count (every bucket overflows: all redone), 3 x (some redone), and the exact
-    histogram -- all byte-identical to the oracle."""
+    histogram (the default) -- all byte-identical to the oracle."""
     import torch
     import oracle_lib as O
     from gpu_util import run_wc
@@ -692,7 +692,8 @@ def test_wide_l2_sampled_leaves_vs_oracle(ctx, knobs):
     exp = O.wc_mt(files, 16, threads=THREADS)
     docs = [_mixed_keys_doc(13, 300_000), b" ".join([b"repeated"] * 40000 + [b"twelvecharsx"] * 30000)]
     exp2 = O.wc(docs, 7, O.FAST)
-    for knob in ({}, {"MRG_TEST_L2_CAP": "1,0"}, {"MRG_TEST_L2_CAP": "3,0"}, {"MRG_WIDE_L2_EXACT": 1}):
+    sampled = {"MRG_WIDE_L2_SAMPLED": 1}
+    for knob in (sampled, dict(sampled, MRG_TEST_L2_CAP="1,0"), dict(sampled, MRG_TEST_L2_CAP="3,0"), {}):
         knobs(MRG_WIDE_MAP=1, MRG_TEST_L2_MIN=1024, **knob)
         got = _run_job(ctx, buf, nf, fb, 16)
         st = ctx.stats()
