@@ -831,6 +831,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     __shared__ __attribute__((aligned(16))) uint64_t s_wspl[WIDE ? 2 * MRG_WMAP_MAXB1 : 1];  // its splitters
     __shared__ __attribute__((aligned(4))) uint8_t s_wix[WIDE ? MRG_WMAP_IXR * MRG_WIDE_IX1 : 4];
     __shared__ uint32_t s_next, s_ngen;                  // next block of the workgroup's share; list length
+    __shared__ uint32_t s_stolen;                        // pool blocks this workgroup's waves have claimed
+    __shared__ uint32_t s_pool[NW][3];                   // per wave: its pool chunk [cur, end) past n_static, part | tried << 8
     __shared__ uint32_t s_nuni;                          // non-ASCII tiles tokenized with UTF-8-exact masks
     // the class table's blocks for U+0000..U+07FF (2-byte codepoints: Latin-1, Latin Extended, Greek,
     // Cyrillic, ...) and U+2000..U+20FF (General Punctuation: the quotes and dashes of English text),
@@ -887,6 +889,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     }
     if (tid == 0) {
         s_next = 0;
+        s_stolen = 0;
         s_ngen = 0;
         s_nuni = 0;
         s_tot[0] = 0;
@@ -978,12 +981,15 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         X.e = ld(lane == 0 ? 0u : 128u + (uint32_t)lane);
     };
 
-    // Work split: workgroup w owns blocks [wlo_b, whi_b) (equal shares); its waves take the next
-    // block from an LDS counter, so a wave that the SIMD's age-ordered issue leaves behind simply
-    // takes fewer blocks (a static per-wave split left the youngest waves finishing last).
-    const uint64_t nb = A.n_chunks;  // blocks of the job
-    const uint64_t wlo_b = nb * blockIdx.x / gridDim.x, whi_b = nb * (blockIdx.x + 1) / gridDim.x;
-    // non-ASCII tiles: appended to this workgroup's list (tile index relative to wlo_b * NSUB),
+    // Work split: workgroup w owns blocks [wlo_b, whi_b) (equal shares of the first n_static); its
+    // waves take the next block from an LDS counter, so a wave that the SIMD's age-ordered issue leaves
+    // behind simply takes fewer blocks (a static per-wave split left the youngest waves finishing last).
+    // The blocks past n_static are a pool the waves of workgroups done with their share take from
+    // (r06: workgroups ran 7.14-7.58 ms on equal shares of C3, the launch lasting as long as the
+    // slowest), MRG_MAP_STEAL_K at a time from one of 8 part counters, within the workgroup's budget.
+    const uint64_t ns = A.n_static;  // blocks in equal shares (of A.n_chunks)
+    const uint64_t wlo_b = ns * blockIdx.x / gridDim.x, whi_b = ns * (blockIdx.x + 1) / gridDim.x;
+    // non-ASCII tiles: appended to this workgroup's list (absolute tile index: block * NSUB + tile),
     // processed after the main loop by all 16 waves
     GAS uint32_t *glist = gp(A.gbits) + (uint64_t)blockIdx.x * A.kwords;
 
@@ -1420,7 +1426,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
             if (lane == 0) {
                 for (uint32_t j = 0; j < NSUB && Ab + (uint64_t)j * TILE < doc_hi; ++j) {
                     const uint32_t k = atomicAdd(&s_ngen, 1u);
-                    glist[k] = (uint32_t)((cblk - wlo_b) * NSUB + j);
+                    glist[k] = (uint32_t)(cblk * NSUB + j);
                 }
             }
             return;
@@ -1559,13 +1565,56 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     // Main loop: two register sets, A and B.  Block c's loads were issued one block earlier; the
     // next block's loads go out before c is processed, so exactly five loads are younger than c's
     // when its data is first used.  Past the end, the "next" block is a reload of the current one.
+    // the wave's pool state lives in LDS (s_pool[wv]): registers held across the main loop would add
+    // to the kernel's SGPR spills; it is touched once per block
+    constexpr uint64_t NONE = ~0ull;
+    uint32_t dcur = 0;
+    if (lane == 0) {
+        s_pool[wv][0] = 0;
+        s_pool[wv][1] = 0;
+        s_pool[wv][2] = (blockIdx.x & 7u) | ((A.n_static < A.n_chunks ? 0u : 8u) << 8);
+    }
     auto grab = [&]() -> uint64_t {
         uint32_t r = 0;
         if (lane == 0) r = atomicAdd(&s_next, 1u);
-        return wlo_b + (uint64_t)first_u32(r);
+        const uint64_t c0 = wlo_b + (uint64_t)first_u32(r);
+        if (c0 < whi_b) return c0;
+        const uint64_t ns2 = A.n_static, np = A.n_chunks - ns2;   // (re-read: not held in registers)
+        wave_sync_lds();
+        const uint32_t cur = first_u32(s_pool[wv][0]), end = first_u32(s_pool[wv][1]);
+        if (cur < end) {
+            if (lane == 0) s_pool[wv][0] = cur + 1u;
+            return ns2 + cur;
+        }
+        uint32_t pt = first_u32(s_pool[wv][2]);
+        while ((pt >> 8) < 8u) {
+            const uint32_t part = pt & 7u;
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(&s_stolen, (uint32_t)MRG_MAP_STEAL_K);
+            if (first_u32(k) >= A.steal_max) {  // this workgroup's budget is spent
+                pt = 8u << 8;
+                break;
+            }
+            const uint32_t plo = (uint32_t)(np * part / 8u), phi = (uint32_t)(np * (part + 1u) / 8u);
+            unsigned long long q = 0;
+            if (lane == 0) q = atomicAdd(&A.pool_ctr[16u * part], (unsigned long long)MRG_MAP_STEAL_K);
+            const uint32_t at = plo + first_u32((uint32_t)umin64(q, 0xFFFFFFFFull));
+            if (at < phi) {
+                if (lane == 0) {
+                    s_pool[wv][0] = at + 1u;
+                    s_pool[wv][1] = min(phi, at + (uint32_t)MRG_MAP_STEAL_K);
+                    s_pool[wv][2] = pt;
+                }
+                dcur = find_doc(A, ns2 + at);  // (a part may lie before the previous one)
+                return ns2 + at;
+            }
+            pt = ((pt & 7u) + 1u) % 8u | (((pt >> 8) + 1u) << 8);
+        }
+        if (lane == 0) s_pool[wv][2] = pt;
+        return NONE;
     };
     uint64_t c = grab();
-    uint32_t dcur = c < whi_b ? find_doc(A, c) : 0u;
+    if (c != NONE) dcur = find_doc(A, c);
     Blk XA, XB;
     BlkInfo IA{}, IB{};
     // Make a block's registers available HERE (the compiler waits for its loads at this point, when
@@ -1575,7 +1624,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         asm volatile("" : "+v"(X.v0.x), "+v"(X.v0.y), "+v"(X.v0.z), "+v"(X.v0.w), "+v"(X.v1.x), "+v"(X.v1.y),
                      "+v"(X.v1.z), "+v"(X.v1.w), "+v"(X.e.x), "+v"(X.e.y), "+v"(X.e.z), "+v"(X.e.w));
     };
-    if (c < whi_b) {
+    if (c != NONE) {
         IA = locate_blk(A, c, dcur);
 #ifdef MRG_MAP_ABLATION
         first_blk = IA;
@@ -1583,15 +1632,15 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         load_blk(IA, XA);
         settle(XA);
     }
-    while (c < whi_b) {
+    while (c != NONE) {
         const uint64_t cB = grab();
-        IB = cB < whi_b ? locate_blk(A, cB, dcur) : IA;
+        IB = cB != NONE ? locate_blk(A, cB, dcur) : IA;
         load_blk(IB, XB);
         process_blk(IA, XA, c, [&]() { settle(XB); });
         c = cB;
-        if (c >= whi_b) break;
+        if (c == NONE) break;
         const uint64_t cA = grab();
-        IA = cA < whi_b ? locate_blk(A, cA, dcur) : IB;
+        IA = cA != NONE ? locate_blk(A, cA, dcur) : IB;
         load_blk(IA, XA);
         process_blk(IB, XB, c, [&]() { settle(XA); });
         c = cA;
@@ -1604,7 +1653,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         for (uint32_t i = (uint32_t)wv; i < ng; i += NW) {
             {
                 const uint32_t kk = first_u32(glist[i]);
-                const uint64_t cb = wlo_b + kk / NSUB;
+                const uint64_t cb = kk / NSUB;
                 uint32_t dgen = find_doc(A, cb);
                 const BlkInfo b = locate_blk(A, cb, dgen);
                 const TileInfo T = sub_tile(b, kk % NSUB);

@@ -90,9 +90,9 @@ struct MapArgs {
     uint64_t lovf;
     uint32_t *lcount;
     // non-ASCII tiles, recorded by the main loop and processed after it: workgroup g appends the
-    // index of each such tile (relative to its first block's first tile) to gbits[g * kwords ..)
+    // index of each such tile (block * NSUB + tile, absolute) to gbits[g * kwords ..)
     uint32_t *gbits;
-    uint32_t kwords;             // list capacity per workgroup (tiles of its share)
+    uint32_t kwords;             // list capacity per workgroup (tiles of its share + its steal budget)
     unsigned long long *counters;
     uint32_t hash_bits;          // 0 = full; else truncate internal hashes (collision test knob)
     uint32_t ablate;             // perf diagnostics only (env MRG_ABLATE; results are WRONG when set):
@@ -122,7 +122,16 @@ struct MapArgs {
     uint32_t w12, wl16cap;
     uint64_t *wl16;
     uint32_t *wl16n;
+    // load balance (mrgpu.cpp map_steal): blocks [0, n_static) are split into
+    // equal workgroup shares; blocks [n_static, n_chunks) are a pool in 8 parts, part j's next block at
+    // pool_ctr[16 * j] (zeroed per launch), that a wave takes MRG_MAP_STEAL_K blocks at a time once its
+    // workgroup's share is done, at most steal_max blocks per workgroup (the per-workgroup capacities
+    // are sized for share + steal_max).  n_static = n_chunks: static shares only.
+    uint64_t n_static;
+    uint32_t steal_max;
+    unsigned long long *pool_ctr;
 };
+#define MRG_MAP_STEAL_K 4        // blocks a wave takes from the pool at a time
 #define MRG_WMAP_MAXB1 4096      // L1 buckets the wide map's LDS cursors hold
 #define MRG_WIDE_IX1 260         // bytes of one partition's L1 splitter index (257 entries + prefix bits)
 #define MRG_WMAP_IXR 64          // partitions whose index fits the wide map's LDS

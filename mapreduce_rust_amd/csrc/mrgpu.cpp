@@ -548,8 +548,10 @@ struct MapBufs {
     uint32_t *dlen = nullptr, *ddoc = nullptr;
     uint32_t *gbits = nullptr;
     unsigned long long *prof = nullptr;
+    unsigned long long *pool_ctr = nullptr;  // the load-balance pool's part counters
     void release(Pool &p) {
         p.put(prof);
+        p.put(pool_ctr);
         p.put(lcount); p.put(dstart); p.put(dlen); p.put(ddoc);
         p.put(pool); p.put(rbase); p.put(bcap); p.put(bcount); p.put(dargs); p.put(ovf); p.put(onext);
         p.put(pool16); p.put(rbase16); p.put(bcap16); p.put(bcount16);
@@ -558,6 +560,9 @@ struct MapBufs {
         *this = MapBufs{};
     }
 };
+
+struct MapSteal;
+void set_steal(mrg_ctx *c, MapArgs &A, MapBufs &M, const MapSteal &ms, uint64_t n_chunks);
 
 struct AggLaunch {
     BucketArgs B{};
@@ -1215,6 +1220,46 @@ WideMapPlan wide_map_plan(mrg_ctx *c, const uint64_t *d_doc_off, uint32_t nd, ui
     return P;
 }
 
+// Load balance of a map launch: the last 1/16 of the blocks form a pool that a
+// workgroup's waves take from once its equal share of the rest is done, at most steal_max blocks per
+// workgroup -- so a workgroup maps at most per_wg_blocks blocks, and its per-workgroup capacities (tail
+// and long-token regions, wide-map regions, the non-ASCII tile list) are sized for that (wg_scale x an
+// equal share).  MRG_MAP_STEAL=0, or a small input: equal shares of every block, as before r06.
+struct MapSteal {
+    uint64_t n_static = 0;     // blocks in equal shares
+    uint32_t steal_max = 0;    // pool blocks one workgroup may take
+    uint64_t per_wg_blocks = 0;
+    double wg_scale = 1.0;
+};
+MapSteal map_steal(uint64_t n_chunks, int grid) {
+    MapSteal m;
+    const uint64_t g = (uint64_t)std::max(grid, 1);
+    const uint64_t pool = env_u64("MRG_MAP_STEAL", 1) ? n_chunks / 16 : 0;
+    if (pool < 64 * g) {  // nothing worth balancing
+        m.n_static = n_chunks;
+        m.per_wg_blocks = (n_chunks + g - 1) / g + 1;
+        return m;
+    }
+    m.n_static = n_chunks - pool;
+    m.steal_max = (uint32_t)(2 * pool / g + 1024);
+    m.per_wg_blocks = (m.n_static + g - 1) / g + 1 + m.steal_max;
+    m.wg_scale = (double)m.per_wg_blocks / ((double)n_chunks / (double)g);
+    return m;
+}
+
+// the steal plan into a launch's arguments, with its pool counters (zeroed on the stream)
+void set_steal(mrg_ctx *c, MapArgs &A, MapBufs &M, const MapSteal &ms, uint64_t n_chunks) {
+    if (n_chunks * MRG_MAP_NSUB >= 0xFFFFFFFFull) raise(MRG_ENOMEM, "input too large for one map launch");
+    A.n_static = ms.n_static;
+    A.steal_max = ms.steal_max;
+    A.pool_ctr = nullptr;
+    if (ms.n_static < n_chunks) {
+        if (!M.pool_ctr) M.pool_ctr = pget<unsigned long long>(c->pool, 8 * 16);
+        HIPCHK(hipMemsetAsync(M.pool_ctr, 0, 8ull * 8 * 16, c->stream));
+        A.pool_ctr = M.pool_ctr;
+    }
+}
+
 void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_cb, uint32_t *d_ids, uint32_t nd,
                   uint64_t n_chunks, uint64_t total, int grid, const std::vector<uint32_t> &ids) {
     Pool &p = c->pool;
@@ -1222,8 +1267,9 @@ void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_
     const uint32_t B1 = wp.B1;
     // records per (bucket, workgroup) region: the splitters make the buckets about equal; a token per
     // ~10 input bytes, +30 %, or the last run's demand
+    const MapSteal ms = map_steal(n_chunks, grid);
     uint64_t wcap = std::max<uint64_t>(c->wcap_hint,
-                                       (uint64_t)(1.3 * (double)total / 10.0 / (double)grid / (double)B1) + 64);
+                                       (uint64_t)(1.3 * ms.wg_scale * (double)total / 10.0 / (double)grid / (double)B1) + 64);
     if (const uint64_t t = env_u64("MRG_TEST_WMAP_CAP", 0)) wcap = t;
     uint64_t lcap = std::max<uint64_t>(c->long_hint, total / 1024 + 1024);
     MapArgs A{};
@@ -1239,17 +1285,17 @@ void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_
     for (;;) {
         if (wcap > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
         M.dargs = pget<MapArgs>(p, 1);
-        uint64_t lper = std::max<uint64_t>(c->lper_hint, (lcap + grid - 1) / grid + 16);
+        uint64_t lper = std::max<uint64_t>(c->lper_hint, (uint64_t)(ms.wg_scale * (double)((lcap + grid - 1) / grid)) + 16);
         const uint64_t lovf = lcap / 4 + 1024;
         const uint64_t lslots = (uint64_t)grid * lper + lovf;
         M.lstart = pget<uint64_t>(p, lslots);
         M.llen = pget<uint32_t>(p, lslots);
         M.ldoc = pget<uint32_t>(p, lslots);
         M.lcount = pget<uint32_t>(p, (uint64_t)grid);
-        const uint64_t per_wg_blocks = (n_chunks + grid - 1) / grid + 1;
         A = MapArgs{};
-        A.kwords = (uint32_t)(MRG_MAP_NSUB * per_wg_blocks);
+        A.kwords = (uint32_t)(MRG_MAP_NSUB * ms.per_wg_blocks);
         M.gbits = pget<uint32_t>(p, (uint64_t)grid * A.kwords);
+        set_steal(c, A, M, ms, n_chunks);
         const uint64_t nslots = (uint64_t)B1 * grid * wcap;
         wrec = pget<uint64_t>(p, w12 ? (12 * nslots + 16 + 7) / 8 : 2 * nslots + 2);
         wcnt = pget<uint32_t>(p, (uint64_t)B1 * grid);
@@ -1410,7 +1456,9 @@ void job_map(mrg_ctx *c) {
     h2d(c, d_ids, ids.data(), 4ull * nd);
 
     if (!c->map_grid) c->map_grid = mrg_map_max_grid(c->app, c->lds_cap, c->device);
-    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->map_grid, n_chunks));
+    // (MRG_TEST_MAP_GRID: more workgroups than fit at once, run in waves: an A/B knob for load balance)
+    const uint64_t grid_want = env_u64("MRG_TEST_MAP_GRID", (uint64_t)c->map_grid);
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(grid_want, n_chunks));
     bool cold_repeats = false;  // a cold context whose sample found repeats: queue the aggregation too
     {  // near-unique input: the wide map (every key straight to its L1 bucket)
         WideMapPlan wp = wide_map_plan(c, d_doc_off, nd, total, grid);
@@ -1426,7 +1474,8 @@ void job_map(mrg_ctx *c) {
     uint64_t lcap = std::max<uint64_t>(c->long_hint, total / 1024 + 1024);
     // records per (bucket, workgroup) tail region: ~1 in 20 input bytes is a tail record (combine
     // misses), spread evenly over the buckets; grown per bucket to the measured demand on a rerun
-    const double per_wg = (double)std::max<uint64_t>(total, 1) / grid;
+    const MapSteal ms = map_steal(n_chunks, grid);
+    const double per_wg = (double)std::max<uint64_t>(total, 1) / grid * ms.wg_scale;
     // wc keys of 13..16 bytes (rare in text) get regions of 16-byte records a sixteenth that size
     std::vector<uint64_t> bcap(MRG_NBUCKET), bcap16(MRG_NBUCKET, 0);
     for (int b = 0; b < MRG_NBUCKET; ++b) {
@@ -1498,7 +1547,7 @@ void job_map(mrg_ctx *c) {
         M.fdoc = idx ? pget<uint32_t>(p, (uint64_t)grid * cap) : nullptr;
         M.foff = pget<uint32_t>(p, (uint64_t)grid * (MRG_NBUCKET + 1));
         // long tokens: per-workgroup regions of lper records + a shared list of lovf
-        uint64_t lper = std::max<uint64_t>(c->lper_hint, (lcap + grid - 1) / grid + 16);
+        uint64_t lper = std::max<uint64_t>(c->lper_hint, (uint64_t)(ms.wg_scale * (double)((lcap + grid - 1) / grid)) + 16);
         uint64_t lovf = lcap / 4 + 1024;
         if (launches == 0) {  // test knobs (first launch only: a rerun grows them from the measured demand)
             if (const uint64_t t = env_u64("MRG_TEST_LONG_PER", 0)) lper = t;
@@ -1516,12 +1565,12 @@ void job_map(mrg_ctx *c) {
         A.fk0 = M.fk0; A.fk1 = M.fk1; A.fcnt = M.fcnt; A.fdoc = M.fdoc; A.foff = M.foff;
         A.lstart = M.lstart; A.llen = M.llen; A.ldoc = M.ldoc; A.lper = (uint32_t)lper; A.lovf = lovf;
         A.lcount = M.lcount;
-        {  // non-ASCII tile lists: one entry per tile of a workgroup's share at most
-            const uint64_t per_wg_blocks = (n_chunks + grid - 1) / grid + 1;
-            A.kwords = (uint32_t)(MRG_MAP_NSUB * per_wg_blocks);
+        {  // non-ASCII tile lists: one entry per tile of a workgroup's share and steal budget at most
+            A.kwords = (uint32_t)(MRG_MAP_NSUB * ms.per_wg_blocks);
             M.gbits = pget<uint32_t>(p, (uint64_t)grid * A.kwords);
             A.gbits = M.gbits;
         }
+        set_steal(c, A, M, ms, n_chunks);
         A.counters = c->d_cnt;
         A.hash_bits = hash_bits(c);
         A.ablate = getenv("MRG_ABLATE") ? (uint32_t)atoi(getenv("MRG_ABLATE")) : 0u;
