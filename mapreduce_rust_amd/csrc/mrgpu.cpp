@@ -1236,7 +1236,7 @@ MapSteal map_steal(uint64_t n_chunks, int grid) {
     const uint64_t g = (uint64_t)std::max(grid, 1);
     const uint64_t div = env_u64("MRG_MAP_STEAL", 16);  // the pool is 1/div of the blocks (0: no pool)
     const uint64_t pool = div ? n_chunks / div : 0;
-    if (pool < 64 * g) {  // nothing worth balancing
+    if (pool == 0 || pool < env_u64("MRG_TEST_STEAL_MIN", 64 * g)) {  // nothing worth balancing (tests: any pool)
         m.n_static = n_chunks;
         m.per_wg_blocks = (n_chunks + g - 1) / g + 1;
         return m;

@@ -167,6 +167,54 @@ def test_codepoint_density_sweep_vs_oracle(ctx, gap):
         assert run_wc(ctx, docs, 3) == O.wc(docs, 3, O.FAST)
 
 
+@pytest.mark.parametrize("steal", ["2", "16"])
+def test_map_block_pool_vs_oracle(ctx, corpus, steal):
+    """k_map's pool of blocks (mrgpu.cpp map_steal) on inputs below its size
+    floor (MRG_TEST_STEAL_MIN=0): half (steal = 2) or 1/16 of the blocks taken from the 8 part counters
+    by workgroups done with their share -- C1 golden digests, the indexer golden, Unicode and long
+    tokens, deferred (invalid) UTF-8 and a near-unique document through the wide map, against the
+    oracle; a pooled block with invalid UTF-8 fails the job like any other."""
+    import oracle_lib as O
+    import mapreduce_rust_amd as M
+    from gpu_util import run_wc
+    keys = ("MRG_MAP_STEAL", "MRG_TEST_STEAL_MIN", "MRG_WIDE_MAP")
+    saved = {k: os.environ.get(k) for k in keys}
+    os.environ["MRG_MAP_STEAL"] = steal
+    os.environ["MRG_TEST_STEAL_MIN"] = "0"
+    try:
+        for R in ("10", "64"):
+            outs = run_wc(ctx, corpus, int(R))
+            assert [sha(o) for o in outs] == [GOLDEN["wc"][R][f"mr-{r}.txt"] for r in range(int(R))], R
+        names = [f"data/gut-{m}.txt" for m in range(6)]
+        outs = run_wc(ctx, corpus, 10, app=M.APP_INDEXER, names=names)
+        assert [sha(o) for o in outs] == [GOLDEN["indexer"]["10"][f"mr-{r}.txt"] for r in range(10)]
+        rng = random.Random(int(steal))
+        docs = [_rand_text(rng, 20000, ALPHA, SEPS, max_len=40) for _ in range(3)] + corpus[:2]
+        for R in (1, 7):
+            assert run_wc(ctx, docs, R) == O.wc(docs, R, O.FAST), R
+        bad = bytearray(corpus[3])
+        bad[len(bad) - 3000] = 0xC3  # a lead without its continuation near the end: a pooled block
+        bad[len(bad) - 2999] = 0x41
+        with pytest.raises(M.MrgError) as ei:
+            run_wc(ctx, [corpus[0], bytes(bad)], 3)
+        assert ei.value.code == -2
+        assert run_wc(ctx, docs, 7) == O.wc(docs, 7, O.FAST)
+        import torch
+        n = 8 << 20
+        t = torch.empty(n + 64, dtype=torch.uint8, device="cuda:0")
+        ctx.gen_unique(t.data_ptr(), n, 0xC5, 5)
+        udoc = [t[:n].cpu().numpy().tobytes()]
+        os.environ["MRG_WIDE_MAP"] = "1"
+        assert run_wc(ctx, udoc, 64) == O.wc(udoc, 64, O.FAST)
+        assert ctx.stats()["map_kind"] == 1
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def test_tile_boundaries_and_long_tokens(ctx):
     """Tokens straddling 4 KiB tiles / 16 B lane segments / the 256 B halo, and > 16 B keys."""
     import oracle_lib as O
