@@ -1605,7 +1605,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
                     s_pool[wv][1] = min(phi, at + (uint32_t)MRG_MAP_STEAL_K);
                     s_pool[wv][2] = pt;
                 }
-                dcur = find_doc(A, ns2 + at);  // (a part may lie before the previous one)
+                // the document cursor walks forward (locate_blk); a search only when the chunk lies before
+                // it (the wrap from part 7 to part 0)
+                if (cp(A.chunk_base)[dcur] > ns2 + at) dcur = find_doc(A, ns2 + at);
                 return ns2 + at;
             }
             pt = ((pt & 7u) + 1u) % 8u | (((pt >> 8) + 1u) << 8);

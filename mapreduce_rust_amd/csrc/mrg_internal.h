@@ -131,7 +131,9 @@ struct MapArgs {
     uint32_t steal_max;
     unsigned long long *pool_ctr;
 };
+#ifndef MRG_MAP_STEAL_K
 #define MRG_MAP_STEAL_K 4        // blocks a wave takes from the pool at a time
+#endif
 #define MRG_WMAP_MAXB1 4096      // L1 buckets the wide map's LDS cursors hold
 #define MRG_WIDE_IX1 260         // bytes of one partition's L1 splitter index (257 entries + prefix bits)
 #define MRG_WMAP_IXR 64          // partitions whose index fits the wide map's LDS
