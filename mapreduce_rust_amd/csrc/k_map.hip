@@ -94,6 +94,12 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
     return v;
 }
+// a workgroup barrier for LDS only: the wave's outstanding global stores are not waited for (a
+// __syncthreads() waits for them too -- at the end of the map that is every workgroup's last tail
+// stores at once)
+__device__ __forceinline__ void lds_only_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1003,6 +1009,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     const bool P = A.prof != nullptr;
     uint64_t pacc[7] = {0, 0, 0, 0, 0, 0, 0}, tl = P ? clock64() : 0;
     const uint64_t wg_t0 = wall_clock64();  // workgroup start/end (100 MHz): load balance across CUs
+    unsigned long long ftv[5] = {0, 0, 0, 0, 0};   // flush step ends (wall clock, workgroup thread 0)
+#define MRG_FT(i)                                   \
+    if (P && tid == 0) ftv[i] = wall_clock64();
 #define MRG_PT(i)                          \
     if (P) {                               \
         const uint64_t t_ = clock64();     \
@@ -1011,6 +1020,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     }
 #else
 #define MRG_PT(i)
+#define MRG_FT(i)
 #endif
     // A token of the wave's queue: entry q (of total) holds its start s (tile offset); its raw
     // length, \w span and deleted bytes come from one 8-byte mask-pair read, its key bytes from the
@@ -1648,8 +1658,15 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         c = cA;
     }
     MRG_PT(4);
+#ifdef MRG_MAP_PROF
+    __shared__ unsigned long long s_loop_end;
+    if (tid == 0) s_loop_end = 0;
+    lds_only_barrier();
+    if (P && lane == 0) atomicMax(&s_loop_end, (unsigned long long)wall_clock64());
+#endif
     // ---- non-ASCII tiles recorded by the main loop
-    __syncthreads();  // the list is complete (global writes of this workgroup, then the barrier)
+    lds_only_barrier();   // s_ngen final
+    if (s_ngen) __syncthreads();  // (uniform) the list is complete: its global writes, then the barrier
     {
         const uint32_t ng = s_ngen;
         for (uint32_t i = (uint32_t)wv; i < ng; i += NW) {
@@ -1672,8 +1689,9 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
     }
 
     MRG_PT(5);
-    // ---- flush the LDS table into this workgroup's region, sorted by bucket
-    __syncthreads();
+    // ---- flush the LDS table into this workgroup's region, sorted by bucket (LDS-only barriers from
+    // here on: the tail stores drain meanwhile; the kernel's end waits for them)
+    lds_only_barrier();
     uint32_t my_tail = 0, my_tail16 = 0;
     if constexpr (WIDE) {  // the wide map: records per L1 bucket; a region past its capacity -> rerun
         uint32_t over = 0;
@@ -1699,14 +1717,16 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         }
     }
     for (int b = tid; b <= MRG_NBUCKET; b += WG) s_hist[b] = 0;
-    __syncthreads();
+    lds_only_barrier();
+    MRG_FT(0);
     for (int i = tid; i < CAP; i += WG) {
         const KeyPair k = s_key[i];
         if (k.a == MRG_EMPTY_K0) continue;
         const uint32_t b = bucket_of(key_hash(k.a, k.b, IDX ? s_doc[i] : MRG_EMPTY_DOC, A.hash_bits));
         s_rank[i] = (uint16_t)atomicAdd(&s_hist[b], 1u);
     }
-    __syncthreads();
+    lds_only_barrier();
+    MRG_FT(1);
     if (tid < 64) {  // exclusive scan of the bucket histogram by one wave
         uint32_t run = 0;
         for (int b0 = 0; b0 < MRG_NBUCKET; b0 += 64) {
@@ -1717,7 +1737,8 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         }
         if (lane == 0) s_hist[MRG_NBUCKET] = run;
     }
-    __syncthreads();
+    lds_only_barrier();
+    MRG_FT(2);
     GAS uint32_t *foff = gp(A.foff) + (uint64_t)blockIdx.x * (MRG_NBUCKET + 1);
     for (int b = tid; b <= MRG_NBUCKET; b += WG) foff[b] = s_hist[b];
     const uint64_t reg = (uint64_t)blockIdx.x * CAP;
@@ -1733,6 +1754,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         if (IDX) gp(A.fdoc)[pos2] = d;
     }
     }
+    MRG_FT(3);
     // token and tail totals: waves -> LDS -> one device atomic per workgroup and counter (a wave
     // atomic each put 8 K atomics on two counters at the very end of the launch)
     uint32_t t = my_tokens, ttl = my_tail, t16 = my_tail16;
@@ -1746,7 +1768,7 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         atomicAdd(&s_tot[1], ttl);
         if (t16) atomicAdd(&s_tot[2], t16);
     }
-    __syncthreads();
+    lds_only_barrier();
     if (tid == 0) {
         g_add(&A.counters[CNT_TOKENS], (unsigned long long)s_tot[0]);
         g_add(&A.counters[CNT_REC], (unsigned long long)s_tot[1]);
@@ -1755,14 +1777,17 @@ __global__ __launch_bounds__(WG, 1) void k_map(const MapArgs *__restrict__ Ap) {
         gp(A.lcount)[blockIdx.x] = s_lcnt;
         if (s_lcnt) g_add(&A.counters[CNT_LONG], (unsigned long long)s_lcnt);
     }
+    MRG_FT(4);
     MRG_PT(6);
 #ifdef MRG_MAP_PROF
     if (P && lane == 0) {
         for (int i = 0; i < 7; ++i) g_add(&A.prof[i], (unsigned long long)pacc[i]);
     }
     if (P && tid == 0) {
-        gp(A.prof)[8 + 2 * blockIdx.x] = wg_t0;
-        gp(A.prof)[9 + 2 * blockIdx.x] = wall_clock64();
+        gp(A.prof)[8 + 8 * blockIdx.x] = wg_t0;
+        gp(A.prof)[9 + 8 * blockIdx.x] = wall_clock64();
+        gp(A.prof)[10 + 8 * blockIdx.x] = s_loop_end;   // the last wave's main-loop end
+        for (int i = 0; i < 5; ++i) gp(A.prof)[11 + 8 * blockIdx.x + i] = ftv[i];   // the flush's steps
     }
 #endif
 }

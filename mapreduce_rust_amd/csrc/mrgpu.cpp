@@ -1577,8 +1577,8 @@ void job_map(mrg_ctx *c) {
         A.ablate = getenv("MRG_ABLATE") ? (uint32_t)atoi(getenv("MRG_ABLATE")) : 0u;
         A.prof = nullptr;
         if (getenv("MRG_PROF")) {
-            M.prof = pget<unsigned long long>(p, 8 + 2ull * grid);
-            HIPCHK(hipMemsetAsync(M.prof, 0, 8ull * (8 + 2ull * grid), s));
+            M.prof = pget<unsigned long long>(p, 8 + 8ull * grid);
+            HIPCHK(hipMemsetAsync(M.prof, 0, 8ull * (8 + 8ull * grid), s));
             A.prof = M.prof;
         }
         HIPCHK(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long) * CNT_N, s));
@@ -1622,24 +1622,42 @@ void job_map(mrg_ctx *c) {
             for (int i = 0; i < 7; ++i) fprintf(stderr, " %s %.1f%%", nm[i], 100.0 * (double)pr[i] / (tot > 0 ? tot : 1));
             fprintf(stderr, "\n");
             // workgroup start/end wall clocks (100 MHz; written by -DMRG_MAP_PROF builds only)
-            std::vector<unsigned long long> wt(2ull * grid);
+            std::vector<unsigned long long> wt(8ull * grid);
             HIPCHK(hipMemcpy(wt.data(), M.prof + 8, 8ull * wt.size(), hipMemcpyDeviceToHost));
             if (wt[1]) {
                 unsigned long long t0 = ~0ull, t1 = 0, ls = 0;
-                std::vector<double> dur(grid), end(grid);
-                for (int g = 0; g < grid; ++g) t0 = std::min(t0, wt[2 * g]);
+                std::vector<double> dur(grid), end(grid), lend(grid);
+                std::vector<std::vector<double>> fst(5, std::vector<double>(grid, 0.0));
+                for (int g = 0; g < grid; ++g) t0 = std::min(t0, wt[8 * g]);
                 for (int g = 0; g < grid; ++g) {
-                    t1 = std::max(t1, wt[2 * g + 1]);
-                    ls = std::max(ls, wt[2 * g]);
-                    dur[g] = (double)(wt[2 * g + 1] - wt[2 * g]) * 1e-5;
-                    end[g] = (double)(wt[2 * g + 1] - t0) * 1e-5;
+                    const unsigned long long *w = &wt[8ull * g];
+                    t1 = std::max(t1, w[1]);
+                    ls = std::max(ls, w[0]);
+                    dur[g] = (double)(w[1] - w[0]) * 1e-5;
+                    end[g] = (double)(w[1] - t0) * 1e-5;
+                    lend[g] = w[2] ? (double)(w[2] - t0) * 1e-5 : 0.0;
+                    unsigned long long prev = w[2];
+                    for (int k = 0; k < 5; ++k)
+                        if (w[3 + k] && prev) {
+                            fst[k][g] = (double)(w[3 + k] - prev) * 1e-5;
+                            prev = w[3 + k];
+                        }
                 }
                 std::sort(dur.begin(), dur.end());
                 std::sort(end.begin(), end.end());
+                std::sort(lend.begin(), lend.end());
                 fprintf(stderr, "[mrgpu] map workgroups (ms): span %.3f, end min %.3f med %.3f max %.3f, "
-                        "duration min %.3f med %.3f max %.3f, last start %.3f\n", (double)(t1 - t0) * 1e-5,
-                        end[0], end[grid / 2], end[grid - 1], dur[0], dur[grid / 2], dur[grid - 1],
+                        "main loop end min %.3f med %.3f max %.3f, duration min %.3f med %.3f max %.3f, "
+                        "last start %.3f\n", (double)(t1 - t0) * 1e-5, end[0], end[grid / 2], end[grid - 1],
+                        lend[0], lend[grid / 2], lend[grid - 1], dur[0], dur[grid / 2], dur[grid - 1],
                         (double)(ls - t0) * 1e-5);
+                fprintf(stderr, "[mrgpu] map flush steps (ms, median / max over workgroups):");
+                static const char *fn[5] = {"counts", "histogram", "scan", "entries", "totals"};
+                for (int k = 0; k < 5; ++k) {
+                    std::sort(fst[k].begin(), fst[k].end());
+                    fprintf(stderr, " %s %.4f / %.4f", fn[k], fst[k][grid / 2], fst[k][grid - 1]);
+                }
+                fprintf(stderr, "\n");
             }
         }
         const uint64_t nl = c->h_cnt[CNT_LONG];
