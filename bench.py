@@ -293,7 +293,7 @@ def stage_roofline(stats, shard, out_bytes):
     return stages, ratio, note
 
 
-def cold_job(dev, buf, doc_off, n_reduce, steady):
+def cold_job(dev, buf, doc_off, n_reduce, steady, cached=False):
     """The FIRST job on a fresh Context over the same resident input: what mrg_run_job and every
     one-shot worker call run (the reference runs each task once per call, src/bin/mrworker.rs:95,145).
     Reports its wall time, its kernel time (sum of the HIP-event stages) against the steady steps'
@@ -324,6 +324,8 @@ def cold_job(dev, buf, doc_off, n_reduce, steady):
            "pool_allocs": n_alloc, "pool_alloc_bytes": alloc_bytes, "pool_alloc_ms": round(alloc_ms, 3),
            "ms_wall_minus_alloc": round(wall - alloc_ms, 3),
            "map_launches": st["map_launches"], "map_kind": st["map_kind"], "agg_path": st["agg_path"],
+           "blocks": "from the device cache (the warm leg's Context closed first)" if cached else
+                     "fresh device memory (the warm Context still open)",
            "note": "first job on a fresh Context (same resident input, same process): wall = job_begin .. reduce; "
                    "kernels = sum of the HIP-event stages; pool_alloc_ms = host time inside the pool's hipMalloc calls"}
     log(f"cold job: wall {res['ms_wall']} ms (alloc {res['pool_alloc_ms']} ms in {n_alloc} hipMalloc), kernels "
@@ -332,22 +334,31 @@ def cold_job(dev, buf, doc_off, n_reduce, steady):
     return res
 
 
-def leg(ctx, dev, a, workload, files, steps, warmup):
-    """An extra single-GPU workload (zipf_u, C5) on its own buffer, timed like the headline line."""
+def leg(dev, a, workload, files, steps, warmup):
+    """An extra single-GPU workload (zipf_u, C5) on its own buffer and its own Context, timed like the
+    headline line.  The Context is closed after the timed steps, so its device blocks go to the
+    library's per-device cache (as a worker's do between mrg_run_job calls); C5's cold job then opens
+    a fresh Context over them -- beside a live warm context the two held ~130 GB of the 288, and a
+    device-full trim frees memory the driver must wipe before reuse (seconds: DESIGN.md section 15.4)."""
     fbytes = a.file_mib * MIB
     shard = files * fbytes
     buf = torch.empty(shard + 64, dtype=torch.uint8, device=dev)
-    generate(ctx, buf, workload, files, fbytes, 0, a, dev, quiet=True)
-    doc_off = [i * fbytes for i in range(files + 1)]
+    ctx = M.Context(dev.index)
+    try:
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        generate(ctx, buf, workload, files, fbytes, 0, a, dev, quiet=True)
+        doc_off = [i * fbytes for i in range(files + 1)]
 
-    def step():
-        ctx.job_begin(M.APP_WC, a.reduce)
-        ctx.set_input(buf.data_ptr(), doc_off)
-        ctx.map()
-        return ctx.reduce()
+        def step():
+            ctx.job_begin(M.APP_WC, a.reduce)
+            ctx.set_input(buf.data_ptr(), doc_off)
+            ctx.map()
+            return ctx.reduce()
 
-    dt, step_max, stats = time_steps(ctx, step, steps, warmup, dev, 1, 0, workload)
-    cold = cold_job(dev, buf, doc_off, a.reduce, stats) if workload == "unique" else None
+        dt, step_max, stats = time_steps(ctx, step, steps, warmup, dev, 1, 0, workload)
+    finally:
+        ctx.close()
+    cold = cold_job(dev, buf, doc_off, a.reduce, stats, cached=True) if workload == "unique" else None
     del buf
     torch.cuda.empty_cache()
     m = statistics.median(step_max)
@@ -626,13 +637,13 @@ def main():
         del buf
         torch.cuda.empty_cache()
         if not a.no_zipf_u:
-            u = leg(ctx, dev, a, "zipf_u", files, 5, 2)
+            u = leg(dev, a, "zipf_u", files, 5, 2)
             u["k_map_vs_ascii"] = round(u["k_map_gbs"] / achieved, 4)
             line["zipf_u"] = u
             log(f"zipf_u: {u['value']} GB/s, k_map {u['k_map_gbs']} GB/s = {u['k_map_vs_ascii']} of ASCII, "
                 f"{u['nonascii_tile_frac']} of tiles non-ASCII")
         if not a.no_c5:
-            c5 = leg(ctx, dev, a, "unique", a.c5_files, 3, 1)
+            c5 = leg(dev, a, "unique", a.c5_files, 3, 1)
             line["c5"] = c5
             log(f"C5: {c5['value']} GB/s ({c5['ms_per_step']} ms per step, {c5['distinct_keys']} keys)")
         if not a.no_c2:

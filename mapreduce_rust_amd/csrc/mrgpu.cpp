@@ -116,12 +116,13 @@ class DeviceCache {
         static DeviceCache *c = new DeviceCache();
         return *c;
     }
-    // a cached block of `dev` of at least c bytes and at most c + c / 4 (its size in *got), else null
-    void *take(int dev, size_t c, size_t *got) {
+    // a cached block of `dev` of at least c bytes and at most c + c / 4 (any size >= c when `any`: the
+    // device is full) -- its size in *got -- else null
+    void *take(int dev, size_t c, size_t *got, bool any = false) {
         std::lock_guard<std::mutex> lk(mu_);
         auto &f = free_[dev];
         auto it = f.lower_bound(c);
-        if (it == f.end() || it->first > c + (c >> 2)) return nullptr;
+        if (it == f.end() || (!any && it->first > c + (c >> 2))) return nullptr;
         void *p = it->second;
         *got = it->first;
         bytes_[dev] -= it->first;
@@ -203,6 +204,17 @@ class Pool : public DevPool {
         const auto t0 = std::chrono::steady_clock::now();
         if (hipMalloc(&p, c) != hipSuccess) {
             (void)hipGetLastError();
+            // the device is full: a larger cached block first (memory handed back to the driver is
+            // wiped before it can be allocated again: a trim costs seconds)
+            if (dev_ >= 0) {
+                size_t got = 0;
+                if (void *q = DeviceCache::get().take(dev_, c, &got, true)) {
+                    alloc_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                    size_[q] = got;
+                    ++reused_;
+                    return q;
+                }
+            }
             if (debug_) fprintf(stderr, "[mrgpu] pool: device full, trimming %zu free blocks\n", free_.size());
             trim();
             if (hipMalloc(&p, c) != hipSuccess) {
