@@ -493,6 +493,27 @@ __global__ __launch_bounds__(BA_WG, 1) void k_bucket_agg(BucketArgs A) {
     }
 }
 
+// the staged small writes of a job's setup (mrg_internal.h StageOp), in their issue order -- one
+// workgroup, a barrier between writes: a batch may write a range twice (zero the counters, then set
+// one of them to ~0), and the later write must win, as it did as separate stream operations
+__global__ __launch_bounds__(1024) void k_stage_scatter(const uint8_t *stage, uint32_t table_off, uint32_t nops) {
+    const StageOp *ops = reinterpret_cast<const StageOp *>(stage + table_off);
+    for (uint32_t k = 0; k < nops; ++k) {
+        const StageOp op = ops[k];
+        uint8_t *dst = reinterpret_cast<uint8_t *>(op.dst);
+        const bool fill = op.src == 0xFFFFFFFFu;
+        if (((op.dst | op.n) & 3u) == 0u) {  // dword aligned (every pool block and staging offset is)
+            const uint32_t f4 = op.fill * 0x01010101u;
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + (fill ? 0u : op.src));
+            for (uint32_t i = threadIdx.x; i < op.n / 4u; i += blockDim.x)
+                reinterpret_cast<uint32_t *>(dst)[i] = fill ? f4 : src[i];
+        } else {
+            for (uint32_t i = threadIdx.x; i < op.n; i += blockDim.x) dst[i] = fill ? (uint8_t)op.fill : stage[op.src + i];
+        }
+        __syncthreads();  // (global writes of this workgroup: ordered by the barrier's release)
+    }
+}
+
 __global__ void k_table_clear(TableArgs T, bool idx) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= T.cap) return;
@@ -919,6 +940,10 @@ __global__ void k_iota(uint32_t *p, uint64_t n) {
 }
 
 }  // namespace
+
+void mrg_launch_stage_scatter(const uint8_t *d_stage, uint32_t table_off, uint32_t nops, hipStream_t s) {
+    if (nops) hipLaunchKernelGGL(k_stage_scatter, dim3(1), dim3(1024), 0, s, d_stage, table_off, nops);
+}
 
 void mrg_launch_bucket_agg(const BucketArgs &a, bool indexer, bool count32, hipStream_t s) {
     const dim3 g(MRG_NBUCKET * std::max<uint32_t>(a.nsub, 1u));

@@ -131,6 +131,16 @@ struct MapArgs {
     uint32_t steal_max;
     unsigned long long *pool_ctr;
 };
+// One staged small write of a job's setup (mrgpu.cpp stage_h2d / stage_fill): `n` bytes to `dst`, from
+// offset `src` of the device copy of the pinned staging buffer, or the byte `fill` when src == ~0u.
+// A batch of them is one host-to-device copy and one k_stage_scatter launch (was one copy or memset
+// each, ~8 us apiece on the stream).
+struct StageOp {
+    uint64_t dst;
+    uint32_t src, n, fill, pad;
+};
+void mrg_launch_stage_scatter(const uint8_t *d_stage, uint32_t table_off, uint32_t nops, hipStream_t s);
+
 #ifndef MRG_MAP_STEAL_K
 #define MRG_MAP_STEAL_K 4        // blocks a wave takes from the pool at a time
 #endif

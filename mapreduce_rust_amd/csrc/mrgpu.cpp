@@ -323,6 +323,11 @@ struct mrg_ctx {
     // bump region, reset by job_begin (after its sync), so their copies are plain async DMA
     uint8_t *h_stage = nullptr;
     size_t stage_used = 0;
+    // batched small writes (stage_h2d / stage_fill): their device copy of the staging buffer, the ops
+    // not yet issued, and the first staging byte they use
+    uint8_t *d_stage = nullptr;
+    std::vector<StageOp> pend;
+    size_t pend_lo = 0;
     bool timing = false;
     hipEvent_t ev[8] = {};
     int lds_cap = 4096;
@@ -403,6 +408,56 @@ void h2d(mrg_ctx *c, void *dst, const void *src, size_t n) {
     } else {
         HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->stream));
     }
+}
+
+// Batched small writes of a job's setup (r06): data staged in the pinned buffer like h2d's, the writes
+// recorded, and issued together by flush_stage -- one copy of the staged range (ops table included)
+// and one k_stage_scatter launch instead of a copy or memset each (C3 map setup: 12 -> 2 stream ops).
+// Every kernel that reads a staged destination must be launched after a flush_stage.
+constexpr size_t MRG_STAGE_OPS = 256;   // ops per batch
+constexpr uint32_t MRG_STAGE_MAX = 16384;  // larger writes go through their own copy / memset
+void flush_stage(mrg_ctx *c) {
+    if (c->pend.empty()) return;
+    const size_t t = (c->stage_used + 63) & ~(size_t)63;  // the ops table after the staged data
+    const size_t tb = sizeof(StageOp) * c->pend.size();
+    memcpy(c->h_stage + t, c->pend.data(), tb);
+    HIPCHK(hipMemcpyAsync(c->d_stage + c->pend_lo, c->h_stage + c->pend_lo, t + tb - c->pend_lo, hipMemcpyHostToDevice,
+                          c->stream));
+    mrg_launch_stage_scatter(c->d_stage, (uint32_t)t, (uint32_t)c->pend.size(), c->stream);
+    HIPCHK(hipGetLastError());
+    c->stage_used = c->pend_lo = (t + tb + 63) & ~(size_t)63;
+    c->pend.clear();
+}
+bool stage_room(mrg_ctx *c, size_t n) {
+    if (!c->h_stage || !c->d_stage || n > MRG_STAGE_MAX) return false;
+    if (c->pend.size() >= MRG_STAGE_OPS ||
+        c->stage_used + n + 64 + sizeof(StageOp) * (MRG_STAGE_OPS + 1) > MRG_STAGE_BYTES) {
+        flush_stage(c);
+        if (c->stage_used + n + 64 + sizeof(StageOp) * (MRG_STAGE_OPS + 1) > MRG_STAGE_BYTES) return false;
+    }
+    return true;
+}
+void stage_h2d(mrg_ctx *c, void *dst, const void *src, size_t n) {
+    if (!n) return;
+    if (!stage_room(c, n)) {
+        flush_stage(c);  // (issue order kept)
+        h2d(c, dst, src, n);
+        return;
+    }
+    if (c->pend.empty()) c->pend_lo = c->stage_used;
+    memcpy(c->h_stage + c->stage_used, src, n);
+    c->pend.push_back(StageOp{(uint64_t)(uintptr_t)dst, (uint32_t)c->stage_used, (uint32_t)n, 0u, 0u});
+    c->stage_used += (n + 63) & ~(size_t)63;
+}
+void stage_fill(mrg_ctx *c, void *dst, int byte, size_t n) {
+    if (!n) return;
+    if (!stage_room(c, 0) || n > MRG_STAGE_MAX) {
+        flush_stage(c);
+        HIPCHK(hipMemsetAsync(dst, byte, n, c->stream));
+        return;
+    }
+    if (c->pend.empty()) c->pend_lo = c->stage_used;
+    c->pend.push_back(StageOp{(uint64_t)(uintptr_t)dst, 0xFFFFFFFFu, (uint32_t)n, (uint32_t)(byte & 0xFF), 0u});
 }
 
 void read_counters(mrg_ctx *c) {
@@ -1118,7 +1173,9 @@ void job_begin(mrg_ctx *c, int app, uint32_t R, uint32_t flags) {
     if (app != MRG_APP_WC && app != MRG_APP_INDEXER) raise(MRG_EINVAL, "unknown app %d", app);
     if (R == 0) raise(MRG_EINVAL, "n_reduce must be > 0");
     sync(c);
+    flush_stage(c);     // (nothing is pending between jobs: every map launch flushes first)
     c->stage_used = 0;  // the previous job's staged copies are done
+    c->pend_lo = 0;
     keys_release(c);
     c->wide.release(c->pool);
     c->job = true;
@@ -1170,6 +1227,7 @@ WideMapPlan wide_map_plan(mrg_ctx *c, const uint64_t *d_doc_off, uint32_t nd, ui
     Pool &p = c->pool;
     hipStream_t s = c->stream;
     const uint32_t S = (uint32_t)std::min<uint64_t>(64ull * B1, 1u << 20);
+    flush_stage(c);  // the document tables, read by the sampling kernels
     if (!P.forced && !c->wide_hint) {  // no hint (a cold context): the one-launch test on 8192 samples first
         const uint32_t S0 = std::min<uint32_t>(S, 8192);
         SortRec *s0 = pget<SortRec>(p, S0);
@@ -1268,7 +1326,7 @@ void set_steal(mrg_ctx *c, MapArgs &A, MapBufs &M, const MapSteal &ms, uint64_t 
     A.pool_ctr = nullptr;
     if (ms.n_static < n_chunks) {
         if (!M.pool_ctr) M.pool_ctr = pget<unsigned long long>(c->pool, 8 * 16);
-        HIPCHK(hipMemsetAsync(M.pool_ctr, 0, 8ull * 8 * 16, c->stream));
+        stage_fill(c, M.pool_ctr, 0, 8ull * 8 * 16);
         A.pool_ctr = M.pool_ctr;
     }
 }
@@ -1337,6 +1395,7 @@ void job_map_wide(mrg_ctx *c, WideMapPlan &wp, uint64_t *d_doc_off, uint64_t *d_
             raise(MRG_EINVAL, "wide map plan exceeds the kernel's LDS bounds");
         HIPCHK(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long) * CNT_N, s));
         HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_ERRPOS], 0xFF, sizeof(unsigned long long), s));
+        flush_stage(c);  // (set_steal's pool counters)
         ev_rec(c, 0);
         h2d(c, M.dargs, &A, sizeof(MapArgs));
         mrg_launch_map(nullptr, M.dargs, c->app, grid, c->lds_cap, s, true);
@@ -1464,9 +1523,9 @@ void job_map(mrg_ctx *c) {
 
     uint64_t *d_doc_off = pget<uint64_t>(p, nd + 1), *d_cb = pget<uint64_t>(p, nd + 1);
     uint32_t *d_ids = pget<uint32_t>(p, nd);
-    h2d(c, d_doc_off, c->doc_off.data(), 8ull * (nd + 1));
-    h2d(c, d_cb, cb.data(), 8ull * (nd + 1));
-    h2d(c, d_ids, ids.data(), 4ull * nd);
+    stage_h2d(c, d_doc_off, c->doc_off.data(), 8ull * (nd + 1));
+    stage_h2d(c, d_cb, cb.data(), 8ull * (nd + 1));
+    stage_h2d(c, d_ids, ids.data(), 4ull * nd);
 
     if (!c->map_grid) c->map_grid = mrg_map_max_grid(c->app, c->lds_cap, c->device);
     // (MRG_TEST_MAP_GRID: more workgroups than fit at once, run in waves: an A/B knob for load balance)
@@ -1540,11 +1599,11 @@ void job_map(mrg_ctx *c) {
         if (ocap > 0xFFFFFFF0ull) raise(MRG_ENOMEM, "input too large for one map launch");
         M.ovf = pget<uint64_t>(p, (uint64_t)MRG_NBUCKET * ocap * RW);
         M.onext = pget<uint32_t>(p, MRG_NBUCKET);
-        HIPCHK(hipMemsetAsync(M.onext, 0, 4ull * MRG_NBUCKET, s));
-        h2d(c, M.rbase, rbase.data(), 8ull * MRG_NBUCKET);
-        h2d(c, M.bcap, bcap32.data(), 4ull * MRG_NBUCKET);
-        h2d(c, M.rbase16, rbase16.data(), 8ull * MRG_NBUCKET);
-        h2d(c, M.bcap16, bcap16_32.data(), 4ull * MRG_NBUCKET);
+        stage_fill(c, M.onext, 0, 4ull * MRG_NBUCKET);
+        stage_h2d(c, M.rbase, rbase.data(), 8ull * MRG_NBUCKET);
+        stage_h2d(c, M.bcap, bcap32.data(), 4ull * MRG_NBUCKET);
+        stage_h2d(c, M.rbase16, rbase16.data(), 8ull * MRG_NBUCKET);
+        stage_h2d(c, M.bcap16, bcap16_32.data(), 4ull * MRG_NBUCKET);
         A.in = c->d_in;
         A.doc_off = d_doc_off;
         A.chunk_base = d_cb;
@@ -1593,10 +1652,11 @@ void job_map(mrg_ctx *c) {
             HIPCHK(hipMemsetAsync(M.prof, 0, 8ull * (8 + 8ull * grid), s));
             A.prof = M.prof;
         }
-        HIPCHK(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long) * CNT_N, s));
-        HIPCHK(hipMemsetAsync(&c->d_cnt[CNT_ERRPOS], 0xFF, sizeof(unsigned long long), s));
+        stage_fill(c, c->d_cnt, 0, sizeof(unsigned long long) * CNT_N);
+        stage_fill(c, &c->d_cnt[CNT_ERRPOS], 0xFF, sizeof(unsigned long long));
+        stage_h2d(c, M.dargs, &A, sizeof(MapArgs));
+        flush_stage(c);
         ev_rec(c, 0);
-        h2d(c, M.dargs, &A, sizeof(MapArgs));
         mrg_launch_map(nullptr, M.dargs, c->app, grid, c->lds_cap, s);  // also with no tiles: writes empty flush regions
         ev_rec(c, 1);
         HIPCHK(hipGetLastError());
@@ -2525,6 +2585,7 @@ int mrg_open(int device, mrg_ctx **out) {
         // [CNT_N, CNT_N + 8): scratch; [CNT_N + 8, + MRG_NBUCKET / 2): the map's overflow-list fill (u32)
         HIPCHK(hipHostMalloc(&c->h_cnt, sizeof(unsigned long long) * (CNT_N + 8 + MRG_NBUCKET / 2), hipHostMallocDefault));
         HIPCHK(hipHostMalloc(&c->h_stage, MRG_STAGE_BYTES, hipHostMallocDefault));
+        HIPCHK(hipMalloc(&c->d_stage, MRG_STAGE_BYTES));
         for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
         if (const char *v = getenv("MRG_LDS_CAP")) c->lds_cap = atoi(v);
         *out = c;
@@ -2540,6 +2601,7 @@ int mrg_close(mrg_ctx *c) {
         (void)hipFree(c->d_cnt);
         (void)hipHostFree(c->h_cnt);
         if (c->h_stage) (void)hipHostFree(c->h_stage);
+        if (c->d_stage) (void)hipFree(c->d_stage);
         if (c->own) (void)hipStreamDestroy(c->own);
         delete c;
     });
